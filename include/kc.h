@@ -1,0 +1,193 @@
+/*
+ * kc.h — C ABI of the MI355X-native k-mer counting path (libkc_hip.so).
+ *
+ * This is the drop-in boundary for the reference's device path. The reference
+ * binds exactly three functions from its CUDA translation unit
+ * (GPUHandler.h:61-65), all called from KMerCounter.cpp only:
+ *
+ *   GPUStream** PrepareGPU(uint32_t streamCount, uint64_t inputSize,
+ *                          uint64_t lineLength, int64_t kmerLength);      GPUHandler.h:61
+ *   int64_t     processKMers(GPUStream*, const char* input, int64_t kmerLength,
+ *                            int64_t inputSize, int64_t lineLength,
+ *                            uint32_t readId, FileDump&);                  GPUHandler.h:64
+ *   void        FreeGPU(GPUStream**, uint32_t streamCount);               GPUHandler.h:62
+ *
+ * and then aggregates the returned records on the host in a TBB
+ * concurrent_hash_map (KMerCounter.cpp:61-82) which it dumps at the end
+ * (KMerCounter.cpp:91-106). Here the aggregation lives on the GPU (an
+ * open-addressed table in HBM), so one context replaces a GPUStream pool plus
+ * the host hash:
+ *
+ *   kc_create             replaces PrepareGPU            (GPUHandler.cu:479-509)
+ *   kc_count_chunk        replaces processKMers + the host hash insert of
+ *                         dispatchWork                   (GPUHandler.cu:397-477,
+ *                                                         KMerCounter.cpp:51-89)
+ *   kc_count_fastq        new: raw record-aligned FASTQ block, decoded on the GPU
+ *                         (replaces FASTQFileReader::readData's host concatenation,
+ *                         FASTQFileReader.cpp:49-89, for well-formed 4-line FASTQ)
+ *   kc_finish/kc_write_output
+ *                         replace DumpResults            (KMerCounter.cpp:91-106)
+ *                         and the disabled sorted-spill merge
+ *                         (KMerFileMergeHandler.cpp:49-100) — output is always
+ *                         the SortedKMerFile format (SortedKMerFile.cpp:18-124).
+ *   kc_destroy            replaces FreeGPU               (GPUHandler.cu:511-519)
+ *
+ * Error handling: the reference calls exit() on any CUDA error
+ * (GPUHandler.h:27-34). Every entry point here returns a kc_status instead;
+ * kc_last_error() gives a human-readable message for the last failure on a ctx.
+ *
+ * Threading: a ctx is bound to one HIP device and one HIP stream and is NOT
+ * thread-safe; distinct ctxs (e.g. one per GPU) may be driven concurrently
+ * from separate host threads (the reference drives 8 GPUStreams from 8
+ * threads, KMerCounter.cpp:123-139).
+ *
+ * Record format of every output (SortedKMerFile): no header;
+ * records of W = ceil(k/32) little-endian uint64 key words followed by a
+ * little-endian uint32 count; rs = 8W+4 bytes; strictly ascending by the key
+ * words compared as unsigned integers, word 0 first (KMerFileMerger.cpp:98-108).
+ */
+#ifndef KC_H
+#define KC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KC_ABI_VERSION 1
+#define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
+
+typedef enum kc_status {
+    KC_OK = 0,
+    KC_ERR_ARG = 1,      /* invalid argument: k outside [1,128], L < k, L > 32767, ... */
+    KC_ERR_HIP = 2,      /* a HIP runtime call failed (reference: gpuAssert -> exit) */
+    KC_ERR_NOMEM = 3,    /* device or host allocation failed */
+    KC_ERR_FORMAT = 4,   /* FASTQ block is not 4-line records with L-byte sequences */
+    KC_ERR_IO = 5,       /* file open/read/write failed */
+    KC_ERR_STATE = 6,    /* call not valid in the ctx's current state */
+    KC_ERR_NODEVICE = 7, /* no HIP device / invalid device ordinal */
+    KC_ERR_INTERNAL = 8  /* device-side invariant violated (bug) */
+} kc_status;
+
+typedef struct kc_ctx kc_ctx;
+
+typedef struct kc_config {
+    int32_t device;            /* HIP device ordinal */
+    int32_t reserved0;
+    int64_t kmer_length;       /* k: Options::GetKmerLength (Options.h:31) */
+    int64_t line_length;       /* L: read length (FASTQFileReader.cpp:35) */
+    uint64_t gpu_memory_limit; /* device working-set cap in bytes: hash table +
+                                  spill buffer + staging (Options::GetGpuMemoryLimit,
+                                  main.cpp:28 default 1e8). 0 = 1e8. */
+    uint64_t table_bytes;      /* optional explicit hash-table size; 0 = derive
+                                  from gpu_memory_limit */
+    const char* temp_dir;      /* spill runs are written here as SortedKMerFile
+                                  files (Options::getTempFileLocation); NULL or ""
+                                  keeps spill runs in host memory */
+    uint32_t flags;            /* KC_FLAG_* */
+    uint32_t reserved1;
+} kc_config;
+
+#define KC_FLAG_NONE 0u
+#define KC_FLAG_QUIET 1u /* no progress lines on stderr */
+
+typedef struct kc_stats {
+    uint64_t reads;            /* reads counted so far */
+    uint64_t windows;          /* k-mer windows examined: reads * (L-k+1) */
+    uint64_t valid_kmers;      /* windows without an invalid base (= sum of counts) */
+    uint64_t table_capacity;   /* slots */
+    uint64_t table_used;       /* occupied slots after kc_finish */
+    uint64_t spilled_kmers;    /* k-mers routed to the spill path */
+    uint64_t spill_runs;       /* sorted spill runs produced */
+    uint64_t output_records;   /* distinct keys in the final output */
+    uint64_t insert_launches;  /* count_kmers kernel launches since the last reset */
+    double insert_ms;          /* summed device time of those launches (HIP events) */
+    double decode_ms;          /* FASTQ index + validate kernels */
+    double finish_ms;          /* compact + sort + pack */
+    double last_count_ms;      /* device time of the last kc_count_* call */
+} kc_stats;
+
+/* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". */
+typedef struct kc_synth_spec {
+    uint64_t n_reads;
+    int64_t read_length;   /* L */
+    uint64_t seed;
+    uint64_t genome_length;/* 0 = iid uniform bases; >0 = reads sampled from a
+                              random genome of this many bases */
+    double n_rate;         /* probability that a base is replaced by 'N' */
+    uint64_t first_read;   /* index of the first record to emit (for sharding) */
+} kc_synth_spec;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+kc_status kc_create(kc_ctx** out, const kc_config* cfg);
+void kc_destroy(kc_ctx* ctx);
+const char* kc_strerror(kc_status s);
+const char* kc_last_error(const kc_ctx* ctx);
+int32_t kc_abi_version(void);
+/* Forget every count (table, spill runs, stats); keeps allocations. */
+kc_status kc_reset(kc_ctx* ctx);
+
+/* ---- counting ----------------------------------------------------------- */
+/* Reference-exact chunk: `size` bytes of concatenated L-byte sequences, exactly
+ * what FASTQFileReader::readData hands to processKMers. floor(size/L) reads are
+ * counted; a trailing partial read is ignored (GPUHandler.cu:13-15). `chunk` is
+ * a host pointer owned by the caller and may be reused when the call returns. */
+kc_status kc_count_chunk(kc_ctx* ctx, const char* chunk, int64_t size, int64_t line_length);
+/* Same, `d_chunk` is device memory on the ctx's device. */
+kc_status kc_count_chunk_device(kc_ctx* ctx, const void* d_chunk, int64_t size, int64_t line_length);
+/* Record-aligned block of raw FASTQ text (host memory). Must consist of whole
+ * 4-line records whose sequence line is exactly `line_length` bytes (0 = the
+ * ctx's configured L) and end with '\n'; otherwise returns KC_ERR_FORMAT
+ * without counting anything from the block. *n_reads (may be NULL) receives
+ * the number of records in the block. The sequence lines are exactly the lines
+ * FASTQFileReader::readData concatenates (the line before each '+' line). */
+kc_status kc_count_fastq(kc_ctx* ctx, const char* fastq, uint64_t n_bytes, int64_t line_length, uint64_t* n_reads);
+/* Same, `d_fastq` is device memory on the ctx's device. */
+kc_status kc_count_fastq_device(kc_ctx* ctx, const void* d_fastq, uint64_t n_bytes, int64_t line_length,
+                                uint64_t* n_reads);
+/* Validation only (the GPU index of kc_count_fastq without counting). */
+kc_status kc_check_fastq(kc_ctx* ctx, const char* fastq, uint64_t n_bytes, int64_t line_length, uint64_t* n_reads);
+
+/* ---- results ------------------------------------------------------------ */
+/* Compacts and radix-sorts the hash table on the device. *n_records receives
+ * the number of records of the table run (spill runs not included). After
+ * kc_finish no more counting is allowed until kc_reset. */
+kc_status kc_finish(kc_ctx* ctx, uint64_t* n_records);
+/* Copies the sorted table run as SortedKMerFile bytes (n_records * rs) to host
+ * memory. Valid only when no spill run exists (see kc_stats.spill_runs). */
+kc_status kc_copy_records(kc_ctx* ctx, void* dst, uint64_t dst_bytes);
+/* Device pointer + byte size of the sorted table run as SortedKMerFile bytes
+ * (valid until kc_reset/kc_destroy). */
+kc_status kc_device_records(kc_ctx* ctx, const void** d_records, uint64_t* n_bytes);
+/* Writes the final SortedKMerFile: the table run k-way merged with every spill
+ * run (KMerFileMergeHandler semantics: groups of `merge_fan_in` files merged by
+ * up to `merge_threads` threads, equal keys summed as uint32). The file is
+ * truncated first (the reference appends, KMerFileMerger.cpp:129). */
+kc_status kc_write_output(kc_ctx* ctx, const char* path, uint32_t merge_fan_in, uint32_t merge_threads);
+/* Writes the table run plus spill runs as separate sorted run files
+ * "<prefix>.<i>" and returns how many were written (for multi-GPU merges). */
+kc_status kc_write_runs(kc_ctx* ctx, const char* prefix, uint32_t* n_runs);
+kc_status kc_get_stats(const kc_ctx* ctx, kc_stats* out);
+
+/* ---- host merge of sorted runs (KMerFileMerger / KMerFileMergeHandler) ---- */
+kc_status kc_merge_files(const char* const* inputs, uint32_t n_inputs, const char* output,
+                         int64_t kmer_length, uint32_t merge_fan_in, uint32_t merge_threads);
+
+/* ---- synthetic input (bench/test data; not on the counting path) ---------- */
+uint64_t kc_synth_fastq_bytes(const kc_synth_spec* spec);
+/* Writes the FASTQ text of spec into host memory (dst_bytes >= kc_synth_fastq_bytes). */
+kc_status kc_synth_fastq_host(const kc_synth_spec* spec, char* dst, uint64_t dst_bytes);
+/* Generates the same bytes directly in device memory of the ctx's device;
+ * the buffer is owned by the ctx (freed by kc_synth_free or kc_destroy). */
+kc_status kc_synth_fastq_device(kc_ctx* ctx, const kc_synth_spec* spec, void** d_out, uint64_t* n_bytes);
+kc_status kc_synth_free(kc_ctx* ctx, void* d_buf);
+/* Device->host copy helper for tests (no torch dependency). */
+kc_status kc_copy_to_host(kc_ctx* ctx, void* dst, const void* d_src, uint64_t n_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KC_H */

@@ -1,0 +1,345 @@
+"""kmer-counter_amd — Python mirror of the reference's count-path interface
+over the C ABI of libkc_hip.so (include/kc.h).
+
+The reference's host interface is C++ (Options, KMerCounter, KMerPrinter:
+Options.h:21-57, KMerCounter.h:70-75, KMerPrinter.h); this module mirrors it
+with the same names and argument meanings so tests read like the reference's
+usage, and adds `Context`, a thin wrapper of one device context (kc_ctx).
+
+Nothing here computes k-mers: every count goes through the HIP kernels in
+libkc_hip.so. If the library is missing the import of `lib()` raises — there
+is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+from typing import List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkc_hip.so")
+CLI_PATH = os.path.join(_HERE, "kmer-counter")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kc.h")
+
+KC_OK = 0
+KC_ERR_ARG = 1
+KC_ERR_HIP = 2
+KC_ERR_NOMEM = 3
+KC_ERR_FORMAT = 4
+KC_ERR_IO = 5
+KC_ERR_STATE = 6
+KC_ERR_NODEVICE = 7
+KC_ERR_INTERNAL = 8
+
+
+class KcError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"kc status {status}: {msg}")
+        self.status = status
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("kmer_length", ctypes.c_int64),
+        ("line_length", ctypes.c_int64),
+        ("gpu_memory_limit", ctypes.c_uint64),
+        ("table_bytes", ctypes.c_uint64),
+        ("temp_dir", ctypes.c_char_p),
+        ("flags", ctypes.c_uint32),
+        ("reserved1", ctypes.c_uint32),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("reads", ctypes.c_uint64),
+        ("windows", ctypes.c_uint64),
+        ("valid_kmers", ctypes.c_uint64),
+        ("table_capacity", ctypes.c_uint64),
+        ("table_used", ctypes.c_uint64),
+        ("spilled_kmers", ctypes.c_uint64),
+        ("spill_runs", ctypes.c_uint64),
+        ("output_records", ctypes.c_uint64),
+        ("insert_launches", ctypes.c_uint64),
+        ("insert_ms", ctypes.c_double),
+        ("decode_ms", ctypes.c_double),
+        ("finish_ms", ctypes.c_double),
+        ("last_count_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class _Synth(ctypes.Structure):
+    _fields_ = [
+        ("n_reads", ctypes.c_uint64),
+        ("read_length", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("genome_length", ctypes.c_uint64),
+        ("n_rate", ctypes.c_double),
+        ("first_read", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def header_functions() -> List[str]:
+    """Names of every function declared in include/kc.h."""
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kc_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Loads libkc_hip.so (built in-tree by __graft_entry__.build / make)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `make -C kmer-counter_amd` (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32
+    P = ctypes.POINTER
+    sig = {
+        "kc_create": ([P(vp), P(_Config)], ctypes.c_int),
+        "kc_destroy": ([vp], None),
+        "kc_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "kc_last_error": ([vp], ctypes.c_char_p),
+        "kc_abi_version": ([], ctypes.c_int32),
+        "kc_reset": ([vp], ctypes.c_int),
+        "kc_count_chunk": ([vp, ctypes.c_char_p, i64, i64], ctypes.c_int),
+        "kc_count_chunk_device": ([vp, vp, i64, i64], ctypes.c_int),
+        "kc_count_fastq": ([vp, ctypes.c_char_p, u64, i64, P(u64)], ctypes.c_int),
+        "kc_count_fastq_device": ([vp, vp, u64, i64, P(u64)], ctypes.c_int),
+        "kc_check_fastq": ([vp, ctypes.c_char_p, u64, i64, P(u64)], ctypes.c_int),
+        "kc_finish": ([vp, P(u64)], ctypes.c_int),
+        "kc_copy_records": ([vp, vp, u64], ctypes.c_int),
+        "kc_device_records": ([vp, P(vp), P(u64)], ctypes.c_int),
+        "kc_write_output": ([vp, ctypes.c_char_p, u32, u32], ctypes.c_int),
+        "kc_write_runs": ([vp, ctypes.c_char_p, P(u32)], ctypes.c_int),
+        "kc_get_stats": ([vp, P(Stats)], ctypes.c_int),
+        "kc_merge_files": ([P(ctypes.c_char_p), u32, ctypes.c_char_p, i64, u32, u32], ctypes.c_int),
+        "kc_synth_fastq_bytes": ([P(_Synth)], u64),
+        "kc_synth_fastq_host": ([P(_Synth), vp, u64], ctypes.c_int),
+        "kc_synth_fastq_device": ([vp, P(_Synth), P(vp), P(u64)], ctypes.c_int),
+        "kc_synth_free": ([vp, vp], ctypes.c_int),
+        "kc_copy_to_host": ([vp, vp, vp, u64], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _spec(n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0):
+    return _Synth(n_reads, read_length, seed, genome_length, n_rate, first_read)
+
+
+def synth_fastq(n_reads: int, read_length: int, seed: int, genome_length: int = 0, n_rate: float = 0.0,
+                first_read: int = 0) -> bytes:
+    """Synthetic FASTQ text (SURVEY §8d generator) produced by the library's host generator."""
+    L = lib()
+    sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read)
+    n = L.kc_synth_fastq_bytes(ctypes.byref(sp))
+    buf = ctypes.create_string_buffer(n + 1)
+    st = L.kc_synth_fastq_host(ctypes.byref(sp), buf, n + 1)
+    if st:
+        raise KcError(st, L.kc_strerror(st).decode())
+    return buf.raw[:n]
+
+
+def merge_files(inputs: List[str], output: str, kmer_length: int, fan_in: int = 2, threads: int = 2) -> None:
+    L = lib()
+    arr = (ctypes.c_char_p * max(1, len(inputs)))(*[p.encode() for p in inputs])
+    st = L.kc_merge_files(arr, len(inputs), output.encode(), kmer_length, fan_in, threads)
+    if st:
+        raise KcError(st, L.kc_strerror(st).decode())
+
+
+class Context:
+    """One device context (kc_ctx): the GPU table of one device."""
+
+    def __init__(self, kmer_length: int, line_length: int = 0, device: int = 0,
+                 gpu_memory_limit: int = 100000000, table_bytes: int = 0, temp_dir: Optional[str] = None,
+                 quiet: bool = True):
+        self._L = lib()
+        self.k = kmer_length
+        self.W = (kmer_length + 31) // 32
+        self.rs = 8 * self.W + 4
+        self._tmp = temp_dir.encode() if temp_dir else None
+        cfg = _Config(device, 0, kmer_length, line_length or kmer_length, int(gpu_memory_limit), int(table_bytes),
+                      self._tmp, 1 if quiet else 0, 0)
+        h = ctypes.c_void_p()
+        st = self._L.kc_create(ctypes.byref(h), ctypes.byref(cfg))
+        if st:
+            raise KcError(st, self._L.kc_strerror(st).decode())
+        self._h = h
+
+    def _chk(self, st: int):
+        if st:
+            raise KcError(st, f"{self._L.kc_strerror(st).decode()}: {self._L.kc_last_error(self._h).decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.kc_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        self._chk(self._L.kc_reset(self._h))
+
+    def count_chunk(self, chunk: bytes, line_length: int):
+        self._chk(self._L.kc_count_chunk(self._h, chunk, len(chunk), line_length))
+
+    def count_chunk_device(self, ptr: int, size: int, line_length: int):
+        self._chk(self._L.kc_count_chunk_device(self._h, ctypes.c_void_p(ptr), size, line_length))
+
+    def count_fastq(self, data: bytes, line_length: int = 0) -> int:
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_count_fastq(self._h, data, len(data), line_length, ctypes.byref(n)))
+        return n.value
+
+    def check_fastq(self, data: bytes, line_length: int = 0) -> int:
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_check_fastq(self._h, data, len(data), line_length, ctypes.byref(n)))
+        return n.value
+
+    def count_fastq_device(self, ptr: int, size: int, line_length: int = 0) -> int:
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_count_fastq_device(self._h, ctypes.c_void_p(ptr), size, line_length, ctypes.byref(n)))
+        return n.value
+
+    def synth_device(self, n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0):
+        """Generates synthetic FASTQ directly in device memory; returns (ptr, nbytes)."""
+        sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read)
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_synth_fastq_device(self._h, ctypes.byref(sp), ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
+
+    def free_device(self, ptr: int):
+        self._chk(self._L.kc_synth_free(self._h, ctypes.c_void_p(ptr)))
+
+    def copy_to_host(self, ptr: int, n: int) -> bytes:
+        buf = ctypes.create_string_buffer(max(1, n))
+        self._chk(self._L.kc_copy_to_host(self._h, buf, ctypes.c_void_p(ptr), n))
+        return buf.raw[:n]
+
+    def finish(self) -> int:
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_finish(self._h, ctypes.byref(n)))
+        return n.value
+
+    def records(self) -> bytes:
+        """Sorted table run (SortedKMerFile bytes); requires no spill runs."""
+        n = self.finish()
+        buf = ctypes.create_string_buffer(max(1, n * self.rs))
+        self._chk(self._L.kc_copy_records(self._h, buf, n * self.rs))
+        return buf.raw[: n * self.rs]
+
+    def write_output(self, path: str, fan_in: int = 2, threads: int = 2):
+        self.finish()
+        self._chk(self._L.kc_write_output(self._h, path.encode(), fan_in, threads))
+
+    def write_runs(self, prefix: str) -> List[str]:
+        self.finish()
+        n = ctypes.c_uint32()
+        self._chk(self._L.kc_write_runs(self._h, prefix.encode(), ctypes.byref(n)))
+        return [f"{prefix}.{i}" for i in range(n.value)]
+
+    def output_bytes(self, tmpdir: str) -> bytes:
+        """Final SortedKMerFile bytes (table run merged with spill runs)."""
+        path = os.path.join(tmpdir, f"kc_out_{id(self)}.bin")
+        self.write_output(path)
+        with open(path, "rb") as f:
+            data = f.read()
+        os.unlink(path)
+        return data
+
+    def stats(self) -> dict:
+        s = Stats()
+        self._chk(self._L.kc_get_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+
+class Options:
+    """Mirror of the reference's Options (Options.h:21-57) with the defaults
+    main.cpp:27-30 installs over Options() (Options.cpp:16-22)."""
+
+    def __init__(self):
+        self._inputFileDirectory = "/home/jayangad/data/1"
+        self._gpuMemoryLimit = 100000000
+        self._kmerLength = 32
+        self._tempFileLocation = "/tmp/1"
+        self._outputFile = "/tmp/2/output.bin"
+        self._noOfMergersAtOnce = 2
+        self._noOfMergeThreads = 2
+
+    def SetInputFileDirectory(self, d): self._inputFileDirectory = d
+    def GetInputFileDirectory(self): return self._inputFileDirectory
+    def SetGpuMemoryLimit(self, v): self._gpuMemoryLimit = int(v)
+    def GetGpuMemoryLimit(self): return self._gpuMemoryLimit
+    def SetKmerLength(self, v): self._kmerLength = int(v)
+    def GetKmerLength(self): return self._kmerLength
+    def setOutputFile(self, v): self._outputFile = v
+    def getOutputFile(self): return self._outputFile
+    def setTempFileLocation(self, v): self._tempFileLocation = v
+    def getTempFileLocation(self): return self._tempFileLocation
+    def setNoOfMergersAtOnce(self, v): self._noOfMergersAtOnce = int(v)
+    def getNoOfMergersAtOnce(self): return self._noOfMergersAtOnce
+    def setNoOfMergeThreads(self, v): self._noOfMergeThreads = int(v)
+    def getNoOfMergeThreads(self): return self._noOfMergeThreads
+
+    def argv(self) -> List[str]:
+        return [f"kmerLength={self._kmerLength}", f"gpuMemoryLimit={self._gpuMemoryLimit}",
+                f"inputFileLocation={self._inputFileDirectory}", f"tempFileLocation={self._tempFileLocation}",
+                f"outputFile={self._outputFile}", f"noOfMergersAtOnce={self._noOfMergersAtOnce}",
+                f"noOfMergeThreads={self._noOfMergeThreads}"]
+
+
+class KMerCounter:
+    """Mirror of KMerCounter (KMerCounter.h:70-75): Start() counts every file of
+    the input directory and writes the SortedKMerFile output, by running the
+    native `kmer-counter` CLI (same key=value arguments)."""
+
+    def __init__(self, options: Options, extra_args: Optional[List[str]] = None):
+        self._options = options
+        self._extra = list(extra_args or [])
+
+    def Start(self) -> subprocess.CompletedProcess:
+        if not os.path.exists(CLI_PATH):
+            raise ImportError(f"{CLI_PATH} is missing: run `make -C kmer-counter_amd`")
+        r = subprocess.run([CLI_PATH] + self._options.argv() + self._extra, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise KcError(KC_ERR_INTERNAL, r.stderr.strip())
+        return r
+
+
+class KMerPrinter:
+    """Mirror of KMerPrinter (KMerPrinter.h): `kmer-counter print in out k`."""
+
+    def __init__(self, inputFilename: str, outputFilename: str, kmerlength: int):
+        self._args = [inputFilename, outputFilename, str(kmerlength)]
+
+    def print(self) -> str:
+        r = subprocess.run([CLI_PATH, "print"] + self._args, capture_output=True, text=True, check=True)
+        return r.stdout

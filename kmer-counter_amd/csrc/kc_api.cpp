@@ -1,0 +1,746 @@
+// kc_api.cpp — the C ABI of include/kc.h: device context, buffers, the count
+// pipeline (FASTQ index -> count_kmers -> spill runs) and the finish pipeline
+// (compact -> radix sort -> pack -> merge with spill runs).
+//
+// Replaces PrepareGPU / processKMers / FreeGPU (GPUHandler.cu:397-519) and the
+// host aggregation of KMerCounter (KMerCounter.cpp:51-106).
+#include <hip/hip_runtime_api.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <string>
+#include <vector>
+
+#include "../../include/kc.h"
+#include "kc_device.h"
+#include "kc_io.h"
+
+using namespace kc;
+
+namespace {
+
+std::atomic<uint64_t> g_ctx_seq(0);
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct HostRun {
+    std::vector<uint8_t> mem;  // used when no temp dir
+    std::string path;          // used with a temp dir
+    uint64_t records = 0;
+};
+
+}  // namespace
+
+struct kc_ctx {
+    kc_config cfg;
+    std::string temp_dir;
+    int W = 1, rs = 12;
+    int64_t k = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint64_t id = 0;
+
+    // table + spill (the gpu_memory_limit working set)
+    uint64_t* table = nullptr;
+    uint64_t cap = 0;
+    size_t table_bytes = 0;
+    uint64_t* spill = nullptr;
+    uint64_t spill_cap = 0;
+    uint64_t* stats = nullptr;      // device ST_N
+    uint64_t* stats_h = nullptr;    // pinned host mirror
+
+    // scratch (grown on demand)
+    DevBuf in_stage;        // host-pointer inputs
+    DevBuf fq_counts, fq_base, fq_tmp, seq_off, seq_end;
+    DevBuf spill_keys2, rle_flags, rle_pos, rle_head, rle_tmp, run_keys, run_cnts, run_packed;
+    DevBuf fin_keys[2], fin_cnts[2], fin_hist, fin_packed, fin_misc;
+
+    // results
+    bool finished = false;
+    uint64_t n_records = 0;  // table run
+    uint64_t spilled_flushed = 0;
+    std::vector<HostRun> runs;
+
+    kc_stats st;
+    std::string err;
+};
+
+static kc_status fail(kc_ctx* c, kc_status s, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return s;
+}
+
+#define HIPCHK(ctx, expr)                                                                                    \
+    do {                                                                                                     \
+        hipError_t e_ = (expr);                                                                              \
+        if (e_ != hipSuccess)                                                                                \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? KC_ERR_NOMEM : KC_ERR_HIP, "%s: %s (%s:%d)", #expr, \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                                          \
+    } while (0)
+
+static kc_status ensure(kc_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return KC_OK;
+    if (b.p) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    size_t want = bytes < 256 ? 256 : bytes;
+    HIPCHK(c, hipMalloc(&b.p, want));
+    b.bytes = want;
+    return KC_OK;
+}
+
+static void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+static kc_status sync_stats(kc_ctx* c) {
+    HIPCHK(c, hipMemcpyAsync(c->stats_h, c->stats, ST_N * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KC_OK;
+}
+
+static uint32_t probe_limit(const kc_ctx* c) {
+    // a nearly full table: give up early and spill instead of walking long runs
+    uint64_t used = c->stats_h[ST_CLAIMED];
+    if (used * 10 >= c->cap * 9) return 8;
+    return c->W == 1 ? 128 : 64;
+}
+
+// ---------------------------------------------------------------------------
+// sorting helpers (device)
+// ---------------------------------------------------------------------------
+
+// Sorts n SoA records (keys at `stride`) in place-or-swap; returns which buffer
+// holds the result (0 = a, 1 = b).
+static kc_status sort_records(kc_ctx* c, uint64_t* ka, uint64_t* kb, uint32_t* va, uint32_t* vb, uint64_t stride,
+                              uint64_t n, int* which) {
+    *which = 0;
+    if (n <= 1) return KC_OK;
+    const int W = c->W;
+    kc_status s = ensure(c, c->fin_misc, 2 * W * 8);
+    if (s) return s;
+    std::vector<uint64_t> init(2 * W);
+    for (int j = 0; j < W; j++) {
+        init[j] = 0;
+        init[W + j] = ~0ull;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->fin_misc.p, init.data(), 2 * W * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_key_bits(W, ka, stride, n, (uint64_t*)c->fin_misc.p, c->stream));
+    std::vector<uint64_t> bits(2 * W);
+    HIPCHK(c, hipMemcpyAsync(bits.data(), c->fin_misc.p, 2 * W * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int grid = sort_grid(n);
+    s = ensure(c, c->fin_hist, (size_t)256 * grid * 4);
+    if (s) return s;
+    uint64_t* kin = ka;
+    uint64_t* kout = kb;
+    uint32_t* vin = va;
+    uint32_t* vout = vb;
+    int cur = 0;
+    for (int word = W - 1; word >= 0; word--) {
+        uint64_t vary = bits[word] ^ bits[W + word];
+        for (int shift = 0; shift < 64; shift += 8) {
+            if (((vary >> shift) & 255u) == 0) continue;
+            HIPCHK(c, launch_sort_pass(W, kin, kout, vin, vout, stride, n, word, shift, (uint32_t*)c->fin_hist.p,
+                                       grid, c->stream));
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+            cur ^= 1;
+        }
+    }
+    *which = cur;
+    return KC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// spill runs: sort the spill buffer, run-length reduce, pack, move to host
+// ---------------------------------------------------------------------------
+
+static kc_status flush_spill(kc_ctx* c) {
+    kc_status s = sync_stats(c);
+    if (s) return s;
+    uint64_t n = c->stats_h[ST_SPILL_FILL];
+    if (n == 0) return KC_OK;
+    if (n > c->spill_cap) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow (%llu > %llu)",
+                                      (unsigned long long)n, (unsigned long long)c->spill_cap);
+    const int W = c->W;
+    uint64_t stride = c->spill_cap;
+    if ((s = ensure(c, c->spill_keys2, (size_t)W * stride * 8))) return s;
+    int which = 0;
+    if ((s = sort_records(c, c->spill, (uint64_t*)c->spill_keys2.p, nullptr, nullptr, stride, n, &which))) return s;
+    uint64_t* sorted = which ? (uint64_t*)c->spill_keys2.p : c->spill;
+    if ((s = ensure(c, c->rle_flags, n * 4)) || (s = ensure(c, c->rle_pos, n * 4)) ||
+        (s = ensure(c, c->rle_head, n * 4)) || (s = ensure(c, c->rle_tmp, scan_tmp_elems(n) * 4)) ||
+        (s = ensure(c, c->run_keys, (size_t)W * n * 8)) || (s = ensure(c, c->run_cnts, n * 4)))
+        return s;
+    HIPCHK(c, launch_rle_heads(W, sorted, stride, n, (uint32_t*)c->rle_flags.p, c->stream));
+    HIPCHK(c, launch_scan_u32((uint32_t*)c->rle_flags.p, (uint32_t*)c->rle_pos.p, n, (uint32_t*)c->rle_tmp.p,
+                              c->stream));
+    uint32_t last[2];
+    HIPCHK(c, hipMemcpyAsync(&last[0], (uint32_t*)c->rle_pos.p + (n - 1), 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&last[1], (uint32_t*)c->rle_flags.p + (n - 1), 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t m = (uint64_t)last[0] + last[1];
+    HIPCHK(c, launch_rle_scatter(W, sorted, stride, n, (uint32_t*)c->rle_flags.p, (uint32_t*)c->rle_pos.p,
+                                 (uint64_t*)c->run_keys.p, n, (uint32_t*)c->rle_head.p, c->stream));
+    HIPCHK(c, launch_rle_counts((uint32_t*)c->rle_head.p, m, n, (uint32_t*)c->run_cnts.p, c->stream));
+    size_t bytes = (size_t)m * c->rs;
+    if ((s = ensure(c, c->run_packed, bytes))) return s;
+    HIPCHK(c, launch_pack(W, (uint64_t*)c->run_keys.p, n, (uint32_t*)c->run_cnts.p, m, c->run_packed.p, c->stream));
+    HostRun run;
+    run.records = m;
+    run.mem.resize(bytes);
+    HIPCHK(c, hipMemcpyAsync(run.mem.data(), c->run_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->stats + ST_SPILL_FILL, 0, 8, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stats_h[ST_SPILL_FILL] = 0;
+    c->spilled_flushed += n;
+    if (!c->temp_dir.empty()) {
+        char name[128];
+        snprintf(name, sizeof(name), "/kc.%d.%llu.%zu", (int)getpid(), (unsigned long long)c->id, c->runs.size());
+        run.path = c->temp_dir + name;
+        FILE* f = fopen(run.path.c_str(), "wb");
+        if (!f) return fail(c, KC_ERR_IO, "cannot create spill run %s", run.path.c_str());
+        size_t w = fwrite(run.mem.data(), 1, bytes, f);
+        fclose(f);
+        if (w != bytes) return fail(c, KC_ERR_IO, "short write to spill run %s", run.path.c_str());
+        std::vector<uint8_t>().swap(run.mem);
+    }
+    c->runs.push_back(std::move(run));
+    c->st.spill_runs = c->runs.size();
+    return KC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// counting
+// ---------------------------------------------------------------------------
+
+static kc_status check_line(kc_ctx* c, int64_t L) {
+    if (L < c->k) return fail(c, KC_ERR_ARG, "read length %lld is shorter than k=%lld", (long long)L, (long long)c->k);
+    if (L > 32767) return fail(c, KC_ERR_ARG, "read length %lld exceeds 32767 (the reference's u16 2L header)",
+                               (long long)L);
+    return KC_OK;
+}
+
+// Counts n_reads reads (stride mode when seq_off == nullptr).
+static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
+    if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
+    const uint64_t nw = (uint64_t)(L - c->k + 1);
+    const uint64_t max_reads = c->spill_cap / nw;
+    if (max_reads == 0) return fail(c, KC_ERR_ARG, "gpu_memory_limit too small for one read's windows");
+    uint64_t done = 0;
+    kc_status s;
+    float ms = 0.f;
+    while (done < n_reads) {
+        uint64_t free_slots = c->spill_cap - c->stats_h[ST_SPILL_FILL];
+        uint64_t nr = n_reads - done;
+        if (nr > max_reads) nr = max_reads;
+        if (nr * nw > free_slots) {
+            if ((s = flush_spill(c))) return s;
+        }
+        CountLaunch a;
+        a.base = base;
+        a.seq_off = seq_off;
+        a.read0 = done;
+        a.n_reads = nr;
+        a.L = (int)L;
+        a.k = (int)c->k;
+        a.table = c->table;
+        a.cap = c->cap;
+        a.spill = c->spill;
+        a.spill_cap = c->spill_cap;
+        a.stats = c->stats;
+        a.probe_limit = probe_limit(c);
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_count_kmers(a, 256 * 16, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        if ((s = sync_stats(c))) return s;
+        float t = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+        ms += t;
+        c->st.insert_launches++;
+        if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
+        done += nr;
+    }
+    c->st.insert_ms += ms;
+    c->st.last_count_ms = ms;
+    c->st.reads += n_reads;
+    c->st.windows += n_reads * nw;
+    c->st.valid_kmers = c->stats_h[ST_VALID];
+    c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
+    return KC_OK;
+}
+
+static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out) {
+    kc_status s;
+    uint64_t nch = fq_chunks(base, n);
+    if ((s = ensure(c, c->fq_counts, nch * 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
+        (s = ensure(c, c->fq_tmp, scan_tmp_elems(nch) * 8)))
+        return s;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
+    HIPCHK(c, launch_fq_count(base, n, (uint64_t*)c->fq_counts.p, c->stream));
+    HIPCHK(c, launch_scan_u64((uint64_t*)c->fq_counts.p, (uint64_t*)c->fq_base.p, nch, (uint64_t*)c->fq_tmp.p,
+                              c->stream));
+    uint64_t tail[2];
+    HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->fq_base.p + nch - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->fq_counts.p + nch - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t lines = tail[0] + tail[1];
+    if (lines % 4 != 0)
+        return fail(c, KC_ERR_FORMAT, "FASTQ block has %llu lines, not a multiple of 4", (unsigned long long)lines);
+    uint64_t n_rec = lines / 4;
+    if ((s = ensure(c, c->seq_off, n_rec * 8 + 8)) || (s = ensure(c, c->seq_end, n_rec * 8 + 8))) return s;
+    HIPCHK(c, launch_fq_emit(base, n, (uint64_t*)c->fq_base.p, (uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p,
+                             n_rec, c->stats, c->stream));
+    HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
+                                 c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if ((s = sync_stats(c))) return s;
+    float t = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    c->st.decode_ms += t;
+    uint64_t e = c->stats_h[ST_ERR];
+    if (e) {
+        std::string why;
+        if (e & ERR_FQ_NOT_AT) why += " record-does-not-start-with-@";
+        if (e & ERR_FQ_NO_PLUS) why += " no-+-line-after-sequence";
+        if (e & ERR_FQ_SEQ_LEN) why += " sequence-length-differs-from-L";
+        if (e & ERR_FQ_TOO_MANY) why += " index-overflow";
+        if (e & ERR_FQ_NO_FINAL_NL) why += " block-does-not-end-with-newline";
+        HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
+        c->stats_h[ST_ERR] = 0;
+        return fail(c, KC_ERR_FORMAT, "FASTQ block is not 4-line records with %lld-base reads:%s", (long long)L,
+                    why.c_str());
+    }
+    *n_rec_out = n_rec;
+    return KC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+int32_t kc_abi_version(void) { return KC_ABI_VERSION; }
+
+const char* kc_strerror(kc_status s) {
+    switch (s) {
+    case KC_OK: return "ok";
+    case KC_ERR_ARG: return "invalid argument";
+    case KC_ERR_HIP: return "HIP runtime error";
+    case KC_ERR_NOMEM: return "out of memory";
+    case KC_ERR_FORMAT: return "malformed FASTQ block";
+    case KC_ERR_IO: return "I/O error";
+    case KC_ERR_STATE: return "invalid call for the context state";
+    case KC_ERR_NODEVICE: return "no HIP device";
+    case KC_ERR_INTERNAL: return "internal error";
+    }
+    return "unknown status";
+}
+
+const char* kc_last_error(const kc_ctx* c) { return c ? c->err.c_str() : ""; }
+
+kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
+    if (!out || !cfg) return KC_ERR_ARG;
+    *out = nullptr;
+    if (cfg->kmer_length < 1 || cfg->kmer_length > KC_MAX_K) return KC_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KC_ERR_NODEVICE;
+    if (cfg->device < 0 || cfg->device >= ndev) return KC_ERR_NODEVICE;
+    kc_ctx* c = new kc_ctx();
+    c->cfg = *cfg;
+    c->temp_dir = (cfg->temp_dir && cfg->temp_dir[0]) ? cfg->temp_dir : "";
+    c->cfg.temp_dir = nullptr;
+    c->k = cfg->kmer_length;
+    c->W = (int)((c->k + 31) / 32);
+    c->rs = 8 * c->W + 4;
+    c->id = g_ctx_seq.fetch_add(1);
+    memset(&c->st, 0, sizeof(c->st));
+    kc_status s = KC_OK;
+    auto bail = [&](kc_status e) {
+        kc_destroy(c);
+        return e;
+    };
+    if (hipSetDevice(cfg->device) != hipSuccess) return bail(KC_ERR_NODEVICE);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(KC_ERR_HIP);
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(KC_ERR_HIP);
+    uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
+    if (M < (1u << 20)) M = 1u << 20;
+    size_t slot_bytes = 8 * (size_t)slot_words(c->W);
+    size_t spill_bytes = M / 16;
+    size_t tbytes = cfg->table_bytes ? cfg->table_bytes : (M - 4 * spill_bytes);
+    c->spill_cap = spill_bytes / (8 * c->W);
+    if (c->spill_cap < 4096) c->spill_cap = 4096;
+    c->cap = tbytes / slot_bytes;
+    if (c->cap < 1024) c->cap = 1024;
+    c->table_bytes = c->cap * slot_bytes;
+    if (hipMalloc((void**)&c->table, c->table_bytes) != hipSuccess) return bail(KC_ERR_NOMEM);
+    if (hipMalloc((void**)&c->spill, (size_t)c->spill_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
+    if (hipMalloc((void**)&c->stats, ST_N * 8) != hipSuccess) return bail(KC_ERR_NOMEM);
+    if (hipHostMalloc((void**)&c->stats_h, ST_N * 8, 0) != hipSuccess) return bail(KC_ERR_NOMEM);
+    s = kc_reset(c);
+    if (s) return bail(s);
+    *out = c;
+    return KC_OK;
+}
+
+void kc_destroy(kc_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& r : c->runs)
+        if (!r.path.empty()) unlink(r.path.c_str());
+    DevBuf* bufs[] = {&c->in_stage, &c->fq_counts, &c->fq_base, &c->fq_tmp, &c->seq_off, &c->seq_end,
+                      &c->spill_keys2, &c->rle_flags, &c->rle_pos, &c->rle_head, &c->rle_tmp, &c->run_keys,
+                      &c->run_cnts, &c->run_packed, &c->fin_keys[0], &c->fin_keys[1], &c->fin_cnts[0],
+                      &c->fin_cnts[1], &c->fin_hist, &c->fin_packed, &c->fin_misc};
+    for (DevBuf* b : bufs) release(*b);
+    if (c->table) (void)hipFree(c->table);
+    if (c->spill) (void)hipFree(c->spill);
+    if (c->stats) (void)hipFree(c->stats);
+    if (c->stats_h) (void)hipHostFree(c->stats_h);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+kc_status kc_reset(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->stats, 0, ST_N * 8, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    memset(c->stats_h, 0, ST_N * 8);
+    for (auto& r : c->runs)
+        if (!r.path.empty()) unlink(r.path.c_str());
+    c->runs.clear();
+    c->spilled_flushed = 0;
+    c->finished = false;
+    c->n_records = 0;
+    memset(&c->st, 0, sizeof(c->st));
+    c->st.table_capacity = c->cap;
+    return KC_OK;
+}
+
+kc_status kc_count_chunk_device(kc_ctx* c, const void* d_chunk, int64_t size, int64_t L) {
+    if (!c || (!d_chunk && size > 0) || size < 0) return KC_ERR_ARG;
+    kc_status s = check_line(c, L);
+    if (s) return s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    uint64_t n = (uint64_t)(size / L);
+    if (n == 0) return KC_OK;
+    return count_reads(c, (const uint8_t*)d_chunk, nullptr, n, L);
+}
+
+kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) {
+    if (!c || (!chunk && size > 0) || size < 0) return KC_ERR_ARG;
+    kc_status s = check_line(c, L);
+    if (s) return s;
+    if (size / L == 0) return KC_OK;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if ((s = ensure(c, c->in_stage, (size_t)size + 64))) return s;
+    HIPCHK(c, hipMemcpyAsync(c->in_stage.p, chunk, (size_t)size, hipMemcpyHostToDevice, c->stream));
+    return count_reads(c, (const uint8_t*)c->in_stage.p, nullptr, (uint64_t)(size / L), L);
+}
+
+static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_t L, uint64_t* n_reads,
+                              bool count) {
+    if (!c || (!d_fastq && n > 0)) return KC_ERR_ARG;
+    if (n_reads) *n_reads = 0;
+    if (n == 0) return KC_OK;
+    if (count && c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
+    if (L == 0) L = c->cfg.line_length;
+    kc_status s = check_line(c, L);
+    if (s) return s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    uint64_t n_rec = 0;
+    if ((s = index_fastq(c, (const uint8_t*)d_fastq, n, L, &n_rec))) return s;
+    if (count && (s = count_reads(c, (const uint8_t*)d_fastq, (const uint64_t*)c->seq_off.p, n_rec, L))) return s;
+    if (n_reads) *n_reads = n_rec;
+    return KC_OK;
+}
+
+static kc_status fastq_host(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, uint64_t* n_reads, bool count) {
+    if (!c || (!fastq && n > 0)) return KC_ERR_ARG;
+    if (n_reads) *n_reads = 0;
+    if (n == 0) return KC_OK;
+    kc_status s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if ((s = ensure(c, c->in_stage, (size_t)n + 64))) return s;
+    HIPCHK(c, hipMemcpyAsync(c->in_stage.p, fastq, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    return fastq_device(c, c->in_stage.p, n, L, n_reads, count);
+}
+
+kc_status kc_count_fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_t L, uint64_t* n_reads) {
+    return fastq_device(c, d_fastq, n, L, n_reads, true);
+}
+
+kc_status kc_count_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, uint64_t* n_reads) {
+    return fastq_host(c, fastq, n, L, n_reads, true);
+}
+
+kc_status kc_check_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, uint64_t* n_reads) {
+    return fastq_host(c, fastq, n, L, n_reads, false);
+}
+
+kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
+    if (!c) return KC_ERR_ARG;
+    if (c->finished) {
+        if (n_records) *n_records = c->n_records;
+        return KC_OK;
+    }
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    kc_status s;
+    if ((s = sync_stats(c))) return s;
+    if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;
+    const int W = c->W;
+    uint64_t out_cap = c->stats_h[ST_CLAIMED] + 1;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    for (int i = 0; i < 2; i++) {
+        if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
+            return s;
+    }
+    if ((s = ensure(c, c->fin_misc, 2 * W * 8 + 8))) return s;
+    uint64_t* cursor = (uint64_t*)c->fin_misc.p + 2 * W;
+    HIPCHK(c, hipMemsetAsync(cursor, 0, 8, c->stream));
+    HIPCHK(c, launch_compact(W, c->table, c->cap, (uint64_t*)c->fin_keys[0].p, (uint32_t*)c->fin_cnts[0].p, out_cap,
+                             cursor, c->stream));
+    HIPCHK(c, launch_append_key0(W, (uint64_t*)c->fin_keys[0].p, (uint32_t*)c->fin_cnts[0].p, out_cap, cursor,
+                                 c->stats, c->stream));
+    uint64_t n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, cursor, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (n > out_cap) return fail(c, KC_ERR_INTERNAL, "compaction found %llu records, expected <= %llu",
+                                 (unsigned long long)n, (unsigned long long)out_cap);
+    int which = 0;
+    // note: sort_records re-uses fin_misc for the key bits (cursor already read)
+    if ((s = sort_records(c, (uint64_t*)c->fin_keys[0].p, (uint64_t*)c->fin_keys[1].p, (uint32_t*)c->fin_cnts[0].p,
+                          (uint32_t*)c->fin_cnts[1].p, out_cap, n, &which)))
+        return s;
+    if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
+    HIPCHK(c, launch_pack(W, (uint64_t*)c->fin_keys[which].p, out_cap, (uint32_t*)c->fin_cnts[which].p, n,
+                          c->fin_packed.p, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    c->st.finish_ms += t;
+    c->n_records = n;
+    c->finished = true;
+    c->st.table_used = c->stats_h[ST_CLAIMED];
+    c->st.output_records = n;
+    if (n_records) *n_records = n;
+    return KC_OK;
+}
+
+kc_status kc_copy_records(kc_ctx* c, void* dst, uint64_t dst_bytes) {
+    if (!c || !dst) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist: use kc_write_output");
+    uint64_t bytes = c->n_records * c->rs;
+    if (dst_bytes < bytes) return fail(c, KC_ERR_ARG, "destination holds %llu bytes, need %llu",
+                                       (unsigned long long)dst_bytes, (unsigned long long)bytes);
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (bytes) {
+        HIPCHK(c, hipMemcpyAsync(dst, c->fin_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return KC_OK;
+}
+
+kc_status kc_device_records(kc_ctx* c, const void** d_records, uint64_t* n_bytes) {
+    if (!c || !d_records || !n_bytes) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    *d_records = c->fin_packed.p;
+    *n_bytes = c->n_records * c->rs;
+    return KC_OK;
+}
+
+static kc_status table_run_to_host(kc_ctx* c, std::vector<uint8_t>* mem) {
+    uint64_t bytes = c->n_records * c->rs;
+    mem->resize(bytes);
+    if (bytes) {
+        HIPCHK(c, hipSetDevice(c->cfg.device));
+        HIPCHK(c, hipMemcpyAsync(mem->data(), c->fin_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return KC_OK;
+}
+
+kc_status kc_write_output(kc_ctx* c, const char* path, uint32_t fan_in, uint32_t threads) {
+    if (!c || !path) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    std::vector<uint8_t> table_run;
+    kc_status s = table_run_to_host(c, &table_run);
+    if (s) return s;
+    if (c->runs.empty()) {
+        FILE* f = fopen(path, "wb");
+        if (!f) return fail(c, KC_ERR_IO, "cannot open output file %s", path);
+        size_t w = table_run.empty() ? 0 : fwrite(table_run.data(), 1, table_run.size(), f);
+        int e = fclose(f);
+        if (w != table_run.size() || e != 0) return fail(c, KC_ERR_IO, "short write to %s", path);
+        return KC_OK;
+    }
+    std::vector<RunSource> src;
+    RunSource t;
+    t.mem = table_run.data();
+    t.bytes = table_run.size();
+    src.push_back(t);
+    for (auto& r : c->runs) {
+        RunSource x;
+        if (!r.path.empty())
+            x.path = r.path;
+        else {
+            x.mem = r.mem.data();
+            x.bytes = r.mem.size();
+        }
+        src.push_back(x);
+    }
+    std::string err;
+    std::string tmp_prefix = std::string(path) + ".kctmp";
+    if (!merge_tree(src, path, c->W, fan_in, threads, tmp_prefix, &err))
+        return fail(c, KC_ERR_IO, "%s", err.c_str());
+    return KC_OK;
+}
+
+kc_status kc_write_runs(kc_ctx* c, const char* prefix, uint32_t* n_runs) {
+    if (!c || !prefix) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    std::vector<uint8_t> table_run;
+    kc_status s = table_run_to_host(c, &table_run);
+    if (s) return s;
+    uint32_t count = 0;
+    auto write_one = [&](const uint8_t* p, size_t bytes, const std::string& from) -> kc_status {
+        std::string name = std::string(prefix) + "." + std::to_string(count);
+        if (!from.empty()) {
+            // copy the temp file
+            FILE* in = fopen(from.c_str(), "rb");
+            FILE* out = fopen(name.c_str(), "wb");
+            if (!in || !out) {
+                if (in) fclose(in);
+                if (out) fclose(out);
+                return fail(c, KC_ERR_IO, "cannot copy run %s", from.c_str());
+            }
+            std::vector<char> buf(1 << 20);
+            size_t got;
+            while ((got = fread(buf.data(), 1, buf.size(), in)) > 0) fwrite(buf.data(), 1, got, out);
+            fclose(in);
+            fclose(out);
+        } else {
+            FILE* out = fopen(name.c_str(), "wb");
+            if (!out) return fail(c, KC_ERR_IO, "cannot write run %s", name.c_str());
+            size_t w = bytes ? fwrite(p, 1, bytes, out) : 0;
+            fclose(out);
+            if (w != bytes) return fail(c, KC_ERR_IO, "short write %s", name.c_str());
+        }
+        count++;
+        return KC_OK;
+    };
+    if ((s = write_one(table_run.data(), table_run.size(), ""))) return s;
+    for (auto& r : c->runs)
+        if ((s = write_one(r.mem.data(), r.mem.size(), r.path))) return s;
+    if (n_runs) *n_runs = count;
+    return KC_OK;
+}
+
+kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
+    if (!c || !out) return KC_ERR_ARG;
+    *out = c->st;
+    out->table_capacity = c->cap;
+    out->valid_kmers = c->stats_h[ST_VALID];
+    out->spill_runs = c->runs.size();
+    return KC_OK;
+}
+
+kc_status kc_merge_files(const char* const* inputs, uint32_t n_inputs, const char* output, int64_t kmer_length,
+                         uint32_t fan_in, uint32_t threads) {
+    if (!output || kmer_length < 1 || kmer_length > KC_MAX_K || (n_inputs && !inputs)) return KC_ERR_ARG;
+    int W = (int)((kmer_length + 31) / 32);
+    std::vector<RunSource> src;
+    for (uint32_t i = 0; i < n_inputs; i++) {
+        RunSource r;
+        r.path = inputs[i];
+        src.push_back(r);
+    }
+    std::string err;
+    if (!merge_tree(src, output, W, fan_in, threads, std::string(output) + ".kctmp", &err)) return KC_ERR_IO;
+    return KC_OK;
+}
+
+uint64_t kc_synth_fastq_bytes(const kc_synth_spec* sp) {
+    if (!sp) return 0;
+    return synth_bytes(sp->first_read, sp->n_reads, sp->read_length);
+}
+
+static SynthArgs synth_args(const kc_synth_spec* sp) {
+    SynthArgs a;
+    a.first = sp->first_read;
+    a.n = sp->n_reads;
+    a.seed = sp->seed;
+    a.genome = sp->genome_length;
+    a.L = sp->read_length;
+    double thr = sp->n_rate * 9007199254740992.0;
+    a.n_threshold = sp->n_rate <= 0 ? 0 : (thr >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)thr);
+    return a;
+}
+
+static bool synth_ok(const kc_synth_spec* sp) {
+    return sp && sp->read_length > 0 && (sp->genome_length == 0 || sp->genome_length >= (uint64_t)sp->read_length);
+}
+
+kc_status kc_synth_fastq_host(const kc_synth_spec* sp, char* dst, uint64_t dst_bytes) {
+    if (!synth_ok(sp) || !dst) return KC_ERR_ARG;
+    if (dst_bytes < kc_synth_fastq_bytes(sp)) return KC_ERR_ARG;
+    synth_host(synth_args(sp), dst);
+    return KC_OK;
+}
+
+kc_status kc_synth_fastq_device(kc_ctx* c, const kc_synth_spec* sp, void** d_out, uint64_t* n_bytes) {
+    if (!c || !synth_ok(sp) || !d_out) return KC_ERR_ARG;
+    uint64_t bytes = kc_synth_fastq_bytes(sp);
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    void* p = nullptr;
+    HIPCHK(c, hipMalloc(&p, bytes + 64));
+    HIPCHK(c, launch_synth(synth_args(sp), (char*)p, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *d_out = p;
+    if (n_bytes) *n_bytes = bytes;
+    return KC_OK;
+}
+
+kc_status kc_synth_free(kc_ctx* c, void* d_buf) {
+    if (!c) return KC_ERR_ARG;
+    if (d_buf) HIPCHK(c, hipFree(d_buf));
+    return KC_OK;
+}
+
+kc_status kc_copy_to_host(kc_ctx* c, void* dst, const void* d_src, uint64_t n) {
+    if (!c || (n && (!dst || !d_src))) return KC_ERR_ARG;
+    if (n == 0) return KC_OK;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipMemcpyAsync(dst, d_src, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,430 @@
+// kc_cli.cpp — the `kmer-counter` command line, a drop-in for the reference's
+// main.cpp / Options / KMerCounter::Start / KMerPrinter.
+//
+//   kmer-counter kmerLength=31 inputFileLocation=DIR outputFile=FILE [key=value...]
+//   kmer-counter print <in> <out-ignored> <k>
+//
+// Keys and defaults follow getOptions (main.cpp:25-70) and Options()
+// (Options.cpp:16-22): every argv (argv[0] included) is prefix-matched, unknown
+// keys are ignored, the last occurrence wins. Additive keys (not in the
+// reference): gpus=N, inputMode=auto|fastq|exact, tableBytes=B, quiet=1.
+//
+// Input (InputFileHandler.cpp:22-47): every directory entry whose name does
+// not start with '.', in readdir order; L of a file = length of its line 2
+// (FASTQFileReader.cpp:31-35).
+//   inputMode=fastq : the file goes to the GPU as raw FASTQ blocks
+//                     (kc_count_fastq); it must be 4-line records of L bases.
+//   inputMode=exact : the host rebuilds the reference's chunks exactly
+//                     (FASTQFileReader::readData with the chunk size of
+//                     KMerCounter::GetChunkSize) and sends them with
+//                     kc_count_chunk — bit-exact even on malformed input.
+//   inputMode=auto  : fastq when every block of the file validates, else exact.
+// Output: the SortedKMerFile (sorted, deduplicated records), see include/kc.h.
+#include <dirent.h>
+#include <fcntl.h>
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <fstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kc.h"
+
+namespace {
+
+struct Options {
+    // main.cpp:27-30 overrides of the Options() constructor defaults (Options.cpp:16-22)
+    std::string input_dir = "/home/jayangad/data/1";
+    int64_t gpu_memory_limit = 100000000;
+    std::string temp_dir = "/tmp/1";
+    std::string output_file = "/tmp/2/output.bin";
+    int64_t kmer_length = 32;
+    uint32_t mergers_at_once = 2;
+    uint32_t merge_threads = 2;
+    // additive
+    int gpus = 1;
+    std::string input_mode = "auto";
+    uint64_t table_bytes = 0;
+    bool quiet = false;
+};
+
+bool starts(const char* s, const char* p) { return strncmp(s, p, strlen(p)) == 0; }
+
+Options parse(int argc, char** argv) {
+    Options o;
+    for (int i = 0; i < argc; i++) {
+        const char* a = argv[i];
+        if (starts(a, "kmerLength=")) {
+            o.kmer_length = (int64_t)strtoull(a + 11, nullptr, 10);
+            printf("Updating KmerLength=%" PRId64 "\n", o.kmer_length);
+        }
+        if (starts(a, "gpuMemoryLimit=")) {
+            o.gpu_memory_limit = (int64_t)strtoull(a + 15, nullptr, 10);
+            printf("Updating Gpu Memory Limit=%" PRId64 "\n", o.gpu_memory_limit);
+        }
+        if (starts(a, "inputFileLocation=")) {
+            o.input_dir = a + 18;
+            printf("Updating Input File Location='%s'\n", o.input_dir.c_str());
+        }
+        if (starts(a, "tempFileLocation=")) {
+            o.temp_dir = a + 17;
+            printf("Updating Temp File Location='%s'\n", o.temp_dir.c_str());
+        }
+        if (starts(a, "outputFile=")) {
+            o.output_file = a + 11;
+            printf("Updating Output File='%s'\n", o.output_file.c_str());
+        }
+        if (starts(a, "noOfMergersAtOnce=")) {
+            o.mergers_at_once = (uint32_t)atoi(a + 18);
+            printf("Updating No Of Mergers At Once='%u'\n", o.mergers_at_once);
+        }
+        if (starts(a, "noOfMergeThreads=")) {
+            o.merge_threads = (uint32_t)atoi(a + 17);
+            printf("Updating No Of Merge Threads='%u'\n", o.merge_threads);
+        }
+        if (starts(a, "gpus=")) o.gpus = atoi(a + 5);
+        if (starts(a, "inputMode=")) o.input_mode = a + 10;
+        if (starts(a, "tableBytes=")) o.table_bytes = strtoull(a + 11, nullptr, 10);
+        if (starts(a, "quiet=")) o.quiet = atoi(a + 6) != 0;
+    }
+    if (o.gpus < 1) o.gpus = 1;
+    return o;
+}
+
+// KMerCounter::GetChunkSize (KMerCounter.cpp:193-212).
+int64_t chunk_size(int64_t L, int64_t k, int64_t limit) {
+    int64_t kb = (k + 3) / 4;
+    int64_t rec = ((kb + 7) / 8 + 1) * 8;
+    int64_t per = rec * (L - k + 1);
+    if (per - 1 == 0) return 0;
+    return L * ((limit - L) / (per - 1));
+}
+
+// ---------------------------------------------------------------------------
+// print subcommand (KMerPrinter.cpp:35-91): each key word as 32 bases, then
+// " <count>". Output file argument is ignored, as in the reference.
+// ---------------------------------------------------------------------------
+int do_print(const char* in, int64_t k) {
+    int W = (int)(k / 32 + (k % 32 > 0 ? 1 : 0));
+    int rs = 8 * W + 4;
+    FILE* f = fopen(in, "rb");
+    if (!f) return 0;  // the reference prints nothing for a missing file
+    std::vector<unsigned char> buf((size_t)rs * 10000);
+    std::string line;
+    for (;;) {
+        size_t got = fread(buf.data(), 1, buf.size(), f);
+        if (got == 0) break;
+        // the reference zero-fills its buffer, so a trailing partial record
+        // prints with zero bytes past the end of the file
+        if (got % rs) memset(buf.data() + got, 0, rs - got % rs);
+        for (size_t off = 0; off < got; off += rs) {
+            line.clear();
+            for (int j = 0; j < W; j++) {
+                uint64_t v;
+                memcpy(&v, buf.data() + off + 8 * j, 8);
+                for (int b = 0; b < 32; b++) line.push_back("ACGT"[(v >> (62 - 2 * b)) & 3]);
+            }
+            uint32_t c;
+            memcpy(&c, buf.data() + off + 8 * W, 4);
+            printf("%s %u\n", line.c_str(), c);
+        }
+        if (got < buf.size()) break;
+    }
+    fclose(f);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// input files
+// ---------------------------------------------------------------------------
+
+struct InputFile {
+    std::string path;
+    int64_t L = 0;
+};
+
+std::vector<InputFile> list_inputs(const std::string& dir) {
+    std::vector<InputFile> v;
+    DIR* d = opendir(dir.c_str());
+    if (!d) {
+        printf("Couldn't open directory : %s\n", dir.c_str());
+        return v;
+    }
+    while (dirent* e = readdir(d)) {
+        if (e->d_name[0] == '.') continue;  // InputFileHandler.cpp:27 skips "." prefixes
+        InputFile f;
+        f.path = dir + "/" + e->d_name;
+        std::ifstream s(f.path.c_str());
+        std::string l1, l2;
+        std::getline(s, l1);
+        std::getline(s, l2);
+        f.L = (int64_t)l2.size();
+        v.push_back(f);
+    }
+    closedir(d);
+    return v;
+}
+
+struct Mapped {
+    const char* p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    bool map(const std::string& path) {
+        fd = open(path.c_str(), O_RDONLY);
+        if (fd < 0) return false;
+        struct stat st;
+        if (fstat(fd, &st) != 0) return false;
+        n = (size_t)st.st_size;
+        if (n == 0) return true;
+        void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) return false;
+        p = (const char*)m;
+        madvise(m, n, MADV_SEQUENTIAL);
+        return true;
+    }
+    ~Mapped() {
+        if (p) munmap((void*)p, n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+// Splits a FASTQ byte range into blocks of whole 4-line groups of roughly
+// `target` bytes (line counting from the start, so alignment is exact).
+std::vector<std::pair<size_t, size_t>> fastq_blocks(const char* p, size_t n, size_t target) {
+    std::vector<std::pair<size_t, size_t>> out;
+    size_t start = 0;
+    while (start < n) {
+        if (n - start <= target) {
+            out.push_back({start, n});
+            break;
+        }
+        size_t pos = start + target;
+        // walk back to the start of the 4-line group containing pos: count the
+        // lines of [start, pos) and move to the end of the current group
+        size_t lines = 0;
+        const char* q = p + start;
+        const char* e = p + pos;
+        while (q < e) {
+            const char* nl = (const char*)memchr(q, '\n', (size_t)(e - q));
+            if (!nl) break;
+            lines++;
+            q = nl + 1;
+        }
+        size_t cut = (size_t)(q - p);
+        while (lines % 4 != 0 && cut < n) {
+            const char* nl = (const char*)memchr(p + cut, '\n', n - cut);
+            cut = nl ? (size_t)(nl - p) + 1 : n;
+            lines++;
+        }
+        if (cut <= start) cut = n;
+        out.push_back({start, cut});
+        start = cut;
+    }
+    return out;
+}
+
+// The reference's chunker (FASTQFileReader::readData, FASTQFileReader.cpp:49-89)
+// driven the way InputFileHandler::read and KMerCounter::Start drive it
+// (InputFileHandler.cpp:82-95, KMerCounter.cpp:123-143).
+class ExactChunker {
+  public:
+    ExactChunker(const std::string& path, int64_t L) : L_(L) {
+        std::ifstream sz(path.c_str(), std::ios::ate | std::ios::binary);
+        size_ = sz.is_open() ? (int64_t)sz.tellg() : 0;
+        in_.open(path.c_str());
+    }
+    bool done() const { return done_; }
+    // Fills `chunk` with the next chunk's bytes; returns its size.
+    int64_t next(int64_t cap, std::vector<char>& chunk) {
+        chunk.resize((size_t)(cap > 0 ? cap : 0) + 1);
+        int64_t used = 0;
+        std::string prev, cur;
+        std::getline(in_, prev);
+        std::getline(in_, cur);
+        while (!cur.empty() && used + (int64_t)prev.size() < cap) {
+            if (cur[0] == '+') {
+                memcpy(chunk.data() + used, prev.data(), prev.size());
+                used += (int64_t)prev.size();
+                std::getline(in_, prev);
+                std::getline(in_, cur);
+            } else {
+                prev.swap(cur);
+                std::getline(in_, cur);
+            }
+        }
+        int64_t at = (int64_t)in_.tellg();
+        if (at + L_ > size_ || used == 0) done_ = true;
+        return used;
+    }
+
+  private:
+    std::ifstream in_;
+    int64_t size_ = 0, L_;
+    bool done_ = false;
+};
+
+void die(kc_ctx* c, kc_status s, const char* what) {
+    fprintf(stderr, "kmer-counter: %s: %s%s%s\n", what, kc_strerror(s), c ? ": " : "", c ? kc_last_error(c) : "");
+    exit(1);
+}
+
+kc_status count_exact(kc_ctx* c, const InputFile& f, const Options& o) {
+    int64_t cs = chunk_size(f.L, o.kmer_length, o.gpu_memory_limit);
+    ExactChunker ch(f.path, f.L);
+    std::vector<char> buf;
+    while (!ch.done()) {
+        int64_t n = ch.next(cs, buf);
+        if (n > 0 && n >= f.L) {  // KMerCounter.cpp:130
+            kc_status s = kc_count_chunk(c, buf.data(), n, f.L);
+            if (s) return s;
+        }
+    }
+    return KC_OK;
+}
+
+struct GpuWork {
+    int gpu;
+    kc_ctx* ctx = nullptr;
+    std::vector<std::string> runs;
+    kc_status status = KC_OK;
+    std::string err;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    printf("### kmer-counter application ###\n");
+    if (argc == 5 && strncmp(argv[1], "print", 5) == 0) return do_print(argv[2], atoll(argv[4]));
+    Options o = parse(argc, argv);
+    fflush(stdout);
+    if (o.kmer_length < 1 || o.kmer_length > KC_MAX_K) {
+        fprintf(stderr, "kmer-counter: kmerLength must be in [1, %d]\n", KC_MAX_K);
+        return 1;
+    }
+    std::vector<InputFile> files = list_inputs(o.input_dir);
+
+    // one context per GPU; blocks are dealt round-robin (read-shard, no collective)
+    std::vector<GpuWork> gw(o.gpus);
+    for (int g = 0; g < o.gpus; g++) {
+        kc_config cfg;
+        memset(&cfg, 0, sizeof(cfg));
+        cfg.device = g;
+        cfg.kmer_length = o.kmer_length;
+        cfg.line_length = files.empty() ? o.kmer_length : files[0].L;
+        cfg.gpu_memory_limit = (uint64_t)o.gpu_memory_limit;
+        cfg.table_bytes = o.table_bytes;
+        cfg.temp_dir = o.temp_dir.c_str();
+        cfg.flags = o.quiet ? KC_FLAG_QUIET : KC_FLAG_NONE;
+        gw[g].gpu = g;
+        kc_status s = kc_create(&gw[g].ctx, &cfg);
+        if (s) die(nullptr, s, "cannot create device context");
+    }
+
+    struct Job {
+        const char* p;
+        size_t n;
+        int64_t L;
+    };
+    for (const InputFile& f : files) {
+        if (f.L < o.kmer_length) continue;
+        bool exact = o.input_mode == "exact";
+        Mapped m;
+        if (!exact) {
+            if (!m.map(f.path)) die(nullptr, KC_ERR_IO, f.path.c_str());
+            if (m.n == 0) continue;
+        }
+        std::vector<std::pair<size_t, size_t>> blocks;
+        if (!exact) blocks = fastq_blocks(m.p, m.n, (size_t)1 << 30);
+        if (!exact && o.input_mode == "auto" && blocks.size() > 1) {
+            // validate every block before counting anything from the file
+            kc_ctx* c = gw[0].ctx;
+            for (auto& b : blocks) {
+                uint64_t nr = 0;
+                kc_status s = kc_check_fastq(c, m.p + b.first, b.second - b.first, f.L, &nr);
+                if (s == KC_ERR_FORMAT) {
+                    exact = true;
+                    break;
+                }
+                if (s) die(c, s, f.path.c_str());
+            }
+        }
+        if (!exact) {
+            std::vector<std::thread> th;
+            std::vector<kc_status> st(o.gpus, KC_OK);
+            bool fallback = false;
+            for (int g = 0; g < o.gpus; g++) {
+                th.emplace_back([&, g]() {
+                    for (size_t i = g; i < blocks.size(); i += o.gpus) {
+                        uint64_t nr = 0;
+                        kc_status s = kc_count_fastq(gw[g].ctx, m.p + blocks[i].first,
+                                                       blocks[i].second - blocks[i].first, f.L, &nr);
+                        if (s) {
+                            st[g] = s;
+                            return;
+                        }
+                    }
+                });
+            }
+            for (auto& t : th) t.join();
+            for (int g = 0; g < o.gpus; g++) {
+                if (st[g] == KC_ERR_FORMAT && o.input_mode == "auto" && blocks.size() == 1) {
+                    fallback = true;  // a single block validates before counting
+                } else if (st[g]) {
+                    die(gw[g].ctx, st[g], f.path.c_str());
+                }
+            }
+            if (!fallback) continue;
+            exact = true;
+        }
+        if (exact) {
+            kc_status s = count_exact(gw[0].ctx, f, o);
+            if (s) die(gw[0].ctx, s, f.path.c_str());
+        }
+    }
+
+    // finish every GPU, then write (one GPU) or merge the per-GPU runs
+    for (auto& w : gw) {
+        uint64_t n = 0;
+        kc_status s = kc_finish(w.ctx, &n);
+        if (s) die(w.ctx, s, "finish");
+    }
+    if (o.gpus == 1) {
+        kc_status s = kc_write_output(gw[0].ctx, o.output_file.c_str(), o.mergers_at_once, o.merge_threads);
+        if (s) die(gw[0].ctx, s, "write output");
+    } else {
+        std::vector<std::string> all;
+        for (auto& w : gw) {
+            std::string prefix = o.temp_dir + "/kc_gpu" + std::to_string(w.gpu) + "." + std::to_string(getpid());
+            uint32_t nr = 0;
+            kc_status s = kc_write_runs(w.ctx, prefix.c_str(), &nr);
+            if (s) die(w.ctx, s, "write runs");
+            for (uint32_t i = 0; i < nr; i++) all.push_back(prefix + "." + std::to_string(i));
+        }
+        std::vector<const char*> ptrs;
+        for (auto& s : all) ptrs.push_back(s.c_str());
+        kc_status s = kc_merge_files(ptrs.data(), (uint32_t)ptrs.size(), o.output_file.c_str(), o.kmer_length,
+                                     o.mergers_at_once, o.merge_threads);
+        for (auto& p : all) unlink(p.c_str());
+        if (s) die(nullptr, s, "merge");
+    }
+    for (auto& w : gw) {
+        if (!o.quiet) {
+            kc_stats st;
+            kc_get_stats(w.ctx, &st);
+            fprintf(stderr,
+                    "gpu %d: reads=%" PRIu64 " windows=%" PRIu64 " valid=%" PRIu64 " distinct=%" PRIu64
+                    " spilled=%" PRIu64 " runs=%" PRIu64 " insert_ms=%.3f\n",
+                    w.gpu, st.reads, st.windows, st.valid_kmers, st.output_records, st.spilled_kmers, st.spill_runs,
+                    st.insert_ms);
+        }
+        kc_destroy(w.ctx);
+    }
+    return 0;
+}

@@ -1,0 +1,113 @@
+// kc_device.h — host-side declarations of the HIP kernels' launch wrappers
+// (implemented in kc_kernels.hip, used by kc_api.cpp). Internal to libkc_hip.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace kc {
+
+// Device counters, one uint64 each, in a small device array owned by the ctx.
+enum Stat : int {
+    ST_VALID = 0,        // valid k-mer windows seen
+    ST_KEY0 = 1,         // count of key 0^W (kept outside the table: 0 is the EMPTY key)
+    ST_KEY0_PRESENT = 2, // key 0^W must appear in the output (a key-0 window or a hole)
+    ST_SPILLED = 3,      // keys appended to the spill buffer
+    ST_CLAIMED = 4,      // table slots claimed (= occupied)
+    ST_ERR = 5,          // bit set: ERR_* below
+    ST_SPILL_FILL = 6,   // next free spill index (may exceed capacity on overflow)
+    ST_NL_TOTAL = 7,     // FASTQ block: total newlines
+    ST_N = 16
+};
+
+enum ErrBits : uint64_t {
+    ERR_SPILL_OVERFLOW = 1,
+    ERR_FQ_NOT_AT = 2,      // record does not start with '@'
+    ERR_FQ_NO_PLUS = 4,     // line after the sequence does not start with '+'
+    ERR_FQ_SEQ_LEN = 8,     // sequence line length != L
+    ERR_FQ_TOO_MANY = 16,   // more records than the index buffer holds
+    ERR_FQ_NO_FINAL_NL = 32 // block does not end with '\n'
+};
+
+// Slot stride (uint64 words) of the open-addressed table for W key words:
+// W=1: {key, count}; W>=2: {key[W], count:u32 | state:u32} padded so that a
+// slot never straddles a 64-byte line.
+inline int slot_words(int W) { return W == 1 ? 2 : (W <= 3 ? 4 : 8); }
+
+struct CountLaunch {
+    const uint8_t* base;      // FASTQ block or stride-L chunk (device)
+    const uint64_t* seq_off;  // per-read start offsets, or nullptr for stride mode
+    uint64_t read0;           // first read of this launch
+    uint64_t n_reads;         // reads in this launch
+    int L, k;
+    uint64_t* table;
+    uint64_t cap;             // slots
+    uint64_t* spill;          // SoA: word j of entry i at spill[j*spill_cap + i]
+    uint64_t spill_cap;
+    uint64_t* stats;          // ST_N counters
+    uint32_t probe_limit;
+};
+
+// Tile geometry of count_kmers for (L, k); also used to size dynamic LDS.
+struct CountGeom {
+    int R;          // reads per tile
+    int NG;         // 16-base groups per read in LDS
+    int raw_stride; // LDS bytes per read of raw text
+    size_t lds;     // dynamic LDS bytes
+};
+CountGeom count_geometry(int L, int k);
+
+hipError_t launch_count_kmers(const CountLaunch& a, int grid_cap, hipStream_t s);
+
+// Table -> dense SoA (keys W x out_cap words, counts); cursor = device u64.
+hipError_t launch_compact(int W, const uint64_t* table, uint64_t cap, uint64_t* keys, uint32_t* cnts,
+                          uint64_t out_cap, uint64_t* cursor, hipStream_t s);
+// Appends (0^W, stats[ST_KEY0]) at index *cursor when stats[ST_KEY0_PRESENT].
+hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t out_cap, uint64_t* cursor,
+                              const uint64_t* stats, hipStream_t s);
+
+// OR / AND of every key word (2*W u64 at `bits`: or[0..W), and[W..2W)); host
+// must pre-set or = 0, and = ~0.
+hipError_t launch_key_bits(int W, const uint64_t* keys, uint64_t stride, uint64_t n, uint64_t* bits, hipStream_t s);
+
+// One LSD pass on digit (word, shift) of SoA records: keys (W arrays at
+// `stride`), optional vals. hist must hold 256 * grid u32. Returns the grid used.
+int sort_grid(uint64_t n);
+hipError_t launch_sort_pass(int W, const uint64_t* keys_in, uint64_t* keys_out, const uint32_t* vals_in,
+                            uint32_t* vals_out, uint64_t stride, uint64_t n, int word, int shift, uint32_t* hist,
+                            int grid, hipStream_t s);
+
+// Exclusive scan of n elements (device-wide); tmp must hold scan_tmp_elems(n).
+uint64_t scan_tmp_elems(uint64_t n);
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp, hipStream_t s);
+hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp, hipStream_t s);
+
+// Run-length reduce of sorted keys (counts = run lengths).
+hipError_t launch_rle_heads(int W, const uint64_t* keys, uint64_t stride, uint64_t n, uint32_t* flags,
+                            hipStream_t s);
+hipError_t launch_rle_scatter(int W, const uint64_t* keys, uint64_t stride, uint64_t n, const uint32_t* flags,
+                              const uint32_t* pos, uint64_t* out_keys, uint64_t out_stride, uint32_t* head_idx,
+                              hipStream_t s);
+hipError_t launch_rle_counts(const uint32_t* head_idx, uint64_t m, uint64_t n, uint32_t* cnts, hipStream_t s);
+
+// SoA -> SortedKMerFile bytes (rs = 8W+4 per record).
+hipError_t launch_pack(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n, void* out,
+                       hipStream_t s);
+
+// FASTQ block index (K1).
+uint64_t fq_chunks(const void* base, uint64_t n);
+hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hipStream_t s);
+hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t* seq_off,
+                          uint64_t* seq_end, uint64_t max_rec, uint64_t* stats, hipStream_t s);
+hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, uint64_t n_rec, int L,
+                              uint64_t* stats, hipStream_t s);
+
+// Synthetic FASTQ generator (bench/test input).
+struct SynthArgs {
+    uint64_t first, n, seed, genome, n_threshold;
+    int64_t L;
+};
+hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s);
+void synth_host(const SynthArgs& a, char* out);
+uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L);
+
+}  // namespace kc

@@ -1,0 +1,80 @@
+// kc_io.h — host-side sorted-run I/O and k-way merge (internal to libkc_hip).
+//
+// Output format (SortedKMerFile, SortedKMerFile.cpp:18-124): records of W
+// little-endian uint64 key words + little-endian uint32 count, rs = 8W+4 bytes,
+// ascending by the key words compared as unsigned integers, word 0 first
+// (KMerFileMerger::CheckLessThan, KMerFileMerger.cpp:98-108).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace kc {
+
+// A sorted run: either a file or a host memory range.
+struct RunSource {
+    std::string path;              // non-empty: read from this file
+    const uint8_t* mem = nullptr;  // else: this memory range
+    uint64_t bytes = 0;
+};
+
+// Streams records of one run, folding consecutive equal keys the way
+// SortedKMerFile::ReadKmer does (SortedKMerFile.cpp:57-82).
+class RunReader {
+  public:
+    RunReader(const RunSource& src, int W);
+    ~RunReader();
+    RunReader(const RunReader&) = delete;
+    RunReader& operator=(const RunReader&) = delete;
+    bool ok() const { return ok_; }
+    // Current (folded) record or nullptr at the end.
+    const uint8_t* head() const { return have_ ? cur_.data() : nullptr; }
+    void pop();
+
+  private:
+    bool raw_next(uint8_t* dst);
+    void fill();
+    int W_, rs_;
+    bool ok_ = true, have_ = false;
+    FILE* f_ = nullptr;
+    const uint8_t* mem_ = nullptr;
+    uint64_t mem_bytes_ = 0, mem_pos_ = 0;
+    std::vector<uint8_t> buf_;
+    size_t buf_pos_ = 0, buf_len_ = 0;
+    std::vector<uint8_t> cur_, look_;
+    bool look_valid_ = false;
+};
+
+// Buffered record writer (truncates the file).
+class RunWriter {
+  public:
+    RunWriter(const std::string& path, int rs);
+    ~RunWriter();
+    bool ok() const { return f_ != nullptr && !err_; }
+    void put(const uint8_t* rec);
+    bool close();
+
+  private:
+    FILE* f_ = nullptr;
+    int rs_;
+    bool err_ = false;
+    std::vector<uint8_t> buf_;
+    size_t len_ = 0;
+};
+
+// k-way merge of sorted runs into `out`; equal keys are summed as uint32
+// (KMerFileMerger::Merge, KMerFileMerger.cpp:49-96). Empty runs are skipped
+// (the reference dereferences NULL on them, KMerFileMerger.cpp:58).
+bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int W);
+
+// Merge tree with the reference handler's knobs (KMerFileMergeHandler.cpp):
+// while more than fan_in runs remain, groups of fan_in runs are merged into
+// temporary files "<tmp_prefix>.m<i>" by up to `threads` threads; the rest is
+// merged into `out`. The bytes of `out` do not depend on fan_in/threads.
+bool merge_tree(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t fan_in,
+                uint32_t threads, const std::string& tmp_prefix, std::string* err);
+
+int key_compare(const uint8_t* a, const uint8_t* b, int W);
+
+}  // namespace kc

@@ -1,0 +1,1112 @@
+// kc_kernels.hip — hand-written CDNA4 (gfx950, wave64) kernels of the k-mer
+// count path. Design and rooflines: DESIGN.md. Reference semantics restated
+// here:
+//   bitEncode     GPUHandler.cu:10-111  -> count_kmers stage 2 (LDS encode)
+//   extractKMers  GPUHandler.cu:129-233 -> count_kmers stage 3 (window keys)
+//   TBB hash      KMerCounter.cpp:61-82 -> count_kmers stage 3 (HBM table insert)
+//   sortKmers     GPUHandler.cu:300-327 -> sort_* (LSD radix, disabled in the ref)
+//   reduceKMers   GPUHandler.cu:329-360 -> rle_* (run-length reduce of spill runs)
+//   readData      FASTQFileReader.cpp:49-89 -> fq_* (FASTQ block index)
+#include <hip/hip_runtime.h>
+
+#include "kc_device.h"
+#include "kc_synth.h"
+
+namespace kc {
+
+typedef uint64_t u64;
+typedef unsigned int u32;
+
+constexpr int kBlock = 256;  // 4 waves of 64
+constexpr int kWave = 64;
+
+static inline u64 hmin(u64 a, u64 b) { return a < b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ u32 lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ u64 lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Wave-aggregated atomicAdd of `mine` (per lane) to *ctr; returns this lane's
+// exclusive position (ctr_old + prefix of lower active lanes).
+__device__ __forceinline__ u64 wave_reserve(u64* ctr, bool want) {
+    u64 m = __ballot(want);
+    u64 base = 0;
+    if (m) {
+        int leader = __ffsll((long long)m) - 1;
+        if ((int)lane_id() == leader) base = atomicAdd((unsigned long long*)ctr, (unsigned long long)__popcll(m));
+        base = __shfl(base, leader);
+    }
+    return base + (u64)__popcll(m & lanemask_lt());
+}
+
+__device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
+    // reduce v over the active lanes, one atomic per wave
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    u64 act = __ballot(1);
+    if ((int)lane_id() == __ffsll((long long)act) - 1 && v) atomicAdd((unsigned long long*)ctr, v);
+}
+
+__device__ __forceinline__ u64 mix64(u64 x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+template <int W>
+__device__ __forceinline__ u64 hash_key(const u64 (&key)[W]) {
+    u64 h = mix64(key[0] ^ 0x9e3779b97f4a7c15ull);
+#pragma unroll
+    for (int j = 1; j < W; j++) h = mix64(h ^ key[j]);
+    return h;
+}
+
+// Block-wide exclusive scan of one u32 per thread (256 threads). `lds` holds
+// >= 4 u32. Returns the exclusive prefix; *total receives the block sum.
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* lds, u32* total) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    u32 x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        u32 y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wave] = x;
+    __syncthreads();
+    u32 w0 = lds[0], w1 = lds[1], w2 = lds[2], w3 = lds[3];
+    u32 before = (wave > 0 ? w0 : 0) + (wave > 1 ? w1 : 0) + (wave > 2 ? w2 : 0);
+    *total = w0 + w1 + w2 + w3;
+    __syncthreads();
+    return before + x - v;
+}
+
+// ---------------------------------------------------------------------------
+// K2: count_kmers<W> — fused FASTQ/chunk tile stage -> 2-bit encode -> window
+// keys -> open-addressed HBM table insert (CAS claim + atomic count).
+//
+// One workgroup (256 threads) per tile of R reads:
+//   1. stage: the 16-byte-aligned span of every read is copied into LDS with
+//      coalesced 16 B loads (one read per aligned run of lanes);
+//   2. encode: each (read, 16-base group) -> a u32 of 2-bit codes
+//      (A0 C1 G2 T3, other bytes 3, MSB-first as bitEncode) and a 16-bit
+//      not-ACGT mask (bitEncode's filter); groups past L are zero, which is
+//      the reference's zero padding of the last word / past-end reads;
+//   3. windows: lane -> window (r, p); the W key words are funnel-shifted out
+//      of three consecutive code groups (extractKMers' shift-combine), the last
+//      word masked to k%32 bases only when ceil(k/4) < 8W (GPUHandler.cu:181);
+//      valid windows (no masked base in p..p+k-1) are inserted into the table.
+// Key 0^W never enters the table (0 is the EMPTY key): it is counted with one
+// wave-aggregated atomic into stats[ST_KEY0]. Any invalid window sets
+// stats[ST_KEY0_PRESENT] (the zeroed hole record of extractKMers reaches the
+// host hash as key 0, count 0: GPUHandler.cu:466 -> KMerCounter.cpp:70).
+// Inserts that exceed probe_limit go to the spill buffer (sorted into runs and
+// merged later), so no key is ever lost.
+// ---------------------------------------------------------------------------
+
+struct CountArgs {
+    const uint8_t* base;
+    const u64* seq_off;
+    u64 read0, n_reads;
+    int L, k, R, NG, raw_stride;
+    u64* table;
+    u64 cap;
+    u64* spill;
+    u64 spill_cap;
+    u64* stats;
+    u32 probe_limit;
+};
+
+CountGeom count_geometry(int L, int k) {
+    CountGeom g;
+    int W = (k + 31) / 32;
+    int nw = L - k + 1;
+    g.NG = (L + 15) / 16 + 2 * W + 1;
+    g.raw_stride = ((L + 31 + 15) / 16) * 16 + 16;
+    // aim for ~8 windows per thread, bounded by a 48 KiB LDS budget
+    int R = (8 * kBlock + nw - 1) / (nw > 0 ? nw : 1);
+    if (R < 1) R = 1;
+    if (R > 64) R = 64;
+    auto bytes = [&](int r) {
+        return (size_t)r * g.raw_stride + (size_t)r * g.NG * 8 + (size_t)r * 8 + 16;
+    };
+    while (R > 1 && bytes(R) > 48 * 1024) R--;
+    g.R = R;
+    g.lds = (bytes(R) + 15) & ~(size_t)15;
+    return g;
+}
+
+// W == 1: slot = {key, count}. Returns true when counted; *claimed when this
+// insert took an empty slot.
+__device__ __forceinline__ bool insert_w1(u64 key, u64* __restrict__ table, u64 cap, u32 limit, bool* claimed) {
+    u64 s = __umul64hi(mix64(key ^ 0x9e3779b97f4a7c15ull), cap);
+    for (u32 pr = 0; pr < limit; ++pr) {
+        u64* slot = table + 2 * s;
+        u64 old = atomicCAS((unsigned long long*)slot, 0ull, (unsigned long long)key);
+        if (old == 0ull || old == key) {
+            atomicAdd((unsigned int*)(slot + 1), 1u);
+            *claimed = (old == 0ull);
+            return true;
+        }
+        if (++s == cap) s = 0;
+    }
+    return false;
+}
+
+// W >= 2: slot = {key[W], count:u32, state:u32}; state 0 EMPTY, 1 WRITING,
+// 2 READY. The claimer writes the key words with agent-scope (sc1,
+// write-through) stores, drains them, then publishes state 2; readers poll the
+// state and read the words with sc1 loads (MI355X_MICROARCH.md "Valid forms").
+// A writer that does not publish within the spin bound makes the key spill,
+// which keeps the count exact.
+template <int W>
+__device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict__ table, u64 cap, u32 limit,
+                                            bool* claimed) {
+    constexpr int SW = (W <= 3) ? 4 : 8;
+    u64 s = __umul64hi(hash_key<W>(key), cap);
+    for (u32 pr = 0; pr < limit; ++pr) {
+        u64* slot = table + SW * s;
+        u32* cnt = (u32*)(slot + W);
+        u32* state = cnt + 1;
+        u32 st = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == 0u) {
+            u32 prev = atomicCAS(state, 0u, 1u);
+            if (prev == 0u) {
+#pragma unroll
+                for (int j = 0; j < W; j++)
+                    __hip_atomic_store(slot + j, key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd(cnt, 1u);
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(state, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *claimed = true;
+                return true;
+            }
+            st = prev;
+        }
+        u32 spins = 0;
+        while (st == 1u) {
+            if (++spins > 4096u) return false;
+            __builtin_amdgcn_s_sleep(1);
+            st = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < W; j++)
+            eq = eq && (__hip_atomic_load(slot + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key[j]);
+        if (eq) {
+            atomicAdd(cnt, 1u);
+            return true;
+        }
+        if (++s == cap) s = 0;
+    }
+    return false;
+}
+
+__device__ __forceinline__ u32 bytes_to_codes(u32 word, int nvalid, u32* bad_bits) {
+    // 4 bytes of text -> 4 2-bit codes in the low byte (first byte highest) and
+    // a 4-bit not-ACGT mask (first byte highest); bytes >= nvalid are zero.
+    u32 codes = 0, bad = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        u32 c = (word >> (8 * b)) & 0xffu;
+        u32 ok = (c == 'A') | (c == 'C') | (c == 'G') | (c == 'T');
+        u32 code = ok ? (((c >> 2) ^ (c >> 1)) & 3u) : 3u;
+        if (b >= nvalid) {
+            code = 0;
+            ok = 1;
+        }
+        codes |= code << (6 - 2 * b);
+        bad |= (ok ^ 1u) << (3 - b);
+    }
+    *bad_bits = bad;
+    return codes;
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void count_kmers(CountArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* raw = smem;
+    u32* codes = (u32*)(smem + (size_t)a.R * a.raw_stride);
+    u32* inval = codes + a.R * a.NG;
+    u32* lead = inval + a.R * a.NG;
+    u32* rflag = lead + a.R;
+
+    const int tid = threadIdx.x;
+    const int L = a.L, k = a.k, NG = a.NG;
+    const int nw = L - k + 1;
+    const bool mask_last = ((k + 3) / 4) < 8 * W;
+    const u64 last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
+    const int nch = (L + 30) / 16 + 1;  // 16 B chunks covering lead (<16) + L bytes
+    const u64 ntiles = (a.n_reads + a.R - 1) / a.R;
+
+    u64 my_valid = 0;
+    bool my_hole = false;
+
+    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const u64 r0 = tile * (u64)a.R;
+        const int nr = (int)min((u64)a.R, a.n_reads - r0);
+
+        // 1. stage the raw text of the tile's reads into LDS
+        for (int it = tid; it < nr * nch; it += kBlock) {
+            int r = it / nch, c = it - r * nch;
+            u64 gr = a.read0 + r0 + (u64)r;
+            u64 off = a.seq_off ? a.seq_off[gr] : gr * (u64)L;
+            uintptr_t addr = (uintptr_t)(a.base + off);
+            int ld = (int)(addr & 15);
+            if (c == 0) lead[r] = (u32)ld;
+            if (16 * c < ld + L) {
+                const uint4 v = *(const uint4*)((addr & ~(uintptr_t)15) + 16 * (uintptr_t)c);
+                *(uint4*)(raw + (size_t)r * a.raw_stride + 16 * c) = v;
+            }
+        }
+        if (tid < nr) rflag[tid] = 0;
+        __syncthreads();
+
+        // 2. encode 16-base groups
+        for (int it = tid; it < nr * NG; it += kBlock) {
+            int r = it / NG, g = it - r * NG;
+            int i0 = 16 * g;
+            u32 cw = 0, iv = 0;
+            if (i0 < L) {
+                int pos = (int)lead[r] + i0;
+                const u32* dw = (const u32*)(raw + (size_t)r * a.raw_stride) + (pos >> 2);
+                int sh = pos & 3;
+                u32 d0 = dw[0], d1 = dw[1], d2 = dw[2], d3 = dw[3], d4 = dw[4];
+                u32 x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                u32 x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                u32 x2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                u32 x3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+                int left = L - i0;
+                u32 b0, b1, b2, b3;
+                u32 c0 = bytes_to_codes(x0, left, &b0);
+                u32 c1 = bytes_to_codes(x1, left - 4, &b1);
+                u32 c2 = bytes_to_codes(x2, left - 8, &b2);
+                u32 c3 = bytes_to_codes(x3, left - 12, &b3);
+                cw = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+                iv = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
+            }
+            codes[it] = cw;
+            inval[it] = iv;
+            if (iv) atomicOr(&rflag[r], 1u);
+        }
+        __syncthreads();
+
+        // 3. windows -> keys -> table
+        const int total = nr * nw;
+        int r = tid / nw, p = tid - (tid / nw) * nw;
+        for (int it = tid; it - (tid & 63) < total; it += kBlock) {
+            // the loop bound is wave-uniform so every lane reaches the ballots
+            const bool active = it < total;
+            u64 key[W];
+            bool valid = false;
+            if (active) {
+                const u32* cr = codes + r * NG;
+                const int g = p >> 4, o = p & 15;
+#pragma unroll
+                for (int j = 0; j < W; j++) {
+                    const int gg = g + 2 * j;
+                    u64 hi = ((u64)cr[gg] << 32) | (u64)cr[gg + 1];
+                    u64 w = o ? ((hi << (2 * o)) | (u64)(cr[gg + 2] >> (32 - 2 * o))) : hi;
+                    key[j] = w;
+                }
+                key[W - 1] &= last_mask;
+                valid = true;
+                if (rflag[r]) {
+                    const u32* ir = inval + r * NG;
+                    const int last = p + k - 1;
+                    for (int gg = p >> 4; gg <= (last >> 4); gg++) {
+                        int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
+                        u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
+                        if (ir[gg] & rm) valid = false;
+                    }
+                }
+                my_hole |= !valid;
+            } else {
+#pragma unroll
+                for (int j = 0; j < W; j++) key[j] = 0;
+            }
+            bool is_zero = true;
+#pragma unroll
+            for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
+            // key 0^W: one atomic per wave
+            u64 zmask = __ballot(valid && is_zero);
+            if (zmask) {
+                if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
+                    atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
+                    atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                }
+            }
+            bool done = true, claimed = false;
+            if (valid) {
+                my_valid++;
+                if (!is_zero) {
+                    if constexpr (W == 1)
+                        done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
+                    else
+                        done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
+                }
+            }
+            u64 cm = __ballot(claimed);
+            if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+            // spill: wave-aggregated reservation in the spill buffer
+            bool spill = !done;
+            if (__ballot(spill)) {
+                u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
+                if (spill) {
+                    if (idx < a.spill_cap) {
+#pragma unroll
+                        for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
+                    } else {
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                    }
+                }
+            }
+            // advance to this lane's next window (stride 256 windows)
+            p += kBlock;
+            while (p >= nw) {
+                p -= nw;
+                r++;
+            }
+        }
+        __syncthreads();
+    }
+    wave_add(&a.stats[ST_VALID], my_valid);
+    if (__ballot(my_hole) && lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+}
+
+hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s) {
+    if (l.n_reads == 0) return hipSuccess;
+    CountGeom g = count_geometry(l.L, l.k);
+    CountArgs a;
+    a.base = l.base;
+    a.seq_off = l.seq_off;
+    a.read0 = l.read0;
+    a.n_reads = l.n_reads;
+    a.L = l.L;
+    a.k = l.k;
+    a.R = g.R;
+    a.NG = g.NG;
+    a.raw_stride = g.raw_stride;
+    a.table = l.table;
+    a.cap = l.cap;
+    a.spill = l.spill;
+    a.spill_cap = l.spill_cap;
+    a.stats = l.stats;
+    a.probe_limit = l.probe_limit;
+    u64 tiles = (l.n_reads + g.R - 1) / g.R;
+    int grid = (int)hmin(tiles, (u64)grid_cap);
+    int W = (l.k + 31) / 32;
+    switch (W) {
+    case 1: hipLaunchKernelGGL(count_kmers<1>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
+    case 2: hipLaunchKernelGGL(count_kmers<2>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
+    case 3: hipLaunchKernelGGL(count_kmers<3>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
+    case 4: hipLaunchKernelGGL(count_kmers<4>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K3: compact — occupied slots -> dense SoA records (order is arbitrary; the
+// radix sort fixes it).
+// ---------------------------------------------------------------------------
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void compact_table(const u64* __restrict__ table, u64 cap,
+                                                        u64* __restrict__ keys, u32* __restrict__ cnts, u64 out_cap,
+                                                        u64* cursor) {
+    constexpr int SW = (W == 1) ? 2 : ((W <= 3) ? 4 : 8);
+    for (u64 b = (u64)blockIdx.x * kBlock; b < cap; b += (u64)gridDim.x * kBlock) {
+        u64 s = b + threadIdx.x;
+        bool occ = false;
+        u64 kw[W];
+        u32 c = 0;
+        if (s < cap) {
+            const u64* slot = table + SW * s;
+#pragma unroll
+            for (int j = 0; j < W; j++) kw[j] = slot[j];
+            u64 meta = slot[W];
+            c = (u32)meta;
+            if constexpr (W == 1)
+                occ = kw[0] != 0ull;
+            else
+                occ = (u32)(meta >> 32) == 2u;
+        }
+        u64 pos = wave_reserve(cursor, occ);
+        if (occ && pos < out_cap) {
+#pragma unroll
+            for (int j = 0; j < W; j++) keys[(u64)j * out_cap + pos] = kw[j];
+            cnts[pos] = c;
+        }
+    }
+}
+
+template <int W>
+__global__ void append_key0(u64* keys, u32* cnts, u64 out_cap, u64* cursor, const u64* stats) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (stats[ST_KEY0_PRESENT] == 0) return;
+    u64 pos = *cursor;
+    if (pos >= out_cap) return;
+    for (int j = 0; j < W; j++) keys[(u64)j * out_cap + pos] = 0ull;
+    cnts[pos] = (u32)stats[ST_KEY0];
+    *cursor = pos + 1;
+}
+
+hipError_t launch_compact(int W, const uint64_t* table, uint64_t cap, uint64_t* keys, uint32_t* cnts,
+                          uint64_t out_cap, uint64_t* cursor, hipStream_t s) {
+    int grid = (int)hmin((cap + kBlock - 1) / kBlock, 8192);
+    if (grid < 1) grid = 1;
+    switch (W) {
+    case 1: hipLaunchKernelGGL(compact_table<1>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
+    case 2: hipLaunchKernelGGL(compact_table<2>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
+    case 3: hipLaunchKernelGGL(compact_table<3>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
+    case 4: hipLaunchKernelGGL(compact_table<4>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t out_cap, uint64_t* cursor,
+                              const uint64_t* stats, hipStream_t s) {
+    switch (W) {
+    case 1: hipLaunchKernelGGL(append_key0<1>, dim3(1), dim3(64), 0, s, keys, cnts, out_cap, cursor, stats); break;
+    case 2: hipLaunchKernelGGL(append_key0<2>, dim3(1), dim3(64), 0, s, keys, cnts, out_cap, cursor, stats); break;
+    case 3: hipLaunchKernelGGL(append_key0<3>, dim3(1), dim3(64), 0, s, keys, cnts, out_cap, cursor, stats); break;
+    case 4: hipLaunchKernelGGL(append_key0<4>, dim3(1), dim3(64), 0, s, keys, cnts, out_cap, cursor, stats); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K4: LSD radix sort (8-bit digits) of SoA records, stable. Per pass:
+//   upsweep   : per-block digit histogram -> hist[d * grid + b]
+//   scan      : single-block exclusive scan of hist (digit-major)
+//   downsweep : per 2048-record tile, stable in-tile ranking (wave match via 8
+//               ballots + cross-wave prefix in LDS), records permuted through
+//               LDS into digit order, then written to their global positions.
+// ---------------------------------------------------------------------------
+
+constexpr int kSortItems = 8;
+constexpr int kSortTile = kBlock * kSortItems;  // 2048
+
+int sort_grid(uint64_t n) {
+    u64 tiles = (n + kSortTile - 1) / kSortTile;
+    u64 g = tiles < 2048 ? tiles : 2048;
+    return (int)(g ? g : 1);
+}
+
+__device__ __forceinline__ void block_range(u64 n, int grid, int b, u64* lo, u64* hi) {
+    u64 tiles = (n + kSortTile - 1) / kSortTile;
+    u64 per = (tiles + grid - 1) / grid;
+    *lo = min(n, (u64)b * per * kSortTile);
+    *hi = min(n, (u64)(b + 1) * per * kSortTile);
+}
+
+__global__ __launch_bounds__(kBlock) void sort_upsweep(const u64* __restrict__ kw, u64 n, int shift,
+                                                       u32* __restrict__ hist) {
+    __shared__ u32 h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    u64 lo, hi;
+    block_range(n, gridDim.x, blockIdx.x, &lo, &hi);
+    for (u64 i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[(kw[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    hist[(u64)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// Single workgroup of 1024 threads: exclusive scan of m u32 in place.
+__global__ __launch_bounds__(1024) void scan_single_u32(u32* data, u64 m) {
+    __shared__ u32 part[1024];
+    const int t = threadIdx.x;
+    u64 per = (m + 1023) / 1024;
+    u64 lo = min(m, (u64)t * per), hi = min(m, lo + per);
+    u32 sum = 0;
+    for (u64 i = lo; i < hi; i++) sum += data[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        u32 v = (t >= o) ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    u32 run = part[t] - sum;
+    for (u64 i = lo; i < hi; i++) {
+        u32 v = data[i];
+        data[i] = run;
+        run += v;
+    }
+}
+
+template <int W, bool HAS_VALS>
+__global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__ kin, u64* __restrict__ kout,
+                                                         const u32* __restrict__ vin, u32* __restrict__ vout,
+                                                         u64 stride, u64 n, int word, int shift,
+                                                         const u32* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* skeys = (u64*)smem;                          // W x kSortTile
+    u32* svals = (u32*)(skeys + W * kSortTile);       // kSortTile
+    u32* wave_cnt = svals + kSortTile;                // 4 x 256
+    u32* wave_base = wave_cnt + 4 * 256;              // 4 x 256
+    u32* digit_run = wave_base + 4 * 256;             // 256: count so far in tile
+    u32* digit_start = digit_run + 256;               // 256: tile-local start
+    u32* global_off = digit_start + 256;              // 256: running global offset
+    u32* scan_tmp = global_off + 256;                 // 4
+
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    global_off[tid] = hist[(u64)tid * gridDim.x + blockIdx.x];
+    digit_run[tid] = 0;
+    for (int i = tid; i < 4 * 256; i += kBlock) wave_cnt[i] = 0;
+    __syncthreads();
+
+    u64 lo, hi;
+    block_range(n, gridDim.x, blockIdx.x, &lo, &hi);
+    for (u64 t0 = lo; t0 < hi; t0 += kSortTile) {
+        u64 kreg[kSortItems][W];
+        u32 vreg[kSortItems];
+        u32 dreg[kSortItems];
+        u32 rank[kSortItems];
+#pragma unroll
+        for (int it = 0; it < kSortItems; it++) {
+            u64 i = t0 + (u64)it * kBlock + tid;
+            bool ok = i < hi;
+#pragma unroll
+            for (int j = 0; j < W; j++) kreg[it][j] = ok ? kin[(u64)j * stride + i] : 0ull;
+            if constexpr (HAS_VALS) vreg[it] = ok ? vin[i] : 0u;
+            u32 d = (u32)(kreg[it][word] >> shift) & 255u;
+            dreg[it] = d;
+            // peers: active lanes with the same digit
+            u64 peers = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                u64 bb = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? bb : ~bb;
+            }
+            if (!ok) peers = 0;
+            u32 before = (u32)__popcll(peers & lanemask_lt());
+            if (ok && before == 0) wave_cnt[wave * 256 + d] = (u32)__popcll(peers);
+            __syncthreads();
+            {
+                // thread tid owns digit tid: per-wave bases in digit order, and
+                // re-zeroes the counters for the next item (the next writes to
+                // wave_cnt come after the barrier below)
+                u32 run = digit_run[tid];
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    u32 c = wave_cnt[w * 256 + tid];
+                    wave_cnt[w * 256 + tid] = 0;
+                    wave_base[w * 256 + tid] = run;
+                    run += c;
+                }
+                digit_run[tid] = run;
+            }
+            __syncthreads();
+            rank[it] = ok ? wave_base[wave * 256 + d] + before : 0xffffffffu;
+        }
+        __syncthreads();
+        u32 total;
+        u32 cnt = digit_run[tid];
+        u32 excl = block_excl_scan(cnt, scan_tmp, &total);
+        digit_start[tid] = excl;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kSortItems; it++) {
+            if (rank[it] == 0xffffffffu) continue;
+            u32 pos = digit_start[dreg[it]] + rank[it];
+#pragma unroll
+            for (int j = 0; j < W; j++) skeys[j * kSortTile + pos] = kreg[it][j];
+            if constexpr (HAS_VALS) svals[pos] = vreg[it];
+        }
+        __syncthreads();
+        u32 m = (u32)min((u64)kSortTile, hi - t0);
+        for (u32 pos = tid; pos < m; pos += kBlock) {
+            u64 k0[W];
+#pragma unroll
+            for (int j = 0; j < W; j++) k0[j] = skeys[j * kSortTile + pos];
+            u32 d = (u32)(k0[word] >> shift) & 255u;
+            u64 g = (u64)global_off[d] + (pos - digit_start[d]);
+#pragma unroll
+            for (int j = 0; j < W; j++) kout[(u64)j * stride + g] = k0[j];
+            if constexpr (HAS_VALS) vout[g] = svals[pos];
+        }
+        __syncthreads();
+        global_off[tid] += cnt;
+        digit_run[tid] = 0;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_sort_pass(int W, const uint64_t* keys_in, uint64_t* keys_out, const uint32_t* vals_in,
+                            uint32_t* vals_out, uint64_t stride, uint64_t n, int word, int shift, uint32_t* hist,
+                            int grid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(sort_upsweep, dim3(grid), dim3(kBlock), 0, s, keys_in + (u64)word * stride, n, shift, hist);
+    hipLaunchKernelGGL(scan_single_u32, dim3(1), dim3(1024), 0, s, hist, (u64)256 * grid);
+    size_t lds = (size_t)W * kSortTile * 8 + (size_t)kSortTile * 4 + (8 * 256 + 3 * 256 + 4) * 4;
+    lds = (lds + 15) & ~(size_t)15;
+    bool hv = vals_in != nullptr;
+#define KC_SORT_CASE(WW)                                                                                           \
+    case WW:                                                                                                       \
+        if (hv)                                                                                                    \
+            hipLaunchKernelGGL((sort_downsweep<WW, true>), dim3(grid), dim3(kBlock), lds, s, keys_in, keys_out,    \
+                               vals_in, vals_out, stride, n, word, shift, hist);                                   \
+        else                                                                                                       \
+            hipLaunchKernelGGL((sort_downsweep<WW, false>), dim3(grid), dim3(kBlock), lds, s, keys_in, keys_out,   \
+                               vals_in, vals_out, stride, n, word, shift, hist);                                   \
+        break;
+    switch (W) {
+        KC_SORT_CASE(1)
+        KC_SORT_CASE(2)
+        KC_SORT_CASE(3)
+        KC_SORT_CASE(4)
+    default: return hipErrorInvalidValue;
+    }
+#undef KC_SORT_CASE
+    return hipGetLastError();
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void key_bits(const u64* __restrict__ keys, u64 stride, u64 n, u64* bits) {
+    u64 o[W], a[W];
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        o[j] = 0;
+        a[j] = ~0ull;
+    }
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            u64 v = keys[(u64)j * stride + i];
+            o[j] |= v;
+            a[j] &= v;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        for (int s = 32; s >= 1; s >>= 1) {
+            o[j] |= __shfl_xor(o[j], s);
+            a[j] &= __shfl_xor(a[j], s);
+        }
+        if (lane_id() == 0) {
+            atomicOr((unsigned long long*)&bits[j], o[j]);
+            atomicAnd((unsigned long long*)&bits[W + j], a[j]);
+        }
+    }
+}
+
+hipError_t launch_key_bits(int W, const uint64_t* keys, uint64_t stride, uint64_t n, uint64_t* bits, hipStream_t s) {
+    int grid = (int)hmin((n + kBlock - 1) / kBlock, 2048);
+    if (grid < 1) grid = 1;
+    switch (W) {
+    case 1: hipLaunchKernelGGL(key_bits<1>, dim3(grid), dim3(kBlock), 0, s, keys, stride, n, bits); break;
+    case 2: hipLaunchKernelGGL(key_bits<2>, dim3(grid), dim3(kBlock), 0, s, keys, stride, n, bits); break;
+    case 3: hipLaunchKernelGGL(key_bits<3>, dim3(grid), dim3(kBlock), 0, s, keys, stride, n, bits); break;
+    case 4: hipLaunchKernelGGL(key_bits<4>, dim3(grid), dim3(kBlock), 0, s, keys, stride, n, bits); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// device-wide exclusive scan (reduce -> single-block scan -> downsweep)
+// ---------------------------------------------------------------------------
+
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kBlock * kScanItems;  // 4096
+
+uint64_t scan_tmp_elems(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void scan_reduce(const T* __restrict__ in, u64 n, T* __restrict__ sums) {
+    __shared__ T part[kBlock / kWave];
+    u64 base = (u64)blockIdx.x * kScanTile;
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        u64 idx = base + (u64)i * kBlock + threadIdx.x;
+        if (idx < n) s += in[idx];
+    }
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void scan_single(T* data, u64 m) {
+    __shared__ T part[1024];
+    const int t = threadIdx.x;
+    u64 per = (m + 1023) / 1024;
+    u64 lo = min(m, (u64)t * per), hi = min(m, lo + per);
+    T sum = 0;
+    for (u64 i = lo; i < hi; i++) sum += data[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        T v = (t >= o) ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    T run = part[t] - sum;
+    for (u64 i = lo; i < hi; i++) {
+        T v = data[i];
+        data[i] = run;
+        run += v;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void scan_down(const T* __restrict__ in, T* __restrict__ out, u64 n,
+                                                    const T* __restrict__ sums) {
+    __shared__ T wsum[kBlock / kWave];
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    // blocked: thread t owns items base + t*kScanItems .. +kScanItems
+    u64 base = (u64)blockIdx.x * kScanTile + (u64)tid * kScanItems;
+    T v[kScanItems];
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        u64 idx = base + i;
+        v[i] = idx < n ? in[idx] : (T)0;
+        s += v[i];
+    }
+    T x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    T before = sums[blockIdx.x];
+    for (int w = 0; w < wave; w++) before += wsum[w];
+    T run = before + x - s;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        u64 idx = base + i;
+        if (idx < n) out[idx] = run;
+        run += v[i];
+    }
+}
+
+template <typename T>
+static hipError_t scan_impl(const T* in, T* out, u64 n, T* tmp, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    u64 blocks = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(scan_reduce<T>, dim3((u32)blocks), dim3(kBlock), 0, s, in, n, tmp);
+    hipLaunchKernelGGL(scan_single<T>, dim3(1), dim3(1024), 0, s, tmp, blocks);
+    hipLaunchKernelGGL(scan_down<T>, dim3((u32)blocks), dim3(kBlock), 0, s, in, out, n, (const T*)tmp);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp, hipStream_t s) {
+    return scan_impl<u32>(in, out, n, tmp, s);
+}
+hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp, hipStream_t s) {
+    return scan_impl<u64>((const u64*)in, (u64*)out, n, (u64*)tmp, s);
+}
+
+// ---------------------------------------------------------------------------
+// run-length reduce of sorted spill keys (reduceKMers after a real sort)
+// ---------------------------------------------------------------------------
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void rle_heads(const u64* __restrict__ keys, u64 stride, u64 n,
+                                                    u32* __restrict__ flags) {
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        u32 h = 1;
+        if (i > 0) {
+            bool same = true;
+#pragma unroll
+            for (int j = 0; j < W; j++) same = same && keys[(u64)j * stride + i] == keys[(u64)j * stride + i - 1];
+            h = same ? 0u : 1u;
+        }
+        flags[i] = h;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void rle_scatter(const u64* __restrict__ keys, u64 stride, u64 n,
+                                                      const u32* __restrict__ flags, const u32* __restrict__ pos,
+                                                      u64* __restrict__ out, u64 ostride, u32* __restrict__ head) {
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        if (!flags[i]) continue;
+        u32 q = pos[i];
+#pragma unroll
+        for (int j = 0; j < W; j++) out[(u64)j * ostride + q] = keys[(u64)j * stride + i];
+        head[q] = (u32)i;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void rle_counts_k(const u32* __restrict__ head, u64 m, u64 n,
+                                                       u32* __restrict__ cnts) {
+    for (u64 q = (u64)blockIdx.x * kBlock + threadIdx.x; q < m; q += (u64)gridDim.x * kBlock) {
+        u64 end = (q + 1 < m) ? (u64)head[q + 1] : n;
+        cnts[q] = (u32)(end - head[q]);
+    }
+}
+
+static int grid_for(u64 n, int cap = 8192) {
+    u64 g = (n + kBlock - 1) / kBlock;
+    if (g > (u64)cap) g = cap;
+    return (int)(g ? g : 1);
+}
+
+hipError_t launch_rle_heads(int W, const uint64_t* keys, uint64_t stride, uint64_t n, uint32_t* flags,
+                            hipStream_t s) {
+    int g = grid_for(n);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(rle_heads<1>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags); break;
+    case 2: hipLaunchKernelGGL(rle_heads<2>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags); break;
+    case 3: hipLaunchKernelGGL(rle_heads<3>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags); break;
+    case 4: hipLaunchKernelGGL(rle_heads<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rle_scatter(int W, const uint64_t* keys, uint64_t stride, uint64_t n, const uint32_t* flags,
+                              const uint32_t* pos, uint64_t* out_keys, uint64_t out_stride, uint32_t* head_idx,
+                              hipStream_t s) {
+    int g = grid_for(n);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(rle_scatter<1>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags, pos, out_keys, out_stride, head_idx); break;
+    case 2: hipLaunchKernelGGL(rle_scatter<2>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags, pos, out_keys, out_stride, head_idx); break;
+    case 3: hipLaunchKernelGGL(rle_scatter<3>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags, pos, out_keys, out_stride, head_idx); break;
+    case 4: hipLaunchKernelGGL(rle_scatter<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, flags, pos, out_keys, out_stride, head_idx); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rle_counts(const uint32_t* head_idx, uint64_t m, uint64_t n, uint32_t* cnts, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(rle_counts_k, dim3(grid_for(m)), dim3(kBlock), 0, s, head_idx, m, n, cnts);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// pack: SoA -> SortedKMerFile records (W LE u64 words + LE u32 count)
+// ---------------------------------------------------------------------------
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void pack_records(const u64* __restrict__ keys, u64 stride,
+                                                       const u32* __restrict__ cnts, u64 n, u32* __restrict__ out) {
+    constexpr int RW = 2 * W + 1;  // u32 words per record
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        u32* o = out + i * RW;
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            u64 v = keys[(u64)j * stride + i];
+            o[2 * j] = (u32)v;
+            o[2 * j + 1] = (u32)(v >> 32);
+        }
+        o[2 * W] = cnts[i];
+    }
+}
+
+hipError_t launch_pack(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n, void* out,
+                       hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    int g = grid_for(n);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(pack_records<1>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
+    case 2: hipLaunchKernelGGL(pack_records<2>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
+    case 3: hipLaunchKernelGGL(pack_records<3>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
+    case 4: hipLaunchKernelGGL(pack_records<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K1: FASTQ block index. The block is viewed through 16-byte-aligned 64 KiB
+// chunks of the address space; fq_count counts '\n' per chunk, a device scan
+// turns counts into each chunk's first line index, and fq_emit re-reads the
+// chunk and, in address order, gives every newline its line index j:
+//   j % 4 == 0 (header ends)   -> seq_off[j/4] = q + 1
+//   j % 4 == 1 (sequence ends) -> seq_end[j/4] = q, next byte must be '+'
+//   j % 4 == 3 (quality ends)  -> next byte must be '@' (or end of block)
+// For well-formed 4-line records this selects exactly the lines readData
+// copies (the line before each '+' line, FASTQFileReader.cpp:57-63).
+// ---------------------------------------------------------------------------
+
+constexpr u64 kFqChunk = 65536;  // 256 threads x 16 B x 16 iterations
+
+uint64_t fq_chunks(const void* base, uint64_t n) {
+    u64 lead = (u64)((uintptr_t)base & 15);
+    return (lead + n + kFqChunk - 1) / kFqChunk;
+}
+
+// Newline bytes of a 16-byte load as a 16-bit mask (bit b = byte b), limited
+// to the bytes whose offset rel0 + b lies in [0, n).
+__device__ __forceinline__ u32 nl_mask16(const uint4 v, long long rel0, u64 n) {
+    u32 m = 0;
+    const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        u32 t = w[q] ^ 0x0a0a0a0au;
+        u32 nz = ((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t;  // 0x80 set in non-zero bytes
+        u32 z = ~nz & 0x80808080u;                      // 0x80 in '\n' bytes
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (z & (0x80u << (8 * b))) m |= 1u << (4 * q + b);
+    }
+    if (rel0 < 0) m &= 0xffffu << (u32)(-rel0 > 16 ? 16 : -rel0);
+    long long over = rel0 + 16 - (long long)n;
+    if (over > 0) m &= (over >= 16) ? 0u : (0xffffu >> (u32)over);
+    return m & 0xffffu;
+}
+
+__global__ __launch_bounds__(kBlock) void fq_count_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
+                                                     u64* __restrict__ counts) {
+    __shared__ u32 part[4];
+    const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
+    for (u64 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        u32 cnt = 0;
+#pragma unroll 4
+        for (int it = 0; it < 16; it++) {
+            uintptr_t addr = A + c * kFqChunk + (u64)it * 4096 + (u64)threadIdx.x * 16;
+            long long rel0 = (long long)(addr - (uintptr_t)base);
+            if (rel0 + 16 <= 0 || rel0 >= (long long)n) continue;
+            uint4 v = *(const uint4*)addr;
+            cnt += __popc(nl_mask16(v, rel0, n));
+        }
+        for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+        if (lane_id() == 0) part[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) counts[c] = (u64)part[0] + part[1] + part[2] + part[3];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fq_emit_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
+                                                    const u64* __restrict__ line_base, u64* __restrict__ seq_off,
+                                                    u64* __restrict__ seq_end, u64 max_rec, u64* stats) {
+    __shared__ u32 scan_tmp[4];
+    const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
+    u64 err = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (n == 0 || base[0] != '@') err |= ERR_FQ_NOT_AT;
+        if (n > 0 && base[n - 1] != '\n') err |= ERR_FQ_NO_FINAL_NL;
+    }
+    for (u64 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        u64 run = line_base[c];
+        for (int it = 0; it < 16; it++) {
+            uintptr_t addr = A + c * kFqChunk + (u64)it * 4096 + (u64)threadIdx.x * 16;
+            long long rel0 = (long long)(addr - (uintptr_t)base);
+            u32 m = 0;
+            if (!(rel0 + 16 <= 0 || rel0 >= (long long)n)) {
+                uint4 v = *(const uint4*)addr;
+                m = nl_mask16(v, rel0, n);
+            }
+            u32 total;
+            u32 before = block_excl_scan((u32)__popc(m), scan_tmp, &total);
+            u64 j = run + before;
+            while (m) {
+                int b = __ffs(m) - 1;
+                m &= m - 1;
+                u64 q = (u64)(rel0 + b);
+                u64 rec = j >> 2;
+                switch (j & 3) {
+                case 0:
+                    if (rec < max_rec) seq_off[rec] = q + 1;
+                    else err |= ERR_FQ_TOO_MANY;
+                    break;
+                case 1:
+                    if (rec < max_rec) seq_end[rec] = q;
+                    else err |= ERR_FQ_TOO_MANY;
+                    if (q + 1 >= n || base[q + 1] != '+') err |= ERR_FQ_NO_PLUS;
+                    break;
+                case 3:
+                    if (q + 1 < n && base[q + 1] != '@') err |= ERR_FQ_NOT_AT;
+                    break;
+                default: break;
+                }
+                j++;
+            }
+            run += total;
+        }
+    }
+    if (err) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)err);
+}
+
+__global__ __launch_bounds__(kBlock) void fq_validate_k(const u64* __restrict__ seq_off,
+                                                        const u64* __restrict__ seq_end, u64 n_rec, int L,
+                                                        u64* stats) {
+    bool bad = false;
+    for (u64 r = (u64)blockIdx.x * kBlock + threadIdx.x; r < n_rec; r += (u64)gridDim.x * kBlock)
+        bad |= (seq_end[r] - seq_off[r]) != (u64)L;
+    if (__ballot(bad) && lane_id() == 0)
+        atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_FQ_SEQ_LEN);
+}
+
+hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hipStream_t s) {
+    u64 nch = fq_chunks(base, n);
+    int g = (int)hmin(nch, 16384);
+    hipLaunchKernelGGL(fq_count_k, dim3(g ? g : 1), dim3(kBlock), 0, s, base, n, nch, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t* seq_off,
+                          uint64_t* seq_end, uint64_t max_rec, uint64_t* stats, hipStream_t s) {
+    u64 nch = fq_chunks(base, n);
+    int g = (int)hmin(nch, 16384);
+    hipLaunchKernelGGL(fq_emit_k, dim3(g ? g : 1), dim3(kBlock), 0, s, base, n, nch, line_base, seq_off, seq_end,
+                       max_rec, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, uint64_t n_rec, int L,
+                              uint64_t* stats, hipStream_t s) {
+    if (n_rec == 0) return hipSuccess;
+    hipLaunchKernelGGL(fq_validate_k, dim3(grid_for(n_rec)), dim3(kBlock), 0, s, seq_off, seq_end, n_rec, L, stats);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// synthetic FASTQ (bench/test input)
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void synth_k(kc_synth_params p, char* out) {
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < p.n; i += (u64)gridDim.x * kBlock) {
+        u64 rec = p.first + i;
+        kc_synth_record(p, rec, out + kc_synth_offset(p.first, rec, p.L));
+    }
+}
+
+static kc_synth_params to_params(const SynthArgs& a) {
+    kc_synth_params p;
+    p.first = a.first;
+    p.n = a.n;
+    p.seed = a.seed;
+    p.genome = a.genome;
+    p.n_threshold = a.n_threshold;
+    p.L = a.L;
+    return p;
+}
+
+hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(synth_k, dim3(grid_for(a.n, 16384)), dim3(kBlock), 0, s, to_params(a), out);
+    return hipGetLastError();
+}
+
+void synth_host(const SynthArgs& a, char* out) {
+    kc_synth_params p = to_params(a);
+    for (u64 i = 0; i < a.n; i++) {
+        u64 rec = a.first + i;
+        kc_synth_record(p, rec, out + kc_synth_offset(a.first, rec, a.L));
+    }
+}
+
+uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L) { return kc_synth_offset(first, first + n, L); }
+
+}  // namespace kc
