@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark of the k-mer count hot path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): k=31, 150 bp reads
+sampled from a 250 Mbp random genome (splitmix64 generator, seed 2), 50M reads
+per GPU, FASTQ text resident in HBM (generated on the device, untimed), in-HBM
+hash table only. One step = one full count of the GPU's reads: clear the table,
+index the FASTQ block (K1), encode + window + insert every k-mer (K2), compact
+and radix-sort the table into SortedKMerFile records (K3/K4). N GPUs: one
+process per GPU, each counts its own disjoint 50M-read shard (read-shard,
+weak scaling, no collective on the data path); the per-GPU sorted runs are what
+the host k-way merge would combine (not timed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--no-cpu]
+
+Prints one JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+METRIC = "k-mers/s (whole node) at k=31, 150bp reads; bit-exact vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def load_pkg():
+    spec = importlib.util.spec_from_file_location("kmer_counter_amd", os.path.join(ROOT, "kmer-counter_amd",
+                                                                                   "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["kmer_counter_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(kca, reads, L, k, genome, seed, first):
+    """The CPU port of the reference pipeline (oracle refcpu) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: timed as the CPU baseline only
+
+    threads = min(16, os.cpu_count() or 1)
+    fq = kca.synth_fastq(reads, L, seed, genome_length=genome, first_read=first)
+    t0 = time.perf_counter()
+    _, windows = oracle.refcpu(fq, k, gpu_memory_limit=100000000, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+            "sample": f"{reads} reads x {L} bp of the same workload ({windows} k-mers), oracle refcpu: "
+                      f"reference chunking (gpuMemoryLimit=1e8), bitEncode/extractKMers/reduceKMers restated, "
+                      f"sharded-lock hash, sorted output; {dt:.2f} s"}
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_count_kmers.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p))
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=50_000_000, help="reads per GPU")
+    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--L", type=int, default=150)
+    ap.add_argument("--genome", type=int, default=250_000_000)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--mem", type=int, default=24 << 30, help="gpuMemoryLimit per GPU (bytes)")
+    ap.add_argument("--cpu-reads", type=int, default=2_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group(backend="nccl")
+        dist = dist_mod
+
+    kca = load_pkg()
+    k, L = args.k, args.L
+    ctx = kca.Context(kmer_length=k, line_length=L, device=local, gpu_memory_limit=args.mem)
+    first = rank * args.reads
+    ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first)
+
+    def step():
+        ctx.reset()
+        ctx.count_fastq_device(ptr, nbytes)
+        return ctx.finish()
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    insert_ms = 0.0
+    launches = 0
+    finish_ms = 0.0
+    decode_ms = 0.0
+    n_rec = 0
+    for _ in range(args.steps):
+        n_rec = step()
+        st = ctx.stats()
+        insert_ms += st["insert_ms"]
+        launches += st["insert_launches"]
+        finish_ms += st["finish_ms"]
+        decode_ms += st["decode_ms"]
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    windows_per_gpu = args.reads * (L - k + 1)
+    total_kmers = windows_per_gpu * world * args.steps
+    value = total_kmers / elapsed
+
+    # roofline of the dominant kernel (count_kmers): algorithmic bytes per k-mer
+    # = FASTQ bytes per k-mer (read once) + 8W key bytes + 8 count bytes (read +
+    # write of the u32); per launch = that x the launch's k-mers.
+    W = (k + 31) // 32
+    b_per_kmer = nbytes / windows_per_gpu + 8 * W + 8
+    avg_launch_ms = insert_ms / max(1, launches)
+    kmers_per_launch = windows_per_gpu * args.steps / max(1, launches)
+    achieved = b_per_kmer * kmers_per_launch / (avg_launch_ms / 1e3) / 1e9
+    traffic = load_traffic()
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                "kernel": "count_kmers<1>", "avg_launch_ms": round(avg_launch_ms, 3),
+                "algorithmic_bytes_per_kmer": round(b_per_kmer, 3), "kmers_per_launch": int(kmers_per_launch)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(kca, args.cpu_reads, L, k, args.genome, args.seed, 0)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"cfg2: k={k}, {args.reads} x {L} bp reads per GPU sampled from a "
+                                   f"{args.genome} bp random genome (seed {args.seed}), FASTQ in HBM, "
+                                   f"in-HBM hash table", "k": k, "read_length": L, "reads_per_gpu": args.reads,
+                       "parallelism": f"read-shard x{world}", "gpu_memory_limit": args.mem},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "breakdown_ms_per_step": {"insert": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
+                                      "finish": finish_ms / args.steps},
+            "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"],
+        }
+        print(json.dumps(line), flush=True)
+    ctx.free_device(ptr)
+    ctx.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -560,7 +560,7 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
     u32* global_off = digit_start + 256;              // 256: running global offset
     u32* scan_tmp = global_off + 256;                 // 4
 
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const int tid = threadIdx.x, wave = tid >> 6;
     global_off[tid] = hist[(u64)tid * gridDim.x + blockIdx.x];
     digit_run[tid] = 0;
     for (int i = tid; i < 4 * 256; i += kBlock) wave_cnt[i] = 0;
@@ -580,7 +580,11 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
 #pragma unroll
             for (int j = 0; j < W; j++) kreg[it][j] = ok ? kin[(u64)j * stride + i] : 0ull;
             if constexpr (HAS_VALS) vreg[it] = ok ? vin[i] : 0u;
-            u32 d = (u32)(kreg[it][word] >> shift) & 255u;
+            u64 dw = kreg[it][0];
+#pragma unroll
+            for (int j = 1; j < W; j++)
+                if (j == word) dw = kreg[it][j];
+            u32 d = (u32)(dw >> shift) & 255u;
             dreg[it] = d;
             // peers: active lanes with the same digit
             u64 peers = __ballot(ok);
@@ -630,7 +634,11 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
             u64 k0[W];
 #pragma unroll
             for (int j = 0; j < W; j++) k0[j] = skeys[j * kSortTile + pos];
-            u32 d = (u32)(k0[word] >> shift) & 255u;
+            u64 dw = k0[0];
+#pragma unroll
+            for (int j = 1; j < W; j++)
+                if (j == word) dw = k0[j];
+            u32 d = (u32)(dw >> shift) & 255u;
             u64 g = (u64)global_off[d] + (pos - digit_start[d]);
 #pragma unroll
             for (int j = 0; j < W; j++) kout[(u64)j * stride + g] = k0[j];

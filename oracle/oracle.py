@@ -145,12 +145,20 @@ def ref_chunks(input_dir: str, chunk: int):
     return out
 
 
-def ref_merge(runs, out_path: str, k: int, fan_in: int = 2, threads: int = 2) -> bytes:
+class RefHang(RuntimeError):
+    """The reference's merge handler did not finish (its Run loop waits for
+    fan_in files forever once fewer remain, KMerFileMergeHandler.cpp:54-84)."""
+
+
+def ref_merge(runs, out_path: str, k: int, fan_in: int = 2, threads: int = 2, timeout: float = 30) -> bytes:
     """Merges sorted run files with the reference's own KMerFileMergeHandler."""
     if os.path.exists(out_path):
         os.unlink(out_path)  # the reference appends (KMerFileMerger.cpp:129)
-    subprocess.run([os.path.join(REF_DIR, "ref_merge"), out_path, str(k), str(fan_in), str(threads)] + list(runs),
-                   check=True, stdout=subprocess.DEVNULL, timeout=600)
+    try:
+        subprocess.run([os.path.join(REF_DIR, "ref_merge"), out_path, str(k), str(fan_in), str(threads)] + list(runs),
+                       check=True, stdout=subprocess.DEVNULL, timeout=timeout)
+    except subprocess.TimeoutExpired as e:
+        raise RefHang(str(e)) from None
     return open(out_path, "rb").read()
 
 

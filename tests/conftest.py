@@ -1,0 +1,37 @@
+import importlib.util
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libkc_hip.so on the device)")
+    config.addinivalue_line("markers", "slow: full-size configuration")
+
+
+def load_pkg():
+    if "kmer_counter_amd" in sys.modules:
+        return sys.modules["kmer_counter_amd"]
+    spec = importlib.util.spec_from_file_location("kmer_counter_amd",
+                                                  os.path.join(ROOT, "kmer-counter_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["kmer_counter_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="session")
+def kca():
+    return load_pkg()
+
+
+@pytest.fixture(scope="session")
+def orc():
+    import oracle
+    oracle.lib()
+    return oracle

@@ -1,0 +1,236 @@
+"""GPU parity: the HIP path (through the C ABI of libkc_hip.so) against the CPU
+oracle, bit-exact SortedKMerFile bytes. Needs an MI355X."""
+import json
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import kmer_ref_py as kp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+MANIFEST = json.load(open(os.path.join(GOLD, "MANIFEST.json")))
+
+
+def _fq(reads):
+    return "".join(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n" for i, s in enumerate(reads))
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_golden_fastq_path(kca, name):
+    m = MANIFEST[name]
+    data = open(os.path.join(GOLD, m["fastq"]), "rb").read()
+    want = open(os.path.join(GOLD, m["expected"]), "rb").read()
+    L = len(data.split(b"\n")[1])
+    with kca.Context(kmer_length=m["k"], line_length=L) as ctx:
+        ctx.count_fastq(data)
+        assert ctx.records() == want
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_golden_chunk_path(kca, orc, name):
+    """Reference-exact chunks (readData restatement) through kc_count_chunk."""
+    m = MANIFEST[name]
+    data = open(os.path.join(GOLD, m["fastq"]), "rb").read()
+    want = open(os.path.join(GOLD, m["expected"]), "rb").read()
+    L = len(data.split(b"\n")[1])
+    with kca.Context(kmer_length=m["k"], line_length=L) as ctx:
+        for chunk, ll in orc.chunks_of(data, orc.chunk_size(L, m["k"], 100000000)):
+            ctx.count_chunk(chunk, ll)
+        assert ctx.records() == want
+
+
+@pytest.mark.parametrize("k,L,n_rate", [(21, 100, 0.002), (31, 150, 0.0), (31, 150, 0.01), (32, 150, 0.001),
+                                        (33, 120, 0.001), (55, 150, 0.002), (64, 150, 0.0), (96, 150, 0.001),
+                                        (127, 150, 0.0), (128, 250, 0.001), (16, 64, 0.01), (31, 96, 0.0),
+                                        (25, 1000, 0.001), (31, 5000, 0.0005), (1, 12, 0.05)])
+def test_synthetic_vs_oracle(kca, orc, k, L, n_rate):
+    n = max(50, 300000 // L)
+    fq = kca.synth_fastq(n, L, seed=k * 7 + L, n_rate=n_rate)
+    with kca.Context(kmer_length=k, line_length=L) as ctx:
+        assert ctx.count_fastq(fq) == n
+        got = ctx.records()
+        st = ctx.stats()
+    assert got == orc.count_fastq(fq, k)
+    assert st["windows"] == n * (L - k + 1)
+
+
+def test_genome_reads_k31(kca, orc):
+    fq = kca.synth_fastq(200000, 150, seed=2, genome_length=2_000_000)
+    with kca.Context(kmer_length=31, line_length=150) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    want, _ = orc.refcpu(fq, 31, threads=8)
+    assert got == want
+
+
+def test_special_reads(kca):
+    reads = ["A" * 80, "N" * 80, "T" * 80, "acgt" * 20, "A" * 40 + "N" + "A" * 39, "C" * 79 + "N",
+             "ACGT" * 20, "T" * 31 + "G" + "T" * 48]
+    for k in (1, 21, 31, 32, 33, 64, 80):
+        text = _fq(reads)
+        want = kp.to_bytes(kp.count_reads(reads, k), k)
+        with kca.Context(kmer_length=k, line_length=80) as ctx:
+            ctx.count_fastq(text.encode())
+            assert ctx.records() == want, k
+
+
+def test_only_invalid_reads_give_key0_count0(kca):
+    text = _fq(["N" * 50] * 3)
+    with kca.Context(kmer_length=31, line_length=50) as ctx:
+        ctx.count_fastq(text.encode())
+        assert kp.parse_records(ctx.records(), 31) == [((0,), 0)]
+
+
+def test_empty_input(kca):
+    with kca.Context(kmer_length=31, line_length=150) as ctx:
+        ctx.count_fastq(b"")
+        ctx.count_chunk(b"", 150)
+        assert ctx.records() == b""
+
+
+def test_chunk_trailing_partial_read_is_ignored(kca):
+    reads = ["ACGTTGCA" * 4 + "AC"] * 3
+    chunk = "".join(reads).encode() + b"ACGTACGTAC"  # 10 bytes of a 4th read
+    with kca.Context(kmer_length=21, line_length=34) as ctx:
+        ctx.count_chunk(chunk, 34)
+        assert ctx.records() == kp.to_bytes(kp.count_reads(reads, 21), 21)
+
+
+def test_malformed_fastq_is_rejected_without_counting(kca):
+    good = _fq(["ACGT" * 25] * 4)
+    bad = good + "@x\nACGT\n+\nIIII\n"  # a short read
+    with kca.Context(kmer_length=21, line_length=100) as ctx:
+        with pytest.raises(kca.KcError) as e:
+            ctx.count_fastq(bad.encode())
+        assert e.value.status == kca.KC_ERR_FORMAT
+        with pytest.raises(kca.KcError):
+            ctx.count_fastq(good.encode()[:-1])  # no final newline
+        with pytest.raises(kca.KcError):
+            ctx.count_fastq(good.replace("\n+\n", "\n-\n", 1).encode())
+        ctx.count_fastq(good.encode())
+        assert ctx.records() == kp.to_bytes(kp.count_reads(["ACGT" * 25] * 4, 21), 21)
+
+
+def test_device_generator_matches_host(kca):
+    with kca.Context(kmer_length=31, line_length=150) as ctx:
+        for spec in [(5000, 150, 9, 0, 0.003, 0), (3000, 150, 2, 1_000_000, 0.0, 12345)]:
+            ptr, n = ctx.synth_device(*spec)
+            dev = ctx.copy_to_host(ptr, n)
+            ctx.free_device(ptr)
+            assert dev == kca.synth_fastq(*spec)
+
+
+def test_device_resident_fastq_and_reset(kca, orc):
+    with kca.Context(kmer_length=31, line_length=150) as ctx:
+        ptr, n = ctx.synth_device(20000, 150, 4, 500_000, 0.001, 0)
+        host = ctx.copy_to_host(ptr, n)
+        assert ctx.count_fastq_device(ptr, n) == 20000
+        first = ctx.records()
+        ctx.reset()
+        ctx.count_fastq_device(ptr, n)
+        again = ctx.records()
+        ctx.free_device(ptr)
+    assert first == again == orc.count_fastq(host, 31)
+
+
+@pytest.mark.parametrize("k,temp", [(31, False), (31, True), (55, False), (21, True), (100, False)])
+def test_spill_path(kca, orc, tmp_path, k, temp):
+    """A tiny working set forces the spill -> radix sort -> run -> merge path."""
+    L = 150
+    fq = kca.synth_fastq(20000, L, seed=k, n_rate=0.001)
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=1 << 20,
+                     temp_dir=str(tmp_path) if temp else None) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.output_bytes(str(tmp_path))
+        st = ctx.stats()
+    assert st["spill_runs"] >= 2 and st["spilled_kmers"] > 0
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_multiple_blocks_accumulate(kca, orc):
+    blocks = [kca.synth_fastq(3000, 150, seed=11, n_rate=0.001, first_read=i * 3000) for i in range(4)]
+    with kca.Context(kmer_length=31, line_length=150) as ctx:
+        for b in blocks:
+            ctx.count_fastq(b)
+        got = ctx.records()
+    assert got == orc.count_fastq(b"".join(blocks), 31)
+
+
+def _write_dir(tmp_path, name, text):
+    d = tmp_path / name
+    d.mkdir()
+    (d / "reads.fq").write_text(text)
+    return d
+
+
+@pytest.mark.parametrize("mode", ["auto", "fastq", "exact"])
+def test_cli_end_to_end(kca, orc, tmp_path, mode):
+    fq = kca.synth_fastq(5000, 150, seed=3, n_rate=0.002).decode()
+    d = _write_dir(tmp_path, "in", fq)
+    out = tmp_path / "out.bin"
+    o = kca.Options()
+    o.SetKmerLength(31)
+    o.SetInputFileDirectory(str(d))
+    o.setOutputFile(str(out))
+    o.setTempFileLocation(str(tmp_path))
+    kca.KMerCounter(o, [f"inputMode={mode}", "quiet=1"]).Start()
+    assert out.read_bytes() == orc.count_fastq(fq.encode(), 31)
+
+
+def test_cli_auto_falls_back_to_exact_on_malformed_input(kca, orc, tmp_path):
+    rng = random.Random(1)
+    text = "".join(f"@{'h' * 70}{i}\n{''.join(rng.choice('ACGT') for _ in range(30))}\n+\n{'I' * 30}\n"
+                   for i in range(200))
+    text = text.replace("\n+\n", "\n+\n", 1) + "\n"  # trailing blank line: not 4-line records
+    d = _write_dir(tmp_path, "in", text)
+    out = tmp_path / "out.bin"
+    limit = 20000
+    subprocess.run([kca.CLI_PATH, "kmerLength=21", f"inputFileLocation={d}", f"outputFile={out}",
+                    f"gpuMemoryLimit={limit}", f"tempFileLocation={tmp_path}", "quiet=1"], check=True,
+                   capture_output=True)
+    # the reference's reader loses reads at chunk edges here (header >= 2L)
+    want = orc.count_chunks(orc.chunks_of(text.encode(), orc.chunk_size(30, 21, limit)), 21)
+    assert out.read_bytes() == want
+
+
+def test_cli_spill_and_merge_knobs(kca, orc, tmp_path):
+    fq = kca.synth_fastq(30000, 100, seed=8, n_rate=0.001).decode()
+    d = _write_dir(tmp_path, "in", fq)
+    want = orc.count_fastq(fq.encode(), 25)
+    for fan, thr in ((2, 2), (3, 1), (8, 4)):
+        out = tmp_path / f"o{fan}.bin"
+        subprocess.run([kca.CLI_PATH, "kmerLength=25", f"inputFileLocation={d}", f"outputFile={out}",
+                        "gpuMemoryLimit=1048576", f"tempFileLocation={tmp_path}", f"noOfMergersAtOnce={fan}",
+                        f"noOfMergeThreads={thr}", "quiet=1"], check=True, capture_output=True)
+        assert out.read_bytes() == want
+    assert not [p for p in os.listdir(tmp_path) if p.startswith("kc.")]  # spill runs cleaned up
+
+
+@pytest.mark.slow
+def test_config2_full_size_properties(kca):
+    """BASELINE config 2 (k=31, 50M x 150 bp from a 250 Mbp genome): properties
+    that do not need a full CPU recount — strictly ascending keys, counts sum
+    to the valid windows, and every k-mer of sampled reads is present with a
+    count no lower than its multiplicity in the sample."""
+    n, L, k = 50_000_000, 150, 31
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=24 << 30) as ctx:
+        ptr, nb = ctx.synth_device(n, L, 2, 250_000_000, 0.0, 0)
+        assert ctx.count_fastq_device(ptr, nb) == n
+        ctx.free_device(ptr)
+        recs = np.frombuffer(ctx.records(), dtype=[("k", "<u8"), ("c", "<u4")])
+        st = ctx.stats()
+    assert st["spilled_kmers"] == 0
+    assert np.all(recs["k"][1:] > recs["k"][:-1])
+    assert int(recs["c"].astype(np.uint64).sum()) == n * (L - k + 1) == st["valid_kmers"]
+    sample = kca.synth_fastq(2000, L, 2, genome_length=250_000_000, first_read=n - 2000).decode()
+    cnt = kp.count_reads(kp.fastq_reads(sample), k)
+    keys = np.array([key[0] for key in cnt], dtype=np.uint64)
+    idx = np.searchsorted(recs["k"], keys)
+    assert np.all(recs["k"][idx] == keys)
+    assert np.all(recs["c"][idx] >= np.array([cnt[key] for key in cnt], dtype=np.uint32))
