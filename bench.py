@@ -73,7 +73,8 @@ def main():
     ap.add_argument("--L", type=int, default=150)
     ap.add_argument("--genome", type=int, default=250_000_000)
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--mem", type=int, default=24 << 30, help="gpuMemoryLimit per GPU (bytes)")
+    ap.add_argument("--mem", type=int, default=160 << 30, help="gpuMemoryLimit per GPU (bytes)")
+    ap.add_argument("--engine", default="partition", choices=["partition", "table"])
     ap.add_argument("--cpu-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -92,7 +93,7 @@ def main():
 
     kca = load_pkg()
     k, L = args.k, args.L
-    ctx = kca.Context(kmer_length=k, line_length=L, device=local, gpu_memory_limit=args.mem)
+    ctx = kca.Context(kmer_length=k, line_length=L, device=local, gpu_memory_limit=args.mem, engine=args.engine)
     first = rank * args.reads
     ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first)
 
@@ -115,6 +116,7 @@ def main():
     launches = 0
     finish_ms = 0.0
     decode_ms = 0.0
+    part_ms = [0.0] * 5
     n_rec = 0
     for _ in range(args.steps):
         n_rec = step()
@@ -123,6 +125,7 @@ def main():
         launches += st["insert_launches"]
         finish_ms += st["finish_ms"]
         decode_ms += st["decode_ms"]
+        part_ms = [a + b for a, b in zip(part_ms, st["part_ms"])]
     barrier_sync()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
@@ -166,7 +169,9 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "breakdown_ms_per_step": {"insert": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
-                                      "finish": finish_ms / args.steps},
+                                      "finish": finish_ms / args.steps,
+                                      "partition_passes": [round(x / args.steps, 3) for x in part_ms]},
+            "engine": args.engine,
             "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"],
         }
         print(json.dumps(line), flush=True)

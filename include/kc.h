@@ -87,11 +87,17 @@ typedef struct kc_config {
                                   files (Options::getTempFileLocation); NULL or ""
                                   keeps spill runs in host memory */
     uint32_t flags;            /* KC_FLAG_* */
-    uint32_t reserved1;
+    uint32_t lds_slots;        /* partition engine: LDS table slots per bucket
+                                  (0 = the maximum that fits; small values force
+                                  the overflow path, for tests) */
 } kc_config;
 
 #define KC_FLAG_NONE 0u
-#define KC_FLAG_QUIET 1u /* no progress lines on stderr */
+#define KC_FLAG_QUIET 1u        /* no progress lines on stderr */
+#define KC_FLAG_ENGINE_TABLE 2u /* count with the global atomic hash table only
+                                   (default engine: hash-partition the k-mers into
+                                   65536 buckets and count each in an LDS table;
+                                   the global table catches LDS overflow) */
 
 typedef struct kc_stats {
     uint64_t reads;            /* reads counted so far */
@@ -107,6 +113,9 @@ typedef struct kc_stats {
     double decode_ms;          /* FASTQ index + validate kernels */
     double finish_ms;          /* compact + sort + pack */
     double last_count_ms;      /* device time of the last kc_count_* call */
+    double part_ms[5];         /* partition engine: hist, scatter, radix pass,
+                                  bucket bounds, LDS bucket count (summed) */
+    uint64_t batches;          /* partition engine batches */
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". */

@@ -50,7 +50,7 @@ class _Config(ctypes.Structure):
         ("table_bytes", ctypes.c_uint64),
         ("temp_dir", ctypes.c_char_p),
         ("flags", ctypes.c_uint32),
-        ("reserved1", ctypes.c_uint32),
+        ("lds_slots", ctypes.c_uint32),
     ]
 
 
@@ -69,10 +69,14 @@ class Stats(ctypes.Structure):
         ("decode_ms", ctypes.c_double),
         ("finish_ms", ctypes.c_double),
         ("last_count_ms", ctypes.c_double),
+        ("part_ms", ctypes.c_double * 5),
+        ("batches", ctypes.c_uint64),
     ]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_}
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["part_ms"] = list(self.part_ms)
+        return d
 
 
 class _Synth(ctypes.Structure):
@@ -169,14 +173,17 @@ class Context:
 
     def __init__(self, kmer_length: int, line_length: int = 0, device: int = 0,
                  gpu_memory_limit: int = 100000000, table_bytes: int = 0, temp_dir: Optional[str] = None,
-                 quiet: bool = True):
+                 quiet: bool = True, engine: str = "partition", lds_slots: int = 0):
         self._L = lib()
         self.k = kmer_length
         self.W = (kmer_length + 31) // 32
         self.rs = 8 * self.W + 4
         self._tmp = temp_dir.encode() if temp_dir else None
+        if engine not in ("partition", "table"):
+            raise ValueError("engine must be 'partition' or 'table'")
+        flags = (1 if quiet else 0) | (2 if engine == "table" else 0)
         cfg = _Config(device, 0, kmer_length, line_length or kmer_length, int(gpu_memory_limit), int(table_bytes),
-                      self._tmp, 1 if quiet else 0, 0)
+                      self._tmp, flags, int(lds_slots))
         h = ctypes.c_void_p()
         st = self._L.kc_create(ctypes.byref(h), ctypes.byref(cfg))
         if st:

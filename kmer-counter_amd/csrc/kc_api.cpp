@@ -55,6 +55,21 @@ struct kc_ctx {
     uint64_t* stats = nullptr;      // device ST_N
     uint64_t* stats_h = nullptr;    // pinned host mirror
 
+    // partition engine (default): key buffers for one batch, records
+    bool part = true;
+    uint64_t key_cap = 0;          // keys per batch
+    uint64_t* keys_a = nullptr;    // W x key_cap
+    uint64_t* keys_b = nullptr;
+    DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
+    uint64_t* rec_keys = nullptr;  // W x rec_cap
+    uint32_t* rec_cnts = nullptr;
+    uint64_t rec_cap = 0;
+    uint64_t* rec_cursor = nullptr;  // device u64
+    uint64_t rec_n = 0;              // host copy after each batch
+    uint64_t batches = 0;
+    int n_cu = 256;
+    double part_ms[5] = {0, 0, 0, 0, 0};  // P1, P2, P3, P4, P5
+
     // scratch (grown on demand)
     DevBuf in_stage;        // host-pointer inputs
     DevBuf fq_counts, fq_base, fq_tmp, seq_off, seq_end;
@@ -148,7 +163,7 @@ static kc_status sort_records(kc_ctx* c, uint64_t* ka, uint64_t* kb, uint32_t* v
     HIPCHK(c, hipMemcpyAsync(bits.data(), c->fin_misc.p, 2 * W * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     int grid = sort_grid(n);
-    s = ensure(c, c->fin_hist, (size_t)256 * grid * 4);
+    s = ensure(c, c->fin_hist, (size_t)sort_hist_elems(grid) * 8);
     if (s) return s;
     uint64_t* kin = ka;
     uint64_t* kout = kb;
@@ -159,8 +174,8 @@ static kc_status sort_records(kc_ctx* c, uint64_t* ka, uint64_t* kb, uint32_t* v
         uint64_t vary = bits[word] ^ bits[W + word];
         for (int shift = 0; shift < 64; shift += 8) {
             if (((vary >> shift) & 255u) == 0) continue;
-            HIPCHK(c, launch_sort_pass(W, kin, kout, vin, vout, stride, n, word, shift, (uint32_t*)c->fin_hist.p,
-                                       grid, c->stream));
+            HIPCHK(c, launch_sort_pass(W, kin, kout, vin, vout, stride, n, word, shift, (uint64_t*)c->fin_hist.p,
+                                       grid, false, c->stream));
             std::swap(kin, kout);
             std::swap(vin, vout);
             cur ^= 1;
@@ -174,19 +189,15 @@ static kc_status sort_records(kc_ctx* c, uint64_t* ka, uint64_t* kb, uint32_t* v
 // spill runs: sort the spill buffer, run-length reduce, pack, move to host
 // ---------------------------------------------------------------------------
 
-static kc_status flush_spill(kc_ctx* c) {
-    kc_status s = sync_stats(c);
-    if (s) return s;
-    uint64_t n = c->stats_h[ST_SPILL_FILL];
-    if (n == 0) return KC_OK;
-    if (n > c->spill_cap) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow (%llu > %llu)",
-                                      (unsigned long long)n, (unsigned long long)c->spill_cap);
+// Sorts n spilled keys (SoA at `stride` in `keys`, `scratch` of the same
+// shape), run-length reduces them and stores the run (host memory or a temp
+// file).
+static kc_status flush_keys(kc_ctx* c, uint64_t* keys, uint64_t stride, uint64_t n, uint64_t* scratch) {
+    kc_status s;
     const int W = c->W;
-    uint64_t stride = c->spill_cap;
-    if ((s = ensure(c, c->spill_keys2, (size_t)W * stride * 8))) return s;
     int which = 0;
-    if ((s = sort_records(c, c->spill, (uint64_t*)c->spill_keys2.p, nullptr, nullptr, stride, n, &which))) return s;
-    uint64_t* sorted = which ? (uint64_t*)c->spill_keys2.p : c->spill;
+    if ((s = sort_records(c, keys, scratch, nullptr, nullptr, stride, n, &which))) return s;
+    uint64_t* sorted = which ? scratch : keys;
     if ((s = ensure(c, c->rle_flags, n * 4)) || (s = ensure(c, c->rle_pos, n * 4)) ||
         (s = ensure(c, c->rle_head, n * 4)) || (s = ensure(c, c->rle_tmp, scan_tmp_elems(n) * 4)) ||
         (s = ensure(c, c->run_keys, (size_t)W * n * 8)) || (s = ensure(c, c->run_cnts, n * 4)))
@@ -209,9 +220,7 @@ static kc_status flush_spill(kc_ctx* c) {
     run.records = m;
     run.mem.resize(bytes);
     HIPCHK(c, hipMemcpyAsync(run.mem.data(), c->run_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->stats + ST_SPILL_FILL, 0, 8, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->stats_h[ST_SPILL_FILL] = 0;
     c->spilled_flushed += n;
     if (!c->temp_dir.empty()) {
         char name[128];
@@ -229,6 +238,22 @@ static kc_status flush_spill(kc_ctx* c) {
     return KC_OK;
 }
 
+// Flushes the spill buffer of the global table into a sorted run.
+static kc_status flush_spill(kc_ctx* c) {
+    kc_status s = sync_stats(c);
+    if (s) return s;
+    uint64_t n = c->stats_h[ST_SPILL_FILL];
+    if (n == 0) return KC_OK;
+    if (n > c->spill_cap) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow (%llu > %llu)",
+                                      (unsigned long long)n, (unsigned long long)c->spill_cap);
+    if ((s = ensure(c, c->spill_keys2, (size_t)c->W * c->spill_cap * 8))) return s;
+    if ((s = flush_keys(c, c->spill, c->spill_cap, n, (uint64_t*)c->spill_keys2.p))) return s;
+    HIPCHK(c, hipMemsetAsync(c->stats + ST_SPILL_FILL, 0, 8, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stats_h[ST_SPILL_FILL] = 0;
+    return KC_OK;
+}
+
 // ---------------------------------------------------------------------------
 // counting
 // ---------------------------------------------------------------------------
@@ -240,8 +265,10 @@ static kc_status check_line(kc_ctx* c, int64_t L) {
     return KC_OK;
 }
 
-// Counts n_reads reads (stride mode when seq_off == nullptr).
-static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
+// Engine "table": every k-mer is inserted into the global HBM table with
+// atomics. Counts n_reads reads (stride mode when seq_off == nullptr).
+static kc_status count_reads_table(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
+                                   int64_t L) {
     if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     const uint64_t nw = (uint64_t)(L - c->k + 1);
     const uint64_t max_reads = c->spill_cap / nw;
@@ -287,6 +314,157 @@ static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq
     c->st.valid_kmers = c->stats_h[ST_VALID];
     c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
     return KC_OK;
+}
+
+static kc_status grow_records(kc_ctx* c, uint64_t need) {
+    if (need <= c->rec_cap) return KC_OK;
+    uint64_t ncap = c->rec_cap ? c->rec_cap : 1024;
+    while (ncap < need) ncap = ncap + ncap / 2 + 1024;
+    const int W = c->W;
+    uint64_t* nk = nullptr;
+    uint32_t* nc = nullptr;
+    HIPCHK(c, hipMalloc((void**)&nk, (size_t)W * ncap * 8));
+    HIPCHK(c, hipMalloc((void**)&nc, (size_t)ncap * 4));
+    if (c->rec_n) {
+        for (int j = 0; j < W; j++)
+            HIPCHK(c, hipMemcpyAsync(nk + (size_t)j * ncap, c->rec_keys + (size_t)j * c->rec_cap, c->rec_n * 8,
+                                     hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(nc, c->rec_cnts, c->rec_n * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->rec_keys) HIPCHK(c, hipFree(c->rec_keys));
+    if (c->rec_cnts) HIPCHK(c, hipFree(c->rec_cnts));
+    c->rec_keys = nk;
+    c->rec_cnts = nc;
+    c->rec_cap = ncap;
+    return KC_OK;
+}
+
+static const int kBucketBits = 16;
+
+// Engine "partition": per batch of reads
+//   P1 hist   : digit (hash >> 48) & 255 per segment of reads
+//   P2 scatter: keys to their digit's region (LDS counting sort per tile)
+//   P3        : stable radix pass on digit (hash >> 56) -> grouped by bucket = hash >> 48
+//   P4        : bucket ranges (binary search)
+//   P5        : per-bucket LDS hash count -> (key, count) records
+static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
+                                  int64_t L) {
+    if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
+    const int W = c->W;
+    const uint64_t nw = (uint64_t)(L - c->k + 1);
+    const uint64_t max_reads = c->key_cap / nw;
+    if (max_reads == 0) return fail(c, KC_ERR_ARG, "gpu_memory_limit too small for one read's windows");
+    kc_status s;
+    uint64_t done = 0;
+    float t = 0.f;
+    while (done < n_reads) {
+        uint64_t nr = n_reads - done;
+        if (nr > max_reads) nr = max_reads;
+        CountLaunch l;
+        l.base = base;
+        l.seq_off = seq_off;
+        l.read0 = done;
+        l.n_reads = nr;
+        l.L = (int)L;
+        l.k = (int)c->k;
+        l.table = c->table;
+        l.cap = c->cap;
+        l.spill = c->spill;
+        l.spill_cap = c->spill_cap;
+        l.stats = c->stats;
+        l.probe_limit = probe_limit(c);
+        PartGeom pg = part_geometry((int)L, (int)c->k, nr);
+        uint64_t hn = 256 * pg.nseg;
+        if ((s = ensure(c, c->part_hist, hn * 8)) || (s = ensure(c, c->part_base, hn * 8)) ||
+            (s = ensure(c, c->part_tmp, scan_tmp_elems(hn) * 8)))
+            return s;
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 48, c->stream));
+        HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn, (uint64_t*)c->part_tmp.p,
+                                  c->stream));
+        uint64_t tail[2];
+        HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->part_base.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->part_hist.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+        c->part_ms[0] += t;
+        const uint64_t n = tail[0] + tail[1];
+        if (n > c->key_cap) return fail(c, KC_ERR_INTERNAL, "batch keys %llu exceed capacity", (unsigned long long)n);
+
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        HIPCHK(c, hipEventSynchronize(c->ev1));
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+        c->part_ms[1] += t;
+        c->st.insert_launches++;
+        c->st.insert_ms += t;
+
+        if (n > 0) {
+            int grid = sort_grid(n);
+            if ((s = ensure(c, c->part_sort_hist, (size_t)sort_hist_elems(grid) * 8))) return s;
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            HIPCHK(c, launch_sort_pass(W, c->keys_a, c->keys_b, nullptr, nullptr, c->key_cap, n, 0, 56,
+                                       (uint64_t*)c->part_sort_hist.p, grid, true, c->stream));
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipEventSynchronize(c->ev1));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[2] += t;
+
+            uint32_t nb = 1u << kBucketBits;
+            if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8))) return s;
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            HIPCHK(c, launch_bucket_bounds(W, c->keys_b, c->key_cap, n, kBucketBits, (uint64_t*)c->part_starts.p,
+                                           c->stream));
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipEventSynchronize(c->ev1));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[3] += t;
+
+            uint64_t lslots = (uint64_t)bucket_lds_slots(W);
+            uint64_t bound = (uint64_t)nb * lslots;
+            if ((s = grow_records(c, c->rec_n + (n < bound ? n : bound)))) return s;
+            // keys_a is free after P3: it takes P5's spills (capacity >= n)
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            HIPCHK(c, launch_count_buckets(W, c->keys_b, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
+                                           c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
+                                           c->keys_a, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
+                                           c->n_cu, c->stream));
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+            if ((s = sync_stats(c))) return s;
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[4] += t;
+            if (c->stats_h[ST_ERR] & ERR_REC_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
+            if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
+            uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
+            if (n2) {
+                if ((s = flush_keys(c, c->keys_a, c->key_cap, n2, c->keys_b))) return s;
+                HIPCHK(c, hipMemsetAsync(c->stats + ST_SPILL2_FILL, 0, 8, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                c->stats_h[ST_SPILL2_FILL] = 0;
+            }
+        } else if ((s = sync_stats(c))) {
+            return s;
+        }
+        c->batches++;
+        done += nr;
+    }
+    c->st.reads += n_reads;
+    c->st.windows += n_reads * nw;
+    c->st.valid_kmers = c->stats_h[ST_VALID];
+    c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
+    return KC_OK;
+}
+
+static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
+    // very long reads (one read's windows do not fit a P2 workgroup's LDS)
+    // take the table engine; both feed the same finish
+    if (c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= 150 * 1024)
+        return count_reads_part(c, base, seq_off, n_reads, L);
+    return count_reads_table(c, base, seq_off, n_reads, L);
 }
 
 static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out) {
@@ -386,9 +564,21 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(KC_ERR_HIP);
     uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
     if (M < (1u << 20)) M = 1u << 20;
+    c->part = (cfg->flags & KC_FLAG_ENGINE_TABLE) == 0;
     size_t slot_bytes = 8 * (size_t)slot_words(c->W);
-    size_t spill_bytes = M / 16;
-    size_t tbytes = cfg->table_bytes ? cfg->table_bytes : (M - 4 * spill_bytes);
+    size_t spill_bytes, tbytes;
+    if (c->part) {
+        // partition engine: two key buffers take the working set; the global
+        // table and spill buffer only catch LDS-table overflow
+        spill_bytes = M / 64;
+        tbytes = cfg->table_bytes ? cfg->table_bytes : M / 16;
+        uint64_t rest = M - M / 64 - M / 16;
+        c->key_cap = rest / (16 * (uint64_t)c->W);
+        if (c->key_cap < 65536) c->key_cap = 65536;
+    } else {
+        spill_bytes = M / 16;
+        tbytes = cfg->table_bytes ? cfg->table_bytes : (M - 4 * spill_bytes);
+    }
     c->spill_cap = spill_bytes / (8 * c->W);
     if (c->spill_cap < 4096) c->spill_cap = 4096;
     c->cap = tbytes / slot_bytes;
@@ -398,6 +588,14 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     if (hipMalloc((void**)&c->spill, (size_t)c->spill_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
     if (hipMalloc((void**)&c->stats, ST_N * 8) != hipSuccess) return bail(KC_ERR_NOMEM);
     if (hipHostMalloc((void**)&c->stats_h, ST_N * 8, 0) != hipSuccess) return bail(KC_ERR_NOMEM);
+    if (c->part) {
+        if (hipMalloc((void**)&c->keys_a, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
+        if (hipMalloc((void**)&c->keys_b, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
+        if (hipMalloc((void**)&c->rec_cursor, 8) != hipSuccess) return bail(KC_ERR_NOMEM);
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->n_cu = prop.multiProcessorCount;
+    }
     s = kc_reset(c);
     if (s) return bail(s);
     *out = c;
@@ -416,6 +614,16 @@ void kc_destroy(kc_ctx* c) {
     for (DevBuf* b : bufs) release(*b);
     if (c->table) (void)hipFree(c->table);
     if (c->spill) (void)hipFree(c->spill);
+    if (c->keys_a) (void)hipFree(c->keys_a);
+    if (c->keys_b) (void)hipFree(c->keys_b);
+    if (c->rec_keys) (void)hipFree(c->rec_keys);
+    if (c->rec_cnts) (void)hipFree(c->rec_cnts);
+    if (c->rec_cursor) (void)hipFree(c->rec_cursor);
+    release(c->part_hist);
+    release(c->part_base);
+    release(c->part_tmp);
+    release(c->part_starts);
+    release(c->part_sort_hist);
     if (c->stats) (void)hipFree(c->stats);
     if (c->stats_h) (void)hipHostFree(c->stats_h);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -429,8 +637,12 @@ kc_status kc_reset(kc_ctx* c) {
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
     HIPCHK(c, hipMemsetAsync(c->stats, 0, ST_N * 8, c->stream));
+    if (c->rec_cursor) HIPCHK(c, hipMemsetAsync(c->rec_cursor, 0, 8, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     memset(c->stats_h, 0, ST_N * 8);
+    c->rec_n = 0;
+    c->batches = 0;
+    for (double& x : c->part_ms) x = 0;
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
@@ -503,6 +715,72 @@ kc_status kc_check_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, ui
     return fastq_host(c, fastq, n, L, n_reads, false);
 }
 
+// Finish of the partition engine: LDS records + fallback-table records + key 0
+// -> radix sort -> (sum duplicates when several batches or the fallback table
+// contributed) -> pack.
+static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
+    kc_status s;
+    const int W = c->W;
+    const uint64_t nrec = c->rec_n;
+    const uint64_t claimed = c->stats_h[ST_CLAIMED];
+    const uint64_t out_cap = nrec + claimed + 1;
+    for (int i = 0; i < 2; i++) {
+        if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
+            return s;
+    }
+    if ((s = ensure(c, c->fin_misc, (2 * W + 1 + compact_tmp_elems()) * 8))) return s;
+    uint64_t* k0 = (uint64_t*)c->fin_keys[0].p;
+    uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
+    uint64_t* cursor = (uint64_t*)c->fin_misc.p + 2 * W;
+    if (nrec) {
+        for (int j = 0; j < W; j++)
+            HIPCHK(c, hipMemcpyAsync(k0 + (size_t)j * out_cap, c->rec_keys + (size_t)j * c->rec_cap, nrec * 8,
+                                     hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c0, c->rec_cnts, nrec * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    uint64_t t = 0;
+    if (claimed) {
+        HIPCHK(c, launch_compact(W, c->table, c->cap, k0 + nrec, c0 + nrec, out_cap, cursor, cursor + 1, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&t, cursor, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    uint64_t cur = nrec + t;
+    HIPCHK(c, hipMemcpyAsync(cursor, &cur, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_append_key0(W, k0, c0, out_cap, cursor, c->stats, c->stream));
+    uint64_t n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, cursor, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int which = 0;
+    if ((s = sort_records(c, k0, (uint64_t*)c->fin_keys[1].p, c0, (uint32_t*)c->fin_cnts[1].p, out_cap, n, &which)))
+        return s;
+    if ((c->batches > 1 || t > 0) && n > 1) {
+        uint64_t* ks = (uint64_t*)c->fin_keys[which].p;
+        uint32_t* cs = (uint32_t*)c->fin_cnts[which].p;
+        uint64_t* ko = (uint64_t*)c->fin_keys[which ^ 1].p;
+        uint32_t* co = (uint32_t*)c->fin_cnts[which ^ 1].p;
+        if ((s = ensure(c, c->rle_flags, n * 4)) || (s = ensure(c, c->rle_pos, n * 4)) ||
+            (s = ensure(c, c->rle_tmp, scan_tmp_elems(n) * 4)))
+            return s;
+        HIPCHK(c, launch_rle_heads(W, ks, out_cap, n, (uint32_t*)c->rle_flags.p, c->stream));
+        HIPCHK(c, launch_scan_u32((uint32_t*)c->rle_flags.p, (uint32_t*)c->rle_pos.p, n, (uint32_t*)c->rle_tmp.p,
+                                  c->stream));
+        uint32_t last[2];
+        HIPCHK(c, hipMemcpyAsync(&last[0], (uint32_t*)c->rle_pos.p + (n - 1), 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&last[1], (uint32_t*)c->rle_flags.p + (n - 1), 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemsetAsync(co, 0, n * 4, c->stream));
+        HIPCHK(c, launch_reduce_add(W, ks, out_cap, cs, n, (uint32_t*)c->rle_flags.p, (uint32_t*)c->rle_pos.p, ko,
+                                    out_cap, co, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        n = (uint64_t)last[0] + last[1];
+        which ^= 1;
+    }
+    if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
+    HIPCHK(c, launch_pack(W, (uint64_t*)c->fin_keys[which].p, out_cap, (uint32_t*)c->fin_cnts[which].p, n,
+                          c->fin_packed.p, c->stream));
+    *n_out = n;
+    return KC_OK;
+}
+
 kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     if (!c) return KC_ERR_ARG;
     if (c->finished) {
@@ -516,15 +794,29 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     const int W = c->W;
     uint64_t out_cap = c->stats_h[ST_CLAIMED] + 1;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if (c->part) {
+        uint64_t n = 0;
+        if ((s = finish_part(c, &n))) return s;
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        float tf = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&tf, c->ev0, c->ev1));
+        c->st.finish_ms += tf;
+        c->n_records = n;
+        c->finished = true;
+        c->st.table_used = c->stats_h[ST_CLAIMED];
+        c->st.output_records = n;
+        if (n_records) *n_records = n;
+        return KC_OK;
+    }
     for (int i = 0; i < 2; i++) {
         if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
             return s;
     }
-    if ((s = ensure(c, c->fin_misc, 2 * W * 8 + 8))) return s;
+    if ((s = ensure(c, c->fin_misc, (2 * W + 1 + compact_tmp_elems()) * 8))) return s;
     uint64_t* cursor = (uint64_t*)c->fin_misc.p + 2 * W;
-    HIPCHK(c, hipMemsetAsync(cursor, 0, 8, c->stream));
     HIPCHK(c, launch_compact(W, c->table, c->cap, (uint64_t*)c->fin_keys[0].p, (uint32_t*)c->fin_cnts[0].p, out_cap,
-                             cursor, c->stream));
+                             cursor, cursor + 1, c->stream));
     HIPCHK(c, launch_append_key0(W, (uint64_t*)c->fin_keys[0].p, (uint32_t*)c->fin_cnts[0].p, out_cap, cursor,
                                  c->stats, c->stream));
     uint64_t n = 0;
@@ -666,6 +958,8 @@ kc_status kc_write_runs(kc_ctx* c, const char* prefix, uint32_t* n_runs) {
 kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     if (!c || !out) return KC_ERR_ARG;
     *out = c->st;
+    for (int i = 0; i < 5; i++) out->part_ms[i] = c->part_ms[i];
+    out->batches = c->batches;
     out->table_capacity = c->cap;
     out->valid_kmers = c->stats_h[ST_VALID];
     out->spill_runs = c->runs.size();

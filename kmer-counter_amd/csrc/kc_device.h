@@ -15,7 +15,7 @@ enum Stat : int {
     ST_CLAIMED = 4,      // table slots claimed (= occupied)
     ST_ERR = 5,          // bit set: ERR_* below
     ST_SPILL_FILL = 6,   // next free spill index (may exceed capacity on overflow)
-    ST_NL_TOTAL = 7,     // FASTQ block: total newlines
+    ST_SPILL2_FILL = 7,  // partition engine P5: keys spilled into the free key buffer
     ST_N = 16
 };
 
@@ -25,7 +25,8 @@ enum ErrBits : uint64_t {
     ERR_FQ_NO_PLUS = 4,     // line after the sequence does not start with '+'
     ERR_FQ_SEQ_LEN = 8,     // sequence line length != L
     ERR_FQ_TOO_MANY = 16,   // more records than the index buffer holds
-    ERR_FQ_NO_FINAL_NL = 32 // block does not end with '\n'
+    ERR_FQ_NO_FINAL_NL = 32, // block does not end with '\n'
+    ERR_REC_OVERFLOW = 64    // partition engine: record buffer too small
 };
 
 // Slot stride (uint64 words) of the open-addressed table for W key words:
@@ -58,9 +59,44 @@ CountGeom count_geometry(int L, int k);
 
 hipError_t launch_count_kmers(const CountLaunch& a, int grid_cap, hipStream_t s);
 
-// Table -> dense SoA (keys W x out_cap words, counts); cursor = device u64.
+// ---- partition engine ----
+// P1/P2 segment geometry for a launch of n_reads reads.
+struct PartGeom {
+    CountGeom geom;    // tile geometry shared by P1 and P2
+    int seg_tiles;     // tiles per segment
+    uint64_t nseg;     // segments (histogram columns)
+    int max_win;       // windows per tile
+    size_t lds_scatter;// LDS bytes of the P2 workgroup
+};
+PartGeom part_geometry(int L, int k, uint64_t n_reads);
+// P1: hist[d * nseg + seg] = keys of segment seg with digit d = (hash >> shift) & 255
+hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* hist, int shift, hipStream_t s);
+// P2: scatter keys to out (SoA, out_stride) at base = exclusive scan of hist;
+// also counts key 0 / holes / valid windows into l.stats
+hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
+                               uint64_t out_stride, int shift, hipStream_t s);
+// P4: starts[b] for b in [0, 2^bits]: first key index of bucket b (= hash >> (64 - bits))
+hipError_t launch_bucket_bounds(int W, const uint64_t* keys, uint64_t stride, uint64_t n, int bits, uint64_t* starts,
+                                hipStream_t s);
+// P5: LDS counting per bucket -> records (SoA, rec_cap stride) at *rec_cursor;
+// LDS overflow -> global table -> spill (SoA, spill_cap stride) counted in
+// stats[ST_SPILL2_FILL]
+int bucket_lds_slots(int W);
+hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, const uint64_t* starts,
+                                uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                                uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
+                                uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
+                                hipStream_t s);
+// segmented sum of sorted records (out_cnts zeroed by the caller)
+hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n,
+                             const uint32_t* flags, const uint32_t* pos, uint64_t* out_keys, uint64_t ostride,
+                             uint32_t* out_cnts, hipStream_t s);
+
+// Table -> dense SoA (keys W x out_cap words, counts) in slot order; *cursor
+// (device u64) receives the number of records. tmp: compact_tmp_elems() u64.
 hipError_t launch_compact(int W, const uint64_t* table, uint64_t cap, uint64_t* keys, uint32_t* cnts,
-                          uint64_t out_cap, uint64_t* cursor, hipStream_t s);
+                          uint64_t out_cap, uint64_t* cursor, uint64_t* tmp, hipStream_t s);
+uint64_t compact_tmp_elems();
 // Appends (0^W, stats[ST_KEY0]) at index *cursor when stats[ST_KEY0_PRESENT].
 hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t out_cap, uint64_t* cursor,
                               const uint64_t* stats, hipStream_t s);
@@ -70,11 +106,13 @@ hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t ou
 hipError_t launch_key_bits(int W, const uint64_t* keys, uint64_t stride, uint64_t n, uint64_t* bits, hipStream_t s);
 
 // One LSD pass on digit (word, shift) of SoA records: keys (W arrays at
-// `stride`), optional vals. hist must hold 256 * grid u32. Returns the grid used.
+// `stride`), optional vals. hist must hold sort_hist_elems(grid) u64.
 int sort_grid(uint64_t n);
+uint64_t sort_hist_elems(int grid);
+// hashed: the digit is taken from the key hash instead of key word `word`.
 hipError_t launch_sort_pass(int W, const uint64_t* keys_in, uint64_t* keys_out, const uint32_t* vals_in,
-                            uint32_t* vals_out, uint64_t stride, uint64_t n, int word, int shift, uint32_t* hist,
-                            int grid, hipStream_t s);
+                            uint32_t* vals_out, uint64_t stride, uint64_t n, int word, int shift, uint64_t* hist,
+                            int grid, bool hashed, hipStream_t s);
 
 // Exclusive scan of n elements (device-wide); tmp must hold scan_tmp_elems(n).
 uint64_t scan_tmp_elems(uint64_t n);

@@ -142,15 +142,19 @@ CountGeom count_geometry(int L, int k) {
 }
 
 // W == 1: slot = {key, count}. Returns true when counted; *claimed when this
-// insert took an empty slot.
+// insert took an empty slot. A key word only ever changes 0 -> key, so a plain
+// (possibly stale) load can only be wrong in the EMPTY direction: a non-zero
+// value is the slot's final key and a repeat costs one atomic (the count add);
+// an EMPTY reading is confirmed or corrected by the CAS.
 __device__ __forceinline__ bool insert_w1(u64 key, u64* __restrict__ table, u64 cap, u32 limit, bool* claimed) {
     u64 s = __umul64hi(mix64(key ^ 0x9e3779b97f4a7c15ull), cap);
     for (u32 pr = 0; pr < limit; ++pr) {
         u64* slot = table + 2 * s;
-        u64 old = atomicCAS((unsigned long long*)slot, 0ull, (unsigned long long)key);
-        if (old == 0ull || old == key) {
+        u64 cur = __builtin_nontemporal_load(slot);
+        if (cur == 0ull) cur = atomicCAS((unsigned long long*)slot, 0ull, (unsigned long long)key);
+        if (cur == 0ull || cur == key) {
             atomicAdd((unsigned int*)(slot + 1), 1u);
-            *claimed = (old == 0ull);
+            *claimed = (cur == 0ull);
             return true;
         }
         if (++s == cap) s = 0;
@@ -227,14 +231,54 @@ __device__ __forceinline__ u32 bytes_to_codes(u32 word, int nvalid, u32* bad_bit
     return codes;
 }
 
-template <int W>
-__global__ __launch_bounds__(kBlock) void count_kmers(CountArgs a) {
+// Sinks of the count front end (stages 1-3 above are shared):
+//   SINK_TABLE   : insert into the global open-addressed table (engine "table")
+//   SINK_HIST    : per-segment histogram of the partition digit (engine
+//                  "partition", pass P1); no statistics are touched
+//   SINK_SCATTER : per-tile LDS counting sort by the digit, then coalesced
+//                  writes of the keys to their segment's slice of each digit's
+//                  region (pass P2)
+enum Sink { SINK_TABLE = 0, SINK_HIST = 1, SINK_SCATTER = 2 };
+
+struct PartArgs {
+    u64* hist;        // HIST: counts[d * nseg + seg]
+    const u64* base;  // SCATTER: exclusive scan of hist (global key positions)
+    u64* out;         // SCATTER: keys, SoA with out_stride
+    u64 out_stride;
+    u64 nseg;
+    int seg_tiles;    // tiles per segment
+    int shift;        // digit = (hash >> shift) & 255
+    int max_win;      // SCATTER staging capacity (R * windows per read)
+};
+
+static size_t sink_lds_host(int W, int sink, int max_win) {
+    if (sink == SINK_HIST) return 256 * 4;
+    if (sink == SINK_SCATTER)
+        return (size_t)256 * 4 * 3 + 256 * 8 + 32 + (size_t)2 * W * 8 * max_win + (size_t)2 * 4 * max_win;
+    return 0;
+}
+
+template <int W, int SINK>
+__global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* raw = smem;
     u32* codes = (u32*)(smem + (size_t)a.R * a.raw_stride);
     u32* inval = codes + a.R * a.NG;
     u32* lead = inval + a.R * a.NG;
     u32* rflag = lead + a.R;
+    // sink region (16-byte aligned)
+    unsigned char* sk = (unsigned char*)(((uintptr_t)(rflag + a.R) + 15) & ~(uintptr_t)15);
+    u32* s_hist = (u32*)sk;                      // HIST
+    u32* s_cnt = (u32*)sk;                       // SCATTER: per-digit count in tile
+    u32* s_start = s_cnt + 256;                  //          tile-local start
+    u32* s_fill = s_start + 256;                 //          fill cursor
+    u64* s_cur = (u64*)(s_fill + 256);           //          global cursor of the segment
+    u32* s_misc = (u32*)(s_cur + 256);           //          [0] staged count, [4..7] scan scratch
+    u64* s_stage = (u64*)(s_misc + 8);           //          W x max_win staged keys
+    u64* s_sorted = s_stage + (size_t)W * pa.max_win;
+    u32* s_sdig = (u32*)(s_sorted + (size_t)W * pa.max_win);
+    u32* s_odig = s_sdig + pa.max_win;
+    u32* scan_tmp = s_misc + 4;
 
     const int tid = threadIdx.x;
     const int L = a.L, k = a.k, NG = a.NG;
@@ -243,146 +287,218 @@ __global__ __launch_bounds__(kBlock) void count_kmers(CountArgs a) {
     const u64 last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
     const int nch = (L + 30) / 16 + 1;  // 16 B chunks covering lead (<16) + L bytes
     const u64 ntiles = (a.n_reads + a.R - 1) / a.R;
+    const u64 per_unit = (SINK == SINK_TABLE) ? 1 : (u64)pa.seg_tiles;
+    const u64 nunits = (ntiles + per_unit - 1) / per_unit;
 
     u64 my_valid = 0;
     bool my_hole = false;
 
-    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const u64 r0 = tile * (u64)a.R;
-        const int nr = (int)min((u64)a.R, a.n_reads - r0);
-
-        // 1. stage the raw text of the tile's reads into LDS
-        for (int it = tid; it < nr * nch; it += kBlock) {
-            int r = it / nch, c = it - r * nch;
-            u64 gr = a.read0 + r0 + (u64)r;
-            u64 off = a.seq_off ? a.seq_off[gr] : gr * (u64)L;
-            uintptr_t addr = (uintptr_t)(a.base + off);
-            int ld = (int)(addr & 15);
-            if (c == 0) lead[r] = (u32)ld;
-            if (16 * c < ld + L) {
-                const uint4 v = *(const uint4*)((addr & ~(uintptr_t)15) + 16 * (uintptr_t)c);
-                *(uint4*)(raw + (size_t)r * a.raw_stride + 16 * c) = v;
-            }
+    for (u64 unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
+        if constexpr (SINK == SINK_HIST) {
+            s_hist[tid] = 0;
+        } else if constexpr (SINK == SINK_SCATTER) {
+            s_cnt[tid] = 0;
+            s_cur[tid] = pa.base[(u64)tid * pa.nseg + unit];
+            if (tid == 0) s_misc[0] = 0;
         }
-        if (tid < nr) rflag[tid] = 0;
-        __syncthreads();
+        const u64 t_end = min(ntiles, (unit + 1) * per_unit);
+        for (u64 tile = unit * per_unit; tile < t_end; tile++) {
+            const u64 r0 = tile * (u64)a.R;
+            const int nr = (int)min((u64)a.R, a.n_reads - r0);
 
-        // 2. encode 16-base groups
-        for (int it = tid; it < nr * NG; it += kBlock) {
-            int r = it / NG, g = it - r * NG;
-            int i0 = 16 * g;
-            u32 cw = 0, iv = 0;
-            if (i0 < L) {
-                int pos = (int)lead[r] + i0;
-                const u32* dw = (const u32*)(raw + (size_t)r * a.raw_stride) + (pos >> 2);
-                int sh = pos & 3;
-                u32 d0 = dw[0], d1 = dw[1], d2 = dw[2], d3 = dw[3], d4 = dw[4];
-                u32 x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                u32 x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                u32 x2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-                u32 x3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-                int left = L - i0;
-                u32 b0, b1, b2, b3;
-                u32 c0 = bytes_to_codes(x0, left, &b0);
-                u32 c1 = bytes_to_codes(x1, left - 4, &b1);
-                u32 c2 = bytes_to_codes(x2, left - 8, &b2);
-                u32 c3 = bytes_to_codes(x3, left - 12, &b3);
-                cw = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
-                iv = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
-            }
-            codes[it] = cw;
-            inval[it] = iv;
-            if (iv) atomicOr(&rflag[r], 1u);
-        }
-        __syncthreads();
-
-        // 3. windows -> keys -> table
-        const int total = nr * nw;
-        int r = tid / nw, p = tid - (tid / nw) * nw;
-        for (int it = tid; it - (tid & 63) < total; it += kBlock) {
-            // the loop bound is wave-uniform so every lane reaches the ballots
-            const bool active = it < total;
-            u64 key[W];
-            bool valid = false;
-            if (active) {
-                const u32* cr = codes + r * NG;
-                const int g = p >> 4, o = p & 15;
-#pragma unroll
-                for (int j = 0; j < W; j++) {
-                    const int gg = g + 2 * j;
-                    u64 hi = ((u64)cr[gg] << 32) | (u64)cr[gg + 1];
-                    u64 w = o ? ((hi << (2 * o)) | (u64)(cr[gg + 2] >> (32 - 2 * o))) : hi;
-                    key[j] = w;
+            // 1. stage the raw text of the tile's reads into LDS
+            for (int it = tid; it < nr * nch; it += kBlock) {
+                int r = it / nch, c = it - r * nch;
+                u64 gr = a.read0 + r0 + (u64)r;
+                u64 off = a.seq_off ? a.seq_off[gr] : gr * (u64)L;
+                uintptr_t addr = (uintptr_t)(a.base + off);
+                int ld = (int)(addr & 15);
+                if (c == 0) lead[r] = (u32)ld;
+                if (16 * c < ld + L) {
+                    const uint4 v = *(const uint4*)((addr & ~(uintptr_t)15) + 16 * (uintptr_t)c);
+                    *(uint4*)(raw + (size_t)r * a.raw_stride + 16 * c) = v;
                 }
-                key[W - 1] &= last_mask;
-                valid = true;
-                if (rflag[r]) {
-                    const u32* ir = inval + r * NG;
-                    const int last = p + k - 1;
-                    for (int gg = p >> 4; gg <= (last >> 4); gg++) {
-                        int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
-                        u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
-                        if (ir[gg] & rm) valid = false;
+            }
+            if (tid < nr) rflag[tid] = 0;
+            __syncthreads();
+
+            // 2. encode 16-base groups
+            for (int it = tid; it < nr * NG; it += kBlock) {
+                int r = it / NG, g = it - r * NG;
+                int i0 = 16 * g;
+                u32 cw = 0, iv = 0;
+                if (i0 < L) {
+                    int pos = (int)lead[r] + i0;
+                    const u32* dw = (const u32*)(raw + (size_t)r * a.raw_stride) + (pos >> 2);
+                    int sh = pos & 3;
+                    u32 d0 = dw[0], d1 = dw[1], d2 = dw[2], d3 = dw[3], d4 = dw[4];
+                    u32 x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                    u32 x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    u32 x2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                    u32 x3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+                    int left = L - i0;
+                    u32 b0, b1, b2, b3;
+                    u32 c0 = bytes_to_codes(x0, left, &b0);
+                    u32 c1 = bytes_to_codes(x1, left - 4, &b1);
+                    u32 c2 = bytes_to_codes(x2, left - 8, &b2);
+                    u32 c3 = bytes_to_codes(x3, left - 12, &b3);
+                    cw = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+                    iv = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
+                }
+                codes[it] = cw;
+                inval[it] = iv;
+                if (iv) atomicOr(&rflag[r], 1u);
+            }
+            __syncthreads();
+
+            // 3. windows -> keys -> sink
+            const int total = nr * nw;
+            int r = tid / nw, p = tid - (tid / nw) * nw;
+            for (int it = tid; it - (tid & 63) < total; it += kBlock) {
+                // the loop bound is wave-uniform so every lane reaches the ballots
+                const bool active = it < total;
+                u64 key[W];
+                bool valid = false;
+                if (active) {
+                    const u32* cr = codes + r * NG;
+                    const int g = p >> 4, o = p & 15;
+#pragma unroll
+                    for (int j = 0; j < W; j++) {
+                        const int gg = g + 2 * j;
+                        u64 hi = ((u64)cr[gg] << 32) | (u64)cr[gg + 1];
+                        u64 w = o ? ((hi << (2 * o)) | (u64)(cr[gg + 2] >> (32 - 2 * o))) : hi;
+                        key[j] = w;
+                    }
+                    key[W - 1] &= last_mask;
+                    valid = true;
+                    if (rflag[r]) {
+                        const u32* ir = inval + r * NG;
+                        const int last = p + k - 1;
+                        for (int gg = p >> 4; gg <= (last >> 4); gg++) {
+                            int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
+                            u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
+                            if (ir[gg] & rm) valid = false;
+                        }
+                    }
+                    my_hole |= !valid;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < W; j++) key[j] = 0;
+                }
+                bool is_zero = true;
+#pragma unroll
+                for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
+                const bool live = valid && !is_zero;
+
+                if constexpr (SINK == SINK_HIST) {
+                    if (live) atomicAdd(&s_hist[(u32)(hash_key<W>(key) >> pa.shift) & 255u], 1u);
+                } else {
+                    // key 0^W: one atomic per wave
+                    u64 zmask = __ballot(valid && is_zero);
+                    if (zmask) {
+                        if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
+                            atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
+                            atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                        }
+                    }
+                    if (valid) my_valid++;
+                }
+                if constexpr (SINK == SINK_SCATTER) {
+                    // stage the key (wave-aggregated LDS reservation)
+                    u64 m = __ballot(live);
+                    u32 base = 0;
+                    if (m) {
+                        int leader = __ffsll((long long)m) - 1;
+                        if ((int)lane_id() == leader) base = atomicAdd(&s_misc[0], (u32)__popcll(m));
+                        base = __shfl(base, leader);
+                    }
+                    if (live) {
+                        u32 idx = base + (u32)__popcll(m & lanemask_lt());
+#pragma unroll
+                        for (int j = 0; j < W; j++) s_stage[(size_t)j * pa.max_win + idx] = key[j];
+                        s_sdig[idx] = (u32)(hash_key<W>(key) >> pa.shift) & 255u;
                     }
                 }
-                my_hole |= !valid;
-            } else {
+                if constexpr (SINK == SINK_TABLE) {
+                    bool done = true, claimed = false;
+                    if (live) {
+                        if constexpr (W == 1)
+                            done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
+                        else
+                            done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
+                    }
+                    u64 cm = __ballot(claimed);
+                    if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                        atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+                    // spill: wave-aggregated reservation in the spill buffer
+                    bool spill = !done;
+                    if (__ballot(spill)) {
+                        u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
+                        if (spill) {
+                            if (idx < a.spill_cap) {
 #pragma unroll
-                for (int j = 0; j < W; j++) key[j] = 0;
-            }
-            bool is_zero = true;
-#pragma unroll
-            for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
-            // key 0^W: one atomic per wave
-            u64 zmask = __ballot(valid && is_zero);
-            if (zmask) {
-                if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
-                    atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
-                    atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
-                }
-            }
-            bool done = true, claimed = false;
-            if (valid) {
-                my_valid++;
-                if (!is_zero) {
-                    if constexpr (W == 1)
-                        done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
-                    else
-                        done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
-                }
-            }
-            u64 cm = __ballot(claimed);
-            if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
-                atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-            // spill: wave-aggregated reservation in the spill buffer
-            bool spill = !done;
-            if (__ballot(spill)) {
-                u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
-                if (spill) {
-                    if (idx < a.spill_cap) {
-#pragma unroll
-                        for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
-                    } else {
-                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                                for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
+                            } else {
+                                atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                            }
+                        }
                     }
                 }
+                // advance to this lane's next window (stride 256 windows)
+                p += kBlock;
+                while (p >= nw) {
+                    p -= nw;
+                    r++;
+                }
             }
-            // advance to this lane's next window (stride 256 windows)
-            p += kBlock;
-            while (p >= nw) {
-                p -= nw;
-                r++;
+            __syncthreads();
+
+            if constexpr (SINK == SINK_SCATTER) {
+                // LDS counting sort of the staged keys by digit, then writes in
+                // digit order: consecutive lanes -> consecutive addresses of a
+                // digit's run in this segment's slice
+                const u32 n = s_misc[0];
+                for (u32 i = tid; i < n; i += kBlock) atomicAdd(&s_cnt[s_sdig[i]], 1u);
+                __syncthreads();
+                u32 tot;
+                u32 st = block_excl_scan(s_cnt[tid], scan_tmp, &tot);
+                s_start[tid] = st;
+                s_fill[tid] = st;
+                __syncthreads();
+                for (u32 i = tid; i < n; i += kBlock) {
+                    u32 d = s_sdig[i];
+                    u32 q = atomicAdd(&s_fill[d], 1u);
+#pragma unroll
+                    for (int j = 0; j < W; j++) s_sorted[(size_t)j * pa.max_win + q] = s_stage[(size_t)j * pa.max_win + i];
+                    s_odig[q] = d;
+                }
+                __syncthreads();
+                for (u32 q = tid; q < n; q += kBlock) {
+                    u32 d = s_odig[q];
+                    u64 g = s_cur[d] + (q - s_start[d]);
+#pragma unroll
+                    for (int j = 0; j < W; j++) pa.out[(u64)j * pa.out_stride + g] = s_sorted[(size_t)j * pa.max_win + q];
+                }
+                __syncthreads();
+                s_cur[tid] += s_cnt[tid];
+                s_cnt[tid] = 0;
+                if (tid == 0) s_misc[0] = 0;
+                __syncthreads();
             }
         }
-        __syncthreads();
+        if constexpr (SINK == SINK_HIST) {
+            __syncthreads();
+            pa.hist[(u64)tid * pa.nseg + unit] = s_hist[tid];
+            __syncthreads();
+        }
     }
-    wave_add(&a.stats[ST_VALID], my_valid);
-    if (__ballot(my_hole) && lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+    if constexpr (SINK != SINK_HIST) {
+        wave_add(&a.stats[ST_VALID], my_valid);
+        if (__ballot(my_hole) && lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+    }
 }
 
-hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s) {
-    if (l.n_reads == 0) return hipSuccess;
-    CountGeom g = count_geometry(l.L, l.k);
+static CountArgs make_args(const CountLaunch& l, const CountGeom& g) {
     CountArgs a;
     a.base = l.base;
     a.seq_off = l.seq_off;
@@ -399,51 +515,175 @@ hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s)
     a.spill_cap = l.spill_cap;
     a.stats = l.stats;
     a.probe_limit = l.probe_limit;
+    return a;
+}
+
+#define KC_FRONT_SWITCH(SINKV, GRID, LDS, S, A, PA)                                                                  \
+    switch (W) {                                                                                                     \
+    case 1: hipLaunchKernelGGL((count_front<1, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
+    case 2: hipLaunchKernelGGL((count_front<2, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
+    case 3: hipLaunchKernelGGL((count_front<3, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
+    case 4: hipLaunchKernelGGL((count_front<4, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
+    default: return hipErrorInvalidValue;                                                                            \
+    }
+
+hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s) {
+    if (l.n_reads == 0) return hipSuccess;
+    CountGeom g = count_geometry(l.L, l.k);
+    CountArgs a = make_args(l, g);
+    PartArgs pa;
+    PartArgs zero_pa = {};
+    pa = zero_pa;
     u64 tiles = (l.n_reads + g.R - 1) / g.R;
     int grid = (int)hmin(tiles, (u64)grid_cap);
     int W = (l.k + 31) / 32;
-    switch (W) {
-    case 1: hipLaunchKernelGGL(count_kmers<1>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
-    case 2: hipLaunchKernelGGL(count_kmers<2>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
-    case 3: hipLaunchKernelGGL(count_kmers<3>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
-    case 4: hipLaunchKernelGGL(count_kmers<4>, dim3(grid), dim3(kBlock), g.lds, s, a); break;
-    default: return hipErrorInvalidValue;
-    }
+    KC_FRONT_SWITCH(SINK_TABLE, grid, g.lds, s, a, pa)
     return hipGetLastError();
 }
+
+PartGeom part_geometry(int L, int k, uint64_t n_reads) {
+    PartGeom p;
+    CountGeom g = count_geometry(L, k);
+    // P1 and P2 share this tile geometry; R is limited so that P2's staging
+    // (two W-word key copies + digits per window) keeps the block <= ~72 KiB
+    // (two workgroups per CU)
+    const int W = (k + 31) / 32;
+    const int nw = L - k + 1;
+    auto lds = [&](int r) {
+        size_t front = (size_t)r * g.raw_stride + (size_t)r * g.NG * 8 + (size_t)r * 8 + 16;
+        return ((front + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, r * nw);
+    };
+    while (g.R > 1 && lds(g.R) > 72 * 1024) g.R--;
+    g.lds = (((size_t)g.R * g.raw_stride + (size_t)g.R * g.NG * 8 + (size_t)g.R * 8 + 16) + 15) & ~(size_t)15;
+    p.geom = g;
+    u64 tiles = (n_reads + g.R - 1) / g.R;
+    u64 seg_tiles = (tiles + 16383) / 16384;
+    if (seg_tiles < 4) seg_tiles = 4;
+    p.seg_tiles = (int)seg_tiles;
+    p.nseg = (tiles + seg_tiles - 1) / seg_tiles;
+    p.max_win = g.R * nw;
+    p.lds_scatter = lds(g.R);
+    return p;
+}
+
+hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* hist, int shift, hipStream_t s) {
+    if (l.n_reads == 0) return hipSuccess;
+    const CountGeom& g = pg.geom;
+    CountArgs a = make_args(l, g);
+    int W = (l.k + 31) / 32;
+    PartArgs pa;
+    PartArgs zero_pa = {};
+    pa = zero_pa;
+    pa.hist = hist;
+    pa.nseg = pg.nseg;
+    pa.seg_tiles = pg.seg_tiles;
+    pa.shift = shift;
+    pa.max_win = pg.max_win;
+    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_HIST, pg.max_win);
+    int grid = (int)hmin(pg.nseg, 4096);
+    KC_FRONT_SWITCH(SINK_HIST, grid, lds, s, a, pa)
+    return hipGetLastError();
+}
+
+hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
+                               uint64_t out_stride, int shift, hipStream_t s) {
+    if (l.n_reads == 0) return hipSuccess;
+    const CountGeom& g = pg.geom;
+    CountArgs a = make_args(l, g);
+    int W = (l.k + 31) / 32;
+    PartArgs pa;
+    PartArgs zero_pa = {};
+    pa = zero_pa;
+    pa.base = base;
+    pa.out = out;
+    pa.out_stride = out_stride;
+    pa.nseg = pg.nseg;
+    pa.seg_tiles = pg.seg_tiles;
+    pa.shift = shift;
+    pa.max_win = pg.max_win;
+    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.max_win);
+    int grid = (int)hmin(pg.nseg, 4096);
+    KC_FRONT_SWITCH(SINK_SCATTER, grid, lds, s, a, pa)
+    return hipGetLastError();
+}
+
+#undef KC_FRONT_SWITCH
 
 // ---------------------------------------------------------------------------
 // K3: compact — occupied slots -> dense SoA records (order is arbitrary; the
 // radix sort fixes it).
 // ---------------------------------------------------------------------------
 
+template <typename T>
+static hipError_t scan_impl(const T* in, T* out, u64 n, T* tmp, hipStream_t s);
+
+__global__ void sum_last(const u64* base, const u64* counts, int n, u64* out) { *out = base[n - 1] + counts[n - 1]; }
+
+constexpr int kCompactGrid = 4096;
+
+__device__ __forceinline__ void compact_range(u64 cap, int grid, int b, u64* lo, u64* hi) {
+    u64 per = ((cap + grid - 1) / grid + kBlock - 1) / kBlock * kBlock;
+    *lo = min(cap, (u64)b * per);
+    *hi = min(cap, *lo + per);
+}
+
 template <int W>
-__global__ __launch_bounds__(kBlock) void compact_table(const u64* __restrict__ table, u64 cap,
-                                                        u64* __restrict__ keys, u32* __restrict__ cnts, u64 out_cap,
-                                                        u64* cursor) {
+__device__ __forceinline__ bool slot_occupied(const u64* slot) {
+    if constexpr (W == 1)
+        return slot[0] != 0ull;
+    else
+        return (u32)(slot[W] >> 32) == 2u;
+}
+
+// pass 1: occupied slots per block range
+template <int W>
+__global__ __launch_bounds__(kBlock) void compact_count(const u64* __restrict__ table, u64 cap,
+                                                        u64* __restrict__ block_counts) {
     constexpr int SW = (W == 1) ? 2 : ((W <= 3) ? 4 : 8);
-    for (u64 b = (u64)blockIdx.x * kBlock; b < cap; b += (u64)gridDim.x * kBlock) {
+    __shared__ u32 part[4];
+    u64 lo, hi;
+    compact_range(cap, gridDim.x, blockIdx.x, &lo, &hi);
+    u32 cnt = 0;
+    for (u64 s = lo + threadIdx.x; s < hi; s += kBlock) cnt += slot_occupied<W>(table + SW * s) ? 1u : 0u;
+    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) block_counts[blockIdx.x] = (u64)part[0] + part[1] + part[2] + part[3];
+}
+
+// pass 2: write occupied slots in slot order at the scanned block offsets
+template <int W>
+__global__ __launch_bounds__(kBlock) void compact_emit(const u64* __restrict__ table, u64 cap,
+                                                       const u64* __restrict__ block_base, u64* __restrict__ keys,
+                                                       u32* __restrict__ cnts, u64 out_cap) {
+    constexpr int SW = (W == 1) ? 2 : ((W <= 3) ? 4 : 8);
+    __shared__ u32 scan_tmp[4];
+    u64 lo, hi;
+    compact_range(cap, gridDim.x, blockIdx.x, &lo, &hi);
+    u64 run = block_base[blockIdx.x];
+    for (u64 b = lo; b < hi; b += kBlock) {
         u64 s = b + threadIdx.x;
         bool occ = false;
         u64 kw[W];
         u32 c = 0;
-        if (s < cap) {
+        if (s < hi) {
             const u64* slot = table + SW * s;
 #pragma unroll
             for (int j = 0; j < W; j++) kw[j] = slot[j];
-            u64 meta = slot[W];
-            c = (u32)meta;
-            if constexpr (W == 1)
-                occ = kw[0] != 0ull;
-            else
-                occ = (u32)(meta >> 32) == 2u;
+            c = (u32)slot[W];
+            occ = slot_occupied<W>(slot);
         }
-        u64 pos = wave_reserve(cursor, occ);
-        if (occ && pos < out_cap) {
+        u32 total;
+        u32 before = block_excl_scan(occ ? 1u : 0u, scan_tmp, &total);
+        if (occ) {
+            u64 pos = run + before;
+            if (pos < out_cap) {
 #pragma unroll
-            for (int j = 0; j < W; j++) keys[(u64)j * out_cap + pos] = kw[j];
-            cnts[pos] = c;
+                for (int j = 0; j < W; j++) keys[(u64)j * out_cap + pos] = kw[j];
+                cnts[pos] = c;
+            }
         }
+        run += total;
     }
 }
 
@@ -459,18 +699,37 @@ __global__ void append_key0(u64* keys, u32* cnts, u64 out_cap, u64* cursor, cons
 }
 
 hipError_t launch_compact(int W, const uint64_t* table, uint64_t cap, uint64_t* keys, uint32_t* cnts,
-                          uint64_t out_cap, uint64_t* cursor, hipStream_t s) {
-    int grid = (int)hmin((cap + kBlock - 1) / kBlock, 8192);
-    if (grid < 1) grid = 1;
+                          uint64_t out_cap, uint64_t* cursor, uint64_t* tmp, hipStream_t s) {
+    // tmp: kCompactGrid block counts + kCompactGrid offsets + 1 scan partial
+    int grid = kCompactGrid;
+    u64* counts = tmp;
+    u64* base = tmp + kCompactGrid;
+    u64* stmp = tmp + 2 * kCompactGrid;
+#define KC_CC(WW) hipLaunchKernelGGL(compact_count<WW>, dim3(grid), dim3(kBlock), 0, s, table, cap, counts)
+#define KC_CE(WW) hipLaunchKernelGGL(compact_emit<WW>, dim3(grid), dim3(kBlock), 0, s, table, cap, (const u64*)base, keys, cnts, out_cap)
     switch (W) {
-    case 1: hipLaunchKernelGGL(compact_table<1>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
-    case 2: hipLaunchKernelGGL(compact_table<2>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
-    case 3: hipLaunchKernelGGL(compact_table<3>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
-    case 4: hipLaunchKernelGGL(compact_table<4>, dim3(grid), dim3(kBlock), 0, s, table, cap, keys, cnts, out_cap, cursor); break;
+    case 1: KC_CC(1); break;
+    case 2: KC_CC(2); break;
+    case 3: KC_CC(3); break;
+    case 4: KC_CC(4); break;
     default: return hipErrorInvalidValue;
     }
+    hipError_t e = scan_impl<u64>(counts, base, (u64)grid, stmp, s);
+    if (e != hipSuccess) return e;
+    switch (W) {
+    case 1: KC_CE(1); break;
+    case 2: KC_CE(2); break;
+    case 3: KC_CE(3); break;
+    case 4: KC_CE(4); break;
+    }
+#undef KC_CC
+#undef KC_CE
+    // cursor = total occupied = base[grid-1] + counts[grid-1]
+    hipLaunchKernelGGL(sum_last, dim3(1), dim3(1), 0, s, base, counts, grid, cursor);
     return hipGetLastError();
 }
+
+uint64_t compact_tmp_elems() { return 2 * kCompactGrid + scan_tmp_elems(kCompactGrid) + 8; }
 
 hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t out_cap, uint64_t* cursor,
                               const uint64_t* stats, hipStream_t s) {
@@ -496,6 +755,8 @@ hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t ou
 constexpr int kSortItems = 8;
 constexpr int kSortTile = kBlock * kSortItems;  // 2048
 
+uint64_t sort_hist_elems(int grid) { return (u64)256 * grid + scan_tmp_elems((u64)256 * grid) + 16; }  // u64
+
 int sort_grid(uint64_t n) {
     u64 tiles = (n + kSortTile - 1) / kSortTile;
     u64 g = tiles < 2048 ? tiles : 2048;
@@ -509,47 +770,48 @@ __device__ __forceinline__ void block_range(u64 n, int grid, int b, u64* lo, u64
     *hi = min(n, (u64)(b + 1) * per * kSortTile);
 }
 
-__global__ __launch_bounds__(kBlock) void sort_upsweep(const u64* __restrict__ kw, u64 n, int shift,
-                                                       u32* __restrict__ hist) {
+template <int W, bool HASHED>
+__device__ __forceinline__ u32 sort_digit(const u64 (&k)[W], int word, int shift) {
+    u64 dw;
+    if constexpr (HASHED) {
+        dw = hash_key<W>(k);
+    } else {
+        dw = k[0];
+#pragma unroll
+        for (int j = 1; j < W; j++)
+            if (j == word) dw = k[j];
+    }
+    return (u32)(dw >> shift) & 255u;
+}
+
+template <int W, bool HASHED>
+__global__ __launch_bounds__(kBlock) void sort_upsweep(const u64* __restrict__ keys, u64 stride, u64 n, int word,
+                                                       int shift, u64* __restrict__ hist) {
     __shared__ u32 h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
     u64 lo, hi;
     block_range(n, gridDim.x, blockIdx.x, &lo, &hi);
-    for (u64 i = lo + threadIdx.x; i < hi; i += kBlock) atomicAdd(&h[(kw[i] >> shift) & 255u], 1u);
+    for (u64 i = lo + threadIdx.x; i < hi; i += kBlock) {
+        u64 k[W];
+        if constexpr (HASHED) {
+#pragma unroll
+            for (int j = 0; j < W; j++) k[j] = keys[(u64)j * stride + i];
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; j++) k[j] = (j == word) ? keys[(u64)j * stride + i] : 0ull;
+        }
+        atomicAdd(&h[sort_digit<W, HASHED>(k, word, shift)], 1u);
+    }
     __syncthreads();
     hist[(u64)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
-// Single workgroup of 1024 threads: exclusive scan of m u32 in place.
-__global__ __launch_bounds__(1024) void scan_single_u32(u32* data, u64 m) {
-    __shared__ u32 part[1024];
-    const int t = threadIdx.x;
-    u64 per = (m + 1023) / 1024;
-    u64 lo = min(m, (u64)t * per), hi = min(m, lo + per);
-    u32 sum = 0;
-    for (u64 i = lo; i < hi; i++) sum += data[i];
-    part[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        u32 v = (t >= o) ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    u32 run = part[t] - sum;
-    for (u64 i = lo; i < hi; i++) {
-        u32 v = data[i];
-        data[i] = run;
-        run += v;
-    }
-}
-
-template <int W, bool HAS_VALS>
+template <int W, bool HAS_VALS, bool HASHED>
 __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__ kin, u64* __restrict__ kout,
                                                          const u32* __restrict__ vin, u32* __restrict__ vout,
                                                          u64 stride, u64 n, int word, int shift,
-                                                         const u32* __restrict__ hist) {
+                                                         const u64* __restrict__ hist) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* skeys = (u64*)smem;                          // W x kSortTile
     u32* svals = (u32*)(skeys + W * kSortTile);       // kSortTile
@@ -557,8 +819,8 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
     u32* wave_base = wave_cnt + 4 * 256;              // 4 x 256
     u32* digit_run = wave_base + 4 * 256;             // 256: count so far in tile
     u32* digit_start = digit_run + 256;               // 256: tile-local start
-    u32* global_off = digit_start + 256;              // 256: running global offset
-    u32* scan_tmp = global_off + 256;                 // 4
+    u32* scan_tmp = digit_start + 256;                // 4 (+4 pad)
+    u64* global_off = (u64*)(scan_tmp + 8);           // 256: running global offset
 
     const int tid = threadIdx.x, wave = tid >> 6;
     global_off[tid] = hist[(u64)tid * gridDim.x + blockIdx.x];
@@ -580,11 +842,7 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
 #pragma unroll
             for (int j = 0; j < W; j++) kreg[it][j] = ok ? kin[(u64)j * stride + i] : 0ull;
             if constexpr (HAS_VALS) vreg[it] = ok ? vin[i] : 0u;
-            u64 dw = kreg[it][0];
-#pragma unroll
-            for (int j = 1; j < W; j++)
-                if (j == word) dw = kreg[it][j];
-            u32 d = (u32)(dw >> shift) & 255u;
+            u32 d = sort_digit<W, HASHED>(kreg[it], word, shift);
             dreg[it] = d;
             // peers: active lanes with the same digit
             u64 peers = __ballot(ok);
@@ -634,12 +892,8 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
             u64 k0[W];
 #pragma unroll
             for (int j = 0; j < W; j++) k0[j] = skeys[j * kSortTile + pos];
-            u64 dw = k0[0];
-#pragma unroll
-            for (int j = 1; j < W; j++)
-                if (j == word) dw = k0[j];
-            u32 d = (u32)(dw >> shift) & 255u;
-            u64 g = (u64)global_off[d] + (pos - digit_start[d]);
+            u32 d = sort_digit<W, HASHED>(k0, word, shift);
+            u64 g = global_off[d] + (pos - digit_start[d]);
 #pragma unroll
             for (int j = 0; j < W; j++) kout[(u64)j * stride + g] = k0[j];
             if constexpr (HAS_VALS) vout[g] = svals[pos];
@@ -652,31 +906,48 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
 }
 
 hipError_t launch_sort_pass(int W, const uint64_t* keys_in, uint64_t* keys_out, const uint32_t* vals_in,
-                            uint32_t* vals_out, uint64_t stride, uint64_t n, int word, int shift, uint32_t* hist,
-                            int grid, hipStream_t s) {
+                            uint32_t* vals_out, uint64_t stride, uint64_t n, int word, int shift, uint64_t* hist,
+                            int grid, bool hashed, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(sort_upsweep, dim3(grid), dim3(kBlock), 0, s, keys_in + (u64)word * stride, n, shift, hist);
-    hipLaunchKernelGGL(scan_single_u32, dim3(1), dim3(1024), 0, s, hist, (u64)256 * grid);
-    size_t lds = (size_t)W * kSortTile * 8 + (size_t)kSortTile * 4 + (8 * 256 + 3 * 256 + 4) * 4;
-    lds = (lds + 15) & ~(size_t)15;
-    bool hv = vals_in != nullptr;
-#define KC_SORT_CASE(WW)                                                                                           \
-    case WW:                                                                                                       \
-        if (hv)                                                                                                    \
-            hipLaunchKernelGGL((sort_downsweep<WW, true>), dim3(grid), dim3(kBlock), lds, s, keys_in, keys_out,    \
-                               vals_in, vals_out, stride, n, word, shift, hist);                                   \
-        else                                                                                                       \
-            hipLaunchKernelGGL((sort_downsweep<WW, false>), dim3(grid), dim3(kBlock), lds, s, keys_in, keys_out,   \
-                               vals_in, vals_out, stride, n, word, shift, hist);                                   \
-        break;
-    switch (W) {
-        KC_SORT_CASE(1)
-        KC_SORT_CASE(2)
-        KC_SORT_CASE(3)
-        KC_SORT_CASE(4)
+#define KC_UP(WW, HH) hipLaunchKernelGGL((sort_upsweep<WW, HH>), dim3(grid), dim3(kBlock), 0, s, keys_in, stride, n, word, shift, hist)
+    switch (W * 2 + (hashed ? 1 : 0)) {
+    case 2: KC_UP(1, false); break;
+    case 3: KC_UP(1, true); break;
+    case 4: KC_UP(2, false); break;
+    case 5: KC_UP(2, true); break;
+    case 6: KC_UP(3, false); break;
+    case 7: KC_UP(3, true); break;
+    case 8: KC_UP(4, false); break;
+    case 9: KC_UP(4, true); break;
     default: return hipErrorInvalidValue;
     }
-#undef KC_SORT_CASE
+#undef KC_UP
+    {
+        hipError_t e = scan_impl<u64>(hist, hist, (u64)256 * grid, hist + (u64)256 * grid, s);
+        if (e != hipSuccess) return e;
+    }
+    size_t lds = (size_t)W * kSortTile * 8 + (size_t)kSortTile * 4 + (8 * 256 + 2 * 256 + 8) * 4 + 256 * 8;
+    lds = (lds + 15) & ~(size_t)15;
+    bool hv = vals_in != nullptr;
+#define KC_DOWN(WW, HV, HH)                                                                                      \
+    hipLaunchKernelGGL((sort_downsweep<WW, HV, HH>), dim3(grid), dim3(kBlock), lds, s, keys_in, keys_out, vals_in, \
+                       vals_out, stride, n, word, shift, (const u64*)hist)
+#define KC_DOWN_W(WW)                           \
+    case WW:                                    \
+        if (hv && hashed) KC_DOWN(WW, true, true);       \
+        else if (hv) KC_DOWN(WW, true, false);           \
+        else if (hashed) KC_DOWN(WW, false, true);       \
+        else KC_DOWN(WW, false, false);                  \
+        break;
+    switch (W) {
+        KC_DOWN_W(1)
+        KC_DOWN_W(2)
+        KC_DOWN_W(3)
+        KC_DOWN_W(4)
+    default: return hipErrorInvalidValue;
+    }
+#undef KC_DOWN_W
+#undef KC_DOWN
     return hipGetLastError();
 }
 
@@ -929,6 +1200,301 @@ hipError_t launch_pack(int W, const uint64_t* keys, uint64_t stride, const uint3
     case 2: hipLaunchKernelGGL(pack_records<2>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
     case 3: hipLaunchKernelGGL(pack_records<3>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
     case 4: hipLaunchKernelGGL(pack_records<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, (u32*)out); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Partition engine, passes P4/P5: after P2 (scatter by hash digit 48..55) and
+// P3 (stable radix pass by hash digit 56..63) the keys are grouped by bucket =
+// hash >> 48. P4 finds every bucket's range by binary search; P5 counts each
+// bucket in an LDS-resident open-addressed table (one 1024-thread workgroup
+// per CU walks the buckets) and appends the bucket's distinct (key, count)
+// records with one global reservation per bucket. Keys that do not fit the
+// LDS table fall back to the global table (and from there to the spill
+// buffer), so the count stays exact for any input.
+// ---------------------------------------------------------------------------
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void bucket_bounds_k(const u64* __restrict__ keys, u64 stride, u64 n, int bits,
+                                                          u64* __restrict__ starts) {
+    const u64 nb = 1ull << bits;
+    for (u64 b = (u64)blockIdx.x * kBlock + threadIdx.x; b <= nb; b += (u64)gridDim.x * kBlock) {
+        u64 lo = 0, hi = n;
+        while (lo < hi) {
+            u64 mid = (lo + hi) >> 1;
+            u64 k[W];
+#pragma unroll
+            for (int j = 0; j < W; j++) k[j] = keys[(u64)j * stride + mid];
+            if ((hash_key<W>(k) >> (64 - bits)) < b)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        starts[b] = lo;
+    }
+}
+
+hipError_t launch_bucket_bounds(int W, const uint64_t* keys, uint64_t stride, uint64_t n, int bits, uint64_t* starts,
+                                hipStream_t s) {
+    u64 nb = (1ull << bits) + 1;
+    int g = (int)((nb + kBlock - 1) / kBlock);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(bucket_bounds_k<1>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, bits, starts); break;
+    case 2: hipLaunchKernelGGL(bucket_bounds_k<2>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, bits, starts); break;
+    case 3: hipLaunchKernelGGL(bucket_bounds_k<3>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, bits, starts); break;
+    case 4: hipLaunchKernelGGL(bucket_bounds_k<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, n, bits, starts); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+constexpr int kBucketBlock = 1024;
+
+// Exclusive scan across a workgroup of NT threads (NT/64 waves); lds holds
+// NT/64 u32. Returns this thread's exclusive prefix; *total = block sum.
+template <int NT>
+__device__ __forceinline__ u32 block_excl_scan_n(u32 v, u32* lds, u32* total) {
+    constexpr int NW = NT / 64;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    u32 x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        u32 y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wave] = x;
+    __syncthreads();
+    u32 before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        u32 t = lds[w];
+        before += (w < wave) ? t : 0u;
+        tot += t;
+    }
+    *total = tot;
+    __syncthreads();
+    return before + x - v;
+}
+
+int bucket_lds_slots(int W) {
+    // slot: W key words + u32 count (+ u32 state for W >= 2); ~147 KiB per CU
+    int per = 8 * W + 4 + (W >= 2 ? 4 : 0);
+    int slots = (147 * 1024) / per;
+    return slots / kBucketBlock * kBucketBlock;
+}
+
+struct BucketArgs {
+    const u64* keys;
+    u64 stride;
+    const u64* starts;
+    u32 nbuckets;
+    u32 lcap;
+    u64* rec_keys;  // SoA, rec_cap stride
+    u32* rec_cnts;
+    u64 rec_cap;
+    u64* rec_cursor;
+    u64* table;
+    u64 cap;
+    u64* spill;
+    u64 spill_cap;
+    u64* spill_ctr;
+    u64* stats;
+    u32 probe_limit;
+};
+
+template <int W>
+__device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 h, u64* lkeys, u32* lcnt, u32* lstate, u32 lcap) {
+    u32 slot = (u32)(((h & 0xffffffffffffull) * (u64)lcap) >> 48);
+    for (u32 pr = 0; pr < lcap; ++pr) {
+        if constexpr (W == 1) {
+            u64 old = atomicCAS((unsigned long long*)&lkeys[slot], 0ull, (unsigned long long)key[0]);
+            if (old == 0ull || old == key[0]) {
+                atomicAdd(&lcnt[slot], 1u);
+                return true;
+            }
+        } else {
+            u32 st = __hip_atomic_load(&lstate[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (st == 0u) {
+                u32 prev = atomicCAS(&lstate[slot], 0u, 1u);
+                if (prev == 0u) {
+#pragma unroll
+                    for (int j = 0; j < W; j++) lkeys[(size_t)j * lcap + slot] = key[j];
+                    atomicAdd(&lcnt[slot], 1u);
+                    __hip_atomic_store(&lstate[slot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    return true;
+                }
+                st = prev;
+            }
+            u32 spins = 0;
+            while (st == 1u) {
+                if (++spins > (1u << 20)) return false;
+                st = __hip_atomic_load(&lstate[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < W; j++) eq = eq && lkeys[(size_t)j * lcap + slot] == key[j];
+            if (eq) {
+                atomicAdd(&lcnt[slot], 1u);
+                return true;
+            }
+        }
+        if (++slot == lcap) slot = 0;
+    }
+    return false;
+}
+
+template <int W>
+__global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* lkeys = (u64*)smem;                                  // W x lcap
+    u32* lcnt = (u32*)(lkeys + (size_t)W * a.lcap);           // lcap
+    u32* lstate = lcnt + a.lcap;                              // lcap (W >= 2)
+    u32* misc = lstate + (W >= 2 ? a.lcap : 0);               // scan scratch (16) + base (2)
+    const int tid = threadIdx.x;
+    for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+#pragma unroll
+            for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+            lcnt[i] = 0;
+            if constexpr (W >= 2) lstate[i] = 0;
+        }
+        __syncthreads();
+        const u64 lo = a.starts[b], hi = a.starts[b + 1];
+        for (u64 base = lo; base < hi; base += kBucketBlock) {
+            const u64 i = base + tid;
+            u64 key[W];
+            bool live = i < hi;
+            bool done = true, claimed = false;
+            if (live) {
+#pragma unroll
+                for (int j = 0; j < W; j++) key[j] = a.keys[(u64)j * a.stride + i];
+                u64 h = hash_key<W>(key);
+                if (!lds_insert<W>(key, h, lkeys, lcnt, lstate, a.lcap)) {
+                    if constexpr (W == 1)
+                        done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
+                    else
+                        done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < W; j++) key[j] = 0;
+            }
+            u64 cm = __ballot(claimed);
+            if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+            bool spill = !done;
+            if (__ballot(spill)) {
+                u64 idx = wave_reserve(a.spill_ctr, spill);
+                if (spill) {
+                    if (idx < a.spill_cap) {
+#pragma unroll
+                        for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
+                    } else {
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // emit the occupied slots (slot order) after one reservation
+        u32 mine = 0;
+        for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+            bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
+            mine += occ ? 1u : 0u;
+        }
+        u32 total;
+        u32 before = block_excl_scan_n<kBucketBlock>(mine, misc, &total);
+        if (tid == 0) {
+            u64 base = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
+            *(u64*)(misc + 16) = base;
+            if (base + total > a.rec_cap)
+                atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+        }
+        __syncthreads();
+        u64 pos = *(u64*)(misc + 16) + before;
+        // each thread owns slots tid, tid+1024, ... : emit them in that order
+        for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+            bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
+            if (occ) {
+                if (pos < a.rec_cap) {
+#pragma unroll
+                    for (int j = 0; j < W; j++) a.rec_keys[(u64)j * a.rec_cap + pos] = lkeys[(size_t)j * a.lcap + i];
+                    a.rec_cnts[pos] = lcnt[i];
+                }
+                pos++;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+size_t bucket_lds_bytes(int W) {
+    size_t lcap = (size_t)bucket_lds_slots(W);
+    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + 18 * 4 + 16;
+}
+
+hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, const uint64_t* starts,
+                                uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                                uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
+                                uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
+                                hipStream_t s) {
+    BucketArgs a;
+    a.keys = keys;
+    a.stride = stride;
+    a.starts = starts;
+    a.nbuckets = nbuckets;
+    a.lcap = (lcap == 0 || lcap > (u32)bucket_lds_slots(W)) ? (u32)bucket_lds_slots(W) : lcap;
+    a.rec_keys = rec_keys;
+    a.rec_cnts = rec_cnts;
+    a.rec_cap = rec_cap;
+    a.rec_cursor = rec_cursor;
+    a.table = table;
+    a.cap = cap;
+    a.spill = spill;
+    a.spill_cap = spill_cap;
+    a.spill_ctr = stats + ST_SPILL2_FILL;
+    a.stats = stats;
+    a.probe_limit = probe_limit;
+    size_t lds = (bucket_lds_bytes(W) + 15) & ~(size_t)15;
+    switch (W) {
+    case 1: hipLaunchKernelGGL(count_buckets<1>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(count_buckets<2>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    case 3: hipLaunchKernelGGL(count_buckets<3>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(count_buckets<4>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// Segmented sum after a sort: out index of element i = pos[i] + head[i] - 1
+// (pos = exclusive scan of head flags); out_cnt must be zeroed.
+template <int W>
+__global__ __launch_bounds__(kBlock) void reduce_add_k(const u64* __restrict__ keys, u64 stride,
+                                                       const u32* __restrict__ cnts, u64 n,
+                                                       const u32* __restrict__ flags, const u32* __restrict__ pos,
+                                                       u64* __restrict__ out_keys, u64 ostride,
+                                                       u32* __restrict__ out_cnts) {
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        u32 q = pos[i] + flags[i] - 1u;
+        if (flags[i]) {
+#pragma unroll
+            for (int j = 0; j < W; j++) out_keys[(u64)j * ostride + q] = keys[(u64)j * stride + i];
+        }
+        atomicAdd(&out_cnts[q], cnts[i]);
+    }
+}
+
+hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n,
+                             const uint32_t* flags, const uint32_t* pos, uint64_t* out_keys, uint64_t ostride,
+                             uint32_t* out_cnts, hipStream_t s) {
+    int g = grid_for(n);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(reduce_add_k<1>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, flags, pos, out_keys, ostride, out_cnts); break;
+    case 2: hipLaunchKernelGGL(reduce_add_k<2>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, flags, pos, out_keys, ostride, out_cnts); break;
+    case 3: hipLaunchKernelGGL(reduce_add_k<3>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, flags, pos, out_keys, ostride, out_cnts); break;
+    case 4: hipLaunchKernelGGL(reduce_add_k<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, flags, pos, out_keys, ostride, out_cnts); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -21,25 +21,30 @@ def _fq(reads):
     return "".join(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n" for i, s in enumerate(reads))
 
 
+@pytest.fixture(params=["partition", "table"])
+def engine(request):
+    return request.param
+
+
 @pytest.mark.parametrize("name", sorted(MANIFEST))
-def test_golden_fastq_path(kca, name):
+def test_golden_fastq_path(kca, name, engine):
     m = MANIFEST[name]
     data = open(os.path.join(GOLD, m["fastq"]), "rb").read()
     want = open(os.path.join(GOLD, m["expected"]), "rb").read()
     L = len(data.split(b"\n")[1])
-    with kca.Context(kmer_length=m["k"], line_length=L) as ctx:
+    with kca.Context(kmer_length=m["k"], line_length=L, engine=engine) as ctx:
         ctx.count_fastq(data)
         assert ctx.records() == want
 
 
 @pytest.mark.parametrize("name", sorted(MANIFEST))
-def test_golden_chunk_path(kca, orc, name):
+def test_golden_chunk_path(kca, orc, name, engine):
     """Reference-exact chunks (readData restatement) through kc_count_chunk."""
     m = MANIFEST[name]
     data = open(os.path.join(GOLD, m["fastq"]), "rb").read()
     want = open(os.path.join(GOLD, m["expected"]), "rb").read()
     L = len(data.split(b"\n")[1])
-    with kca.Context(kmer_length=m["k"], line_length=L) as ctx:
+    with kca.Context(kmer_length=m["k"], line_length=L, engine=engine) as ctx:
         for chunk, ll in orc.chunks_of(data, orc.chunk_size(L, m["k"], 100000000)):
             ctx.count_chunk(chunk, ll)
         assert ctx.records() == want
@@ -49,10 +54,10 @@ def test_golden_chunk_path(kca, orc, name):
                                         (33, 120, 0.001), (55, 150, 0.002), (64, 150, 0.0), (96, 150, 0.001),
                                         (127, 150, 0.0), (128, 250, 0.001), (16, 64, 0.01), (31, 96, 0.0),
                                         (25, 1000, 0.001), (31, 5000, 0.0005), (1, 12, 0.05)])
-def test_synthetic_vs_oracle(kca, orc, k, L, n_rate):
+def test_synthetic_vs_oracle(kca, orc, k, L, n_rate, engine):
     n = max(50, 300000 // L)
     fq = kca.synth_fastq(n, L, seed=k * 7 + L, n_rate=n_rate)
-    with kca.Context(kmer_length=k, line_length=L) as ctx:
+    with kca.Context(kmer_length=k, line_length=L, engine=engine) as ctx:
         assert ctx.count_fastq(fq) == n
         got = ctx.records()
         st = ctx.stats()
@@ -60,22 +65,22 @@ def test_synthetic_vs_oracle(kca, orc, k, L, n_rate):
     assert st["windows"] == n * (L - k + 1)
 
 
-def test_genome_reads_k31(kca, orc):
+def test_genome_reads_k31(kca, orc, engine):
     fq = kca.synth_fastq(200000, 150, seed=2, genome_length=2_000_000)
-    with kca.Context(kmer_length=31, line_length=150) as ctx:
+    with kca.Context(kmer_length=31, line_length=150, engine=engine) as ctx:
         ctx.count_fastq(fq)
         got = ctx.records()
     want, _ = orc.refcpu(fq, 31, threads=8)
     assert got == want
 
 
-def test_special_reads(kca):
+def test_special_reads(kca, engine):
     reads = ["A" * 80, "N" * 80, "T" * 80, "acgt" * 20, "A" * 40 + "N" + "A" * 39, "C" * 79 + "N",
              "ACGT" * 20, "T" * 31 + "G" + "T" * 48]
     for k in (1, 21, 31, 32, 33, 64, 80):
         text = _fq(reads)
         want = kp.to_bytes(kp.count_reads(reads, k), k)
-        with kca.Context(kmer_length=k, line_length=80) as ctx:
+        with kca.Context(kmer_length=k, line_length=80, engine=engine) as ctx:
             ctx.count_fastq(text.encode())
             assert ctx.records() == want, k
 
@@ -140,11 +145,13 @@ def test_device_resident_fastq_and_reset(kca, orc):
 
 
 @pytest.mark.parametrize("k,temp", [(31, False), (31, True), (55, False), (21, True), (100, False)])
-def test_spill_path(kca, orc, tmp_path, k, temp):
-    """A tiny working set forces the spill -> radix sort -> run -> merge path."""
+def test_spill_path(kca, orc, tmp_path, k, temp, engine):
+    """A tiny working set forces the spill -> radix sort -> run -> merge path
+    (partition engine: a 1-slot LDS table forces the global-table fallback
+    first)."""
     L = 150
     fq = kca.synth_fastq(20000, L, seed=k, n_rate=0.001)
-    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=1 << 20,
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=1 << 20, engine=engine, lds_slots=1,
                      temp_dir=str(tmp_path) if temp else None) as ctx:
         ctx.count_fastq(fq)
         got = ctx.output_bytes(str(tmp_path))
@@ -153,13 +160,26 @@ def test_spill_path(kca, orc, tmp_path, k, temp):
     assert got == orc.count_fastq(fq, k)
 
 
-def test_multiple_blocks_accumulate(kca, orc):
+def test_multiple_blocks_accumulate(kca, orc, engine):
     blocks = [kca.synth_fastq(3000, 150, seed=11, n_rate=0.001, first_read=i * 3000) for i in range(4)]
-    with kca.Context(kmer_length=31, line_length=150) as ctx:
+    with kca.Context(kmer_length=31, line_length=150, engine=engine) as ctx:
         for b in blocks:
             ctx.count_fastq(b)
         got = ctx.records()
     assert got == orc.count_fastq(b"".join(blocks), 31)
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_partition_many_batches(kca, orc, k):
+    """A small working set splits one block into many partition batches whose
+    records are summed at finish."""
+    fq = kca.synth_fastq(60000, 150, seed=21, genome_length=300_000, n_rate=0.0005)
+    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=1 << 21) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["batches"] > 3
+    assert got == orc.count_fastq(fq, k)
 
 
 def _write_dir(tmp_path, name, text):
