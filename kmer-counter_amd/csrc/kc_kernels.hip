@@ -266,8 +266,11 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
     u32* inval = codes + a.R * a.NG;
     u32* lead = inval + a.R * a.NG;
     u32* rflag = lead + a.R;
-    // sink region (16-byte aligned)
-    unsigned char* sk = (unsigned char*)(((uintptr_t)(rflag + a.R) + 15) & ~(uintptr_t)15);
+    // sink region (16-byte aligned); offset arithmetic on smem keeps the LDS
+    // address space (an integer round trip would turn every access into FLAT)
+    const size_t sk_off = (((size_t)a.R * a.raw_stride + (size_t)2 * a.R * a.NG * 4 + (size_t)2 * a.R * 4) + 15) &
+                          ~(size_t)15;
+    unsigned char* sk = smem + sk_off;
     u32* s_hist = (u32*)sk;                      // HIST
     u32* s_cnt = (u32*)sk;                       // SCATTER: per-digit count in tile
     u32* s_start = s_cnt + 256;                  //          tile-local start
@@ -753,7 +756,13 @@ hipError_t launch_append_key0(int W, uint64_t* keys, uint32_t* cnts, uint64_t ou
 // ---------------------------------------------------------------------------
 
 constexpr int kSortItems = 8;
-constexpr int kSortTile = kBlock * kSortItems;  // 2048
+constexpr int kSortTile = kBlock * kSortItems;  // 2048 (grid sizing granule)
+
+template <int W>
+struct SortCfg {
+    static constexpr int ITEMS = (W == 1) ? 16 : ((W == 2) ? 8 : 4);  // rounds per wave
+    static constexpr int TILE = 4 * 64 * ITEMS;
+};
 
 uint64_t sort_hist_elems(int grid) { return (u64)256 * grid + scan_tmp_elems((u64)256 * grid) + 16; }  // u64
 
@@ -791,7 +800,13 @@ __global__ __launch_bounds__(kBlock) void sort_upsweep(const u64* __restrict__ k
     h[threadIdx.x] = 0;
     __syncthreads();
     u64 lo, hi;
-    block_range(n, gridDim.x, blockIdx.x, &lo, &hi);
+    {
+        constexpr int TILE = SortCfg<W>::TILE;
+        u64 tiles = (n + TILE - 1) / TILE;
+        u64 per = (tiles + gridDim.x - 1) / gridDim.x;
+        lo = min(n, (u64)blockIdx.x * per * TILE);
+        hi = min(n, (u64)(blockIdx.x + 1) * per * TILE);
+    }
     for (u64 i = lo + threadIdx.x; i < hi; i += kBlock) {
         u64 k[W];
         if constexpr (HASHED) {
@@ -807,101 +822,114 @@ __global__ __launch_bounds__(kBlock) void sort_upsweep(const u64* __restrict__ k
     hist[(u64)threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
+// Downsweep with wave-private stable ranking. A tile of kSortTile records is
+// split into 4 contiguous quarters, one per wave; a wave walks its quarter in
+// rounds of 64 consecutive records, finds the lanes sharing its digit with 8
+// ballots, and ranks them against its own running per-digit counters in LDS
+// (only that wave touches its row, so no barrier is needed between rounds).
+// One block-wide prefix over (digit, wave) then gives every record its stable
+// position in the tile; records are permuted through LDS and written out in
+// digit runs.
 template <int W, bool HAS_VALS, bool HASHED>
 __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__ kin, u64* __restrict__ kout,
                                                          const u32* __restrict__ vin, u32* __restrict__ vout,
                                                          u64 stride, u64 n, int word, int shift,
                                                          const u64* __restrict__ hist) {
+    constexpr int ITEMS = SortCfg<W>::ITEMS;
+    constexpr int TILE = SortCfg<W>::TILE;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    u64* skeys = (u64*)smem;                          // W x kSortTile
-    u32* svals = (u32*)(skeys + W * kSortTile);       // kSortTile
-    u32* wave_cnt = svals + kSortTile;                // 4 x 256
-    u32* wave_base = wave_cnt + 4 * 256;              // 4 x 256
-    u32* digit_run = wave_base + 4 * 256;             // 256: count so far in tile
-    u32* digit_start = digit_run + 256;               // 256: tile-local start
-    u32* scan_tmp = digit_start + 256;                // 4 (+4 pad)
-    u64* global_off = (u64*)(scan_tmp + 8);           // 256: running global offset
+    u64* skeys = (u64*)smem;                          // W x TILE
+    u32* svals = (u32*)(skeys + W * TILE);            // TILE (only with values)
+    u32* wcnt = svals + (HAS_VALS ? TILE : 0);        // 4 x 256 running counts per wave
+    u32* woff = wcnt + 4 * 256;                       // 4 x 256 offsets of a wave inside a digit
+    u32* dtot = woff + 4 * 256;                       // 256 digit totals of the tile
+    u32* dstart = dtot + 256;                         // 256 tile-local digit starts
+    u32* scan_tmp = dstart + 256;                     // 4 (+4 pad)
+    u64* global_off = (u64*)(scan_tmp + 8);           // 256 running global offsets
 
-    const int tid = threadIdx.x, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     global_off[tid] = hist[(u64)tid * gridDim.x + blockIdx.x];
-    digit_run[tid] = 0;
-    for (int i = tid; i < 4 * 256; i += kBlock) wave_cnt[i] = 0;
+    for (int i = tid; i < 4 * 256; i += kBlock) wcnt[i] = 0;
     __syncthreads();
 
     u64 lo, hi;
-    block_range(n, gridDim.x, blockIdx.x, &lo, &hi);
-    for (u64 t0 = lo; t0 < hi; t0 += kSortTile) {
-        u64 kreg[kSortItems][W];
-        u32 vreg[kSortItems];
-        u32 dreg[kSortItems];
-        u32 rank[kSortItems];
+    {
+        u64 tiles = (n + TILE - 1) / TILE;
+        u64 per = (tiles + gridDim.x - 1) / gridDim.x;
+        lo = min(n, (u64)blockIdx.x * per * TILE);
+        hi = min(n, (u64)(blockIdx.x + 1) * per * TILE);
+    }
+    const u64 lanemask = lanemask_lt();
+    for (u64 t0 = lo; t0 < hi; t0 += TILE) {
+        u64 kreg[ITEMS][W];
+        u32 vreg[ITEMS];
+        u32 dreg[ITEMS];
+        u32 rank[ITEMS];
+        const u64 q0 = t0 + (u64)wave * (64 * ITEMS) + lane;
 #pragma unroll
-        for (int it = 0; it < kSortItems; it++) {
-            u64 i = t0 + (u64)it * kBlock + tid;
+        for (int it = 0; it < ITEMS; it++) {
+            u64 i = q0 + (u64)it * 64;
             bool ok = i < hi;
 #pragma unroll
             for (int j = 0; j < W; j++) kreg[it][j] = ok ? kin[(u64)j * stride + i] : 0ull;
             if constexpr (HAS_VALS) vreg[it] = ok ? vin[i] : 0u;
+        }
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            u64 i = q0 + (u64)it * 64;
+            bool ok = i < hi;
             u32 d = sort_digit<W, HASHED>(kreg[it], word, shift);
             dreg[it] = d;
-            // peers: active lanes with the same digit
             u64 peers = __ballot(ok);
 #pragma unroll
             for (int b = 0; b < 8; b++) {
                 u64 bb = __ballot((d >> b) & 1u);
                 peers &= ((d >> b) & 1u) ? bb : ~bb;
             }
-            if (!ok) peers = 0;
-            u32 before = (u32)__popcll(peers & lanemask_lt());
-            if (ok && before == 0) wave_cnt[wave * 256 + d] = (u32)__popcll(peers);
-            __syncthreads();
-            {
-                // thread tid owns digit tid: per-wave bases in digit order, and
-                // re-zeroes the counters for the next item (the next writes to
-                // wave_cnt come after the barrier below)
-                u32 run = digit_run[tid];
-#pragma unroll
-                for (int w = 0; w < 4; w++) {
-                    u32 c = wave_cnt[w * 256 + tid];
-                    wave_cnt[w * 256 + tid] = 0;
-                    wave_base[w * 256 + tid] = run;
-                    run += c;
-                }
-                digit_run[tid] = run;
-            }
-            __syncthreads();
-            rank[it] = ok ? wave_base[wave * 256 + d] + before : 0xffffffffu;
+            u32 before = (u32)__popcll(peers & lanemask);
+            u32 base = ok ? wcnt[wave * 256 + d] : 0u;
+            // all lanes have read the counter; the group's lowest lane bumps it
+            if (ok && before == 0) wcnt[wave * 256 + d] = base + (u32)__popcll(peers);
+            rank[it] = ok ? base + before : 0xffffffffu;
         }
         __syncthreads();
-        u32 total;
-        u32 cnt = digit_run[tid];
-        u32 excl = block_excl_scan(cnt, scan_tmp, &total);
-        digit_start[tid] = excl;
+        {
+            u32 run = 0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                u32 c = wcnt[w * 256 + tid];
+                woff[w * 256 + tid] = run;
+                wcnt[w * 256 + tid] = 0;
+                run += c;
+            }
+            dtot[tid] = run;
+            u32 total;
+            dstart[tid] = block_excl_scan(run, scan_tmp, &total);
+        }
         __syncthreads();
 #pragma unroll
-        for (int it = 0; it < kSortItems; it++) {
+        for (int it = 0; it < ITEMS; it++) {
             if (rank[it] == 0xffffffffu) continue;
-            u32 pos = digit_start[dreg[it]] + rank[it];
+            u32 d = dreg[it];
+            u32 pos = dstart[d] + woff[wave * 256 + d] + rank[it];
 #pragma unroll
-            for (int j = 0; j < W; j++) skeys[j * kSortTile + pos] = kreg[it][j];
+            for (int j = 0; j < W; j++) skeys[j * TILE + pos] = kreg[it][j];
             if constexpr (HAS_VALS) svals[pos] = vreg[it];
         }
         __syncthreads();
-        u32 m = (u32)min((u64)kSortTile, hi - t0);
+        const u32 m = (u32)min((u64)TILE, hi - t0);
         for (u32 pos = tid; pos < m; pos += kBlock) {
             u64 k0[W];
 #pragma unroll
-            for (int j = 0; j < W; j++) k0[j] = skeys[j * kSortTile + pos];
+            for (int j = 0; j < W; j++) k0[j] = skeys[j * TILE + pos];
             u32 d = sort_digit<W, HASHED>(k0, word, shift);
-            u64 g = global_off[d] + (pos - digit_start[d]);
+            u64 g = global_off[d] + (pos - dstart[d]);
 #pragma unroll
             for (int j = 0; j < W; j++) kout[(u64)j * stride + g] = k0[j];
             if constexpr (HAS_VALS) vout[g] = svals[pos];
         }
         __syncthreads();
-        global_off[tid] += cnt;
-        digit_run[tid] = 0;
-        __syncthreads();
+        global_off[tid] += dtot[tid];
     }
 }
 
@@ -926,7 +954,8 @@ hipError_t launch_sort_pass(int W, const uint64_t* keys_in, uint64_t* keys_out, 
         hipError_t e = scan_impl<u64>(hist, hist, (u64)256 * grid, hist + (u64)256 * grid, s);
         if (e != hipSuccess) return e;
     }
-    size_t lds = (size_t)W * kSortTile * 8 + (size_t)kSortTile * 4 + (8 * 256 + 2 * 256 + 8) * 4 + 256 * 8;
+    const int tile = 4 * 64 * ((W == 1) ? 16 : ((W == 2) ? 8 : 4));
+    size_t lds = (size_t)W * tile * 8 + (vals_in ? (size_t)tile * 4 : 0) + (8 * 256 + 2 * 256 + 8) * 4 + 256 * 8;
     lds = (lds + 15) & ~(size_t)15;
     bool hv = vals_in != nullptr;
 #define KC_DOWN(WW, HV, HH)                                                                                      \
@@ -1362,50 +1391,57 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         }
         __syncthreads();
         const u64 lo = a.starts[b], hi = a.starts[b + 1];
-        for (u64 base = lo; base < hi; base += kBucketBlock) {
-            const u64 i = base + tid;
-            u64 key[W];
-            bool live = i < hi;
-            bool done = true, claimed = false;
-            if (live) {
+        constexpr int U = 4;  // independent key loads in flight per thread
+        for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
+            u64 key[U][W];
+            bool live[U];
 #pragma unroll
-                for (int j = 0; j < W; j++) key[j] = a.keys[(u64)j * a.stride + i];
-                u64 h = hash_key<W>(key);
-                if (!lds_insert<W>(key, h, lkeys, lcnt, lstate, a.lcap)) {
-                    if constexpr (W == 1)
-                        done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
-                    else
-                        done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
-                }
-            } else {
+            for (int u = 0; u < U; u++) {
+                const u64 i = base + (u64)u * kBucketBlock + tid;
+                live[u] = i < hi;
 #pragma unroll
-                for (int j = 0; j < W; j++) key[j] = 0;
+                for (int j = 0; j < W; j++) key[u][j] = live[u] ? a.keys[(u64)j * a.stride + i] : 0ull;
             }
-            u64 cm = __ballot(claimed);
-            if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
-                atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-            bool spill = !done;
-            if (__ballot(spill)) {
-                u64 idx = wave_reserve(a.spill_ctr, spill);
-                if (spill) {
-                    if (idx < a.spill_cap) {
 #pragma unroll
-                        for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
-                    } else {
-                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+            for (int u = 0; u < U; u++) {
+                bool done = true, claimed = false;
+                if (live[u]) {
+                    u64 h = hash_key<W>(key[u]);
+                    if (!lds_insert<W>(key[u], h, lkeys, lcnt, lstate, a.lcap)) {
+                        if constexpr (W == 1)
+                            done = insert_w1(key[u][0], a.table, a.cap, a.probe_limit, &claimed);
+                        else
+                            done = insert_wide<W>(key[u], a.table, a.cap, a.probe_limit, &claimed);
+                    }
+                }
+                u64 cm = __ballot(claimed);
+                if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                    atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+                bool spill = !done;
+                if (__ballot(spill)) {
+                    u64 idx = wave_reserve(a.spill_ctr, spill);
+                    if (spill) {
+                        if (idx < a.spill_cap) {
+#pragma unroll
+                            for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[u][j];
+                        } else {
+                            atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                        }
                     }
                 }
             }
         }
         __syncthreads();
-        // emit the occupied slots (slot order) after one reservation
+        // emit the occupied slots in slot order: count, one reservation, then
+        // rounds of 1024 consecutive slots with a block scan, so consecutive
+        // lanes write consecutive records
         u32 mine = 0;
         for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
             bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
             mine += occ ? 1u : 0u;
         }
         u32 total;
-        u32 before = block_excl_scan_n<kBucketBlock>(mine, misc, &total);
+        (void)block_excl_scan_n<kBucketBlock>(mine, misc, &total);
         if (tid == 0) {
             u64 base = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
             *(u64*)(misc + 16) = base;
@@ -1413,18 +1449,22 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                 atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
         }
         __syncthreads();
-        u64 pos = *(u64*)(misc + 16) + before;
-        // each thread owns slots tid, tid+1024, ... : emit them in that order
-        for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
-            bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
+        u64 pos = *(u64*)(misc + 16);
+        for (u32 r0 = 0; r0 < a.lcap; r0 += kBucketBlock) {
+            const u32 i = r0 + tid;
+            bool occ = false;
+            if (i < a.lcap) occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
+            u32 rt;
+            u32 before = block_excl_scan_n<kBucketBlock>(occ ? 1u : 0u, misc, &rt);
             if (occ) {
-                if (pos < a.rec_cap) {
+                u64 q = pos + before;
+                if (q < a.rec_cap) {
 #pragma unroll
-                    for (int j = 0; j < W; j++) a.rec_keys[(u64)j * a.rec_cap + pos] = lkeys[(size_t)j * a.lcap + i];
-                    a.rec_cnts[pos] = lcnt[i];
+                    for (int j = 0; j < W; j++) a.rec_keys[(u64)j * a.rec_cap + q] = lkeys[(size_t)j * a.lcap + i];
+                    a.rec_cnts[q] = lcnt[i];
                 }
-                pos++;
             }
+            pos += rt;
         }
         __syncthreads();
     }
