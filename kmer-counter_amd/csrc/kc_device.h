@@ -66,6 +66,7 @@ struct PartGeom {
     int seg_tiles;     // tiles per segment
     uint64_t nseg;     // segments (histogram columns)
     int max_win;       // windows per tile
+    int scap;          // P2 staging capacity (keys)
     size_t lds_scatter;// LDS bytes of the P2 workgroup
 };
 PartGeom part_geometry(int L, int k, uint64_t n_reads);

@@ -16,6 +16,7 @@ namespace kc {
 
 typedef uint64_t u64;
 typedef unsigned int u32;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWave = 64;
@@ -122,20 +123,39 @@ struct CountArgs {
     u32 probe_limit;
 };
 
+// Reads per tile that keep the kRoll-window chunks of a tile close to a whole
+// number of 256-lane rounds (R_max bounds R).
+static int balance_reads(int R_max, int nw) {
+    const int nchr = (nw + 7) / 8;
+    int best = R_max;
+    double best_eff = 0;
+    for (int R = R_max; R >= 1 && R >= R_max / 2; R--) {
+        int ch = R * nchr;
+        int rounds = (ch + kBlock - 1) / kBlock;
+        double eff = (double)ch / (rounds * kBlock);
+        if (eff > best_eff + 1e-9) {
+            best_eff = eff;
+            best = R;
+        }
+    }
+    return best;
+}
+
 CountGeom count_geometry(int L, int k) {
     CountGeom g;
     int W = (k + 31) / 32;
     int nw = L - k + 1;
-    g.NG = (L + 15) / 16 + 2 * W + 1;
+    g.NG = (L + 15) / 16 + 2 * W + 3;
     g.raw_stride = ((L + 31 + 15) / 16) * 16 + 16;
-    // aim for ~8 windows per thread, bounded by a 48 KiB LDS budget
-    int R = (8 * kBlock + nw - 1) / (nw > 0 ? nw : 1);
+    // aim for ~8 window runs per thread, bounded by a 48 KiB LDS budget
+    int R = (64 * kBlock + nw - 1) / (nw > 0 ? nw : 1);
     if (R < 1) R = 1;
     if (R > 64) R = 64;
     auto bytes = [&](int r) {
         return (size_t)r * g.raw_stride + (size_t)r * g.NG * 8 + (size_t)r * 8 + 16;
     };
     while (R > 1 && bytes(R) > 48 * 1024) R--;
+    R = balance_reads(R, nw);
     g.R = R;
     g.lds = (bytes(R) + 15) & ~(size_t)15;
     return g;
@@ -248,14 +268,25 @@ struct PartArgs {
     u64 nseg;
     int seg_tiles;    // tiles per segment
     int shift;        // digit = (hash >> shift) & 255
-    int max_win;      // SCATTER staging capacity (R * windows per read)
+    int max_win;      // windows per tile (R * windows per read)
+    int scap;         // SCATTER staging capacity (keys, >= max_win)
 };
 
-static size_t sink_lds_host(int W, int sink, int max_win) {
+static size_t sink_lds_host(int W, int sink, int scap) {
     if (sink == SINK_HIST) return 256 * 4;
     if (sink == SINK_SCATTER)
-        return (size_t)256 * 4 * 3 + 256 * 8 + 32 + (size_t)2 * W * 8 * max_win + (size_t)2 * 4 * max_win;
+        return 256 * 8 + 3 * 256 * 4 + 32 + (size_t)W * 8 * scap + (((size_t)scap + 15) & ~(size_t)15) + 2 * (size_t)scap;
     return 0;
+}
+
+constexpr int kRoll = 8;  // consecutive windows per lane
+
+// 32 bases starting at base index b of a read's LDS code groups (16 bases per
+// u32, first base highest), as one MSB-first word.
+__device__ __forceinline__ u64 code_word(const u32* cr, int b) {
+    const int g = b >> 4, o = b & 15;
+    const u64 hi = ((u64)cr[g] << 32) | (u64)cr[g + 1];
+    return o ? ((hi << (2 * o)) | (u64)(cr[g + 2] >> (32 - 2 * o))) : hi;
 }
 
 template <int W, int SINK>
@@ -272,15 +303,14 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                           ~(size_t)15;
     unsigned char* sk = smem + sk_off;
     u32* s_hist = (u32*)sk;                      // HIST
-    u32* s_cnt = (u32*)sk;                       // SCATTER: per-digit count in tile
-    u32* s_start = s_cnt + 256;                  //          tile-local start
-    u32* s_fill = s_start + 256;                 //          fill cursor
-    u64* s_cur = (u64*)(s_fill + 256);           //          global cursor of the segment
-    u32* s_misc = (u32*)(s_cur + 256);           //          [0] staged count, [4..7] scan scratch
-    u64* s_stage = (u64*)(s_misc + 8);           //          W x max_win staged keys
-    u64* s_sorted = s_stage + (size_t)W * pa.max_win;
-    u32* s_sdig = (u32*)(s_sorted + (size_t)W * pa.max_win);
-    u32* s_odig = s_sdig + pa.max_win;
+    u64* s_cur = (u64*)sk;                       // SCATTER: global cursor of each digit's run
+    u32* s_cnt = (u32*)(s_cur + 256);            //          staged keys per digit
+    u32* s_start = s_cnt + 256;                  //          digit start in the flush order
+    u32* s_fill = s_start + 256;                 //          rank cursor
+    u32* s_misc = s_fill + 256;                  //          [0] staged count, [4..7] scan scratch
+    u64* s_stage = (u64*)(s_misc + 8);           //          W x scap staged keys
+    unsigned char* s_dig = (unsigned char*)(s_stage + (size_t)W * pa.scap);  // scap digits
+    unsigned short* s_perm = (unsigned short*)(s_dig + ((pa.scap + 15) & ~15)); // scap flush order
     u32* scan_tmp = s_misc + 4;
 
     const int tid = threadIdx.x;
@@ -318,8 +348,10 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                 int ld = (int)(addr & 15);
                 if (c == 0) lead[r] = (u32)ld;
                 if (16 * c < ld + L) {
-                    const uint4 v = *(const uint4*)((addr & ~(uintptr_t)15) + 16 * (uintptr_t)c);
-                    *(uint4*)(raw + (size_t)r * a.raw_stride + 16 * c) = v;
+                    // streamed once: non-temporal, so the input stream does not
+                    // evict the partially written output lines from L2
+                    const v4u v = __builtin_nontemporal_load((const v4u*)((addr & ~(uintptr_t)15) + 16 * (uintptr_t)c));
+                    *(v4u*)(raw + (size_t)r * a.raw_stride + 16 * c) = v;
                 }
             }
             if (tid < nr) rflag[tid] = 0;
@@ -354,27 +386,41 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
             }
             __syncthreads();
 
-            // 3. windows -> keys -> sink
-            const int total = nr * nw;
-            int r = tid / nw, p = tid - (tid / nw) * nw;
-            for (int it = tid; it - (tid & 63) < total; it += kBlock) {
+            // 3. windows -> keys -> sink. A lane takes a run of kRoll consecutive
+            //    windows of one read: the first key is funnel-shifted out of the
+            //    code groups (extractKMers' shift-combine), every further key
+            //    shifts one base in (the base 32W past the window comes from a
+            //    tail word; past the read end it is 0, as in the reference).
+            const int nchr = (nw + kRoll - 1) / kRoll;
+            const int total = nr * nchr;
+            for (int c = tid; c - (tid & 63) < total; c += kBlock) {
                 // the loop bound is wave-uniform so every lane reaches the ballots
-                const bool active = it < total;
-                u64 key[W];
-                bool valid = false;
-                if (active) {
-                    const u32* cr = codes + r * NG;
-                    const int g = p >> 4, o = p & 15;
+                const bool cact = c < total;
+                int r = 0, p0 = 0;
+                u64 raw[W];
+                u64 tail = 0;
+                bool clean = true;
 #pragma unroll
-                    for (int j = 0; j < W; j++) {
-                        const int gg = g + 2 * j;
-                        u64 hi = ((u64)cr[gg] << 32) | (u64)cr[gg + 1];
-                        u64 w = o ? ((hi << (2 * o)) | (u64)(cr[gg + 2] >> (32 - 2 * o))) : hi;
-                        key[j] = w;
-                    }
+                for (int j = 0; j < W; j++) raw[j] = 0;
+                if (cact) {
+                    r = c / nchr;
+                    p0 = (c - r * nchr) * kRoll;
+                    const u32* cr = codes + r * NG;
+#pragma unroll
+                    for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
+                    tail = code_word(cr, p0 + 32 * W);
+                    clean = rflag[r] == 0;
+                }
+#pragma unroll 1
+                for (int sstep = 0; sstep < kRoll; sstep++) {
+                    const int p = p0 + sstep;
+                    const bool active = cact && p < nw;
+                    u64 key[W];
+#pragma unroll
+                    for (int j = 0; j < W; j++) key[j] = active ? raw[j] : 0ull;
                     key[W - 1] &= last_mask;
-                    valid = true;
-                    if (rflag[r]) {
+                    bool valid = active;
+                    if (active && !clean) {
                         const u32* ir = inval + r * NG;
                         const int last = p + k - 1;
                         for (int gg = p >> 4; gg <= (last >> 4); gg++) {
@@ -383,110 +429,106 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                             if (ir[gg] & rm) valid = false;
                         }
                     }
-                    my_hole |= !valid;
-                } else {
-#pragma unroll
-                    for (int j = 0; j < W; j++) key[j] = 0;
-                }
-                bool is_zero = true;
-#pragma unroll
-                for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
-                const bool live = valid && !is_zero;
+                    my_hole |= active && !valid;
+                    bool is_zero = true;
+    #pragma unroll
+                    for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
+                    const bool live = valid && !is_zero;
 
-                if constexpr (SINK == SINK_HIST) {
-                    if (live) atomicAdd(&s_hist[(u32)(hash_key<W>(key) >> pa.shift) & 255u], 1u);
-                } else {
-                    // key 0^W: one atomic per wave
-                    u64 zmask = __ballot(valid && is_zero);
-                    if (zmask) {
-                        if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
-                            atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
-                            atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                    if constexpr (SINK == SINK_HIST) {
+                        if (live) atomicAdd(&s_hist[(u32)(hash_key<W>(key) >> pa.shift) & 255u], 1u);
+                    } else {
+                        // key 0^W: one atomic per wave
+                        u64 zmask = __ballot(valid && is_zero);
+                        if (zmask) {
+                            if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
+                                atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
+                                atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                            }
+                        }
+                        if (valid) my_valid++;
+                    }
+                    if constexpr (SINK == SINK_SCATTER) {
+                        // stage the key (wave-aggregated LDS reservation)
+                        u64 m = __ballot(live);
+                        u32 base = 0;
+                        if (m) {
+                            int leader = __ffsll((long long)m) - 1;
+                            if ((int)lane_id() == leader) base = atomicAdd(&s_misc[0], (u32)__popcll(m));
+                            base = __shfl(base, leader);
+                        }
+                        if (live) {
+                            u32 idx = base + (u32)__popcll(m & lanemask_lt());
+                            const u32 d = (u32)(hash_key<W>(key) >> pa.shift) & 255u;
+    #pragma unroll
+                            for (int j = 0; j < W; j++) s_stage[(size_t)j * pa.scap + idx] = key[j];
+                            s_dig[idx] = (unsigned char)d;
+                            atomicAdd(&s_cnt[d], 1u);
                         }
                     }
-                    if (valid) my_valid++;
-                }
-                if constexpr (SINK == SINK_SCATTER) {
-                    // stage the key (wave-aggregated LDS reservation)
-                    u64 m = __ballot(live);
-                    u32 base = 0;
-                    if (m) {
-                        int leader = __ffsll((long long)m) - 1;
-                        if ((int)lane_id() == leader) base = atomicAdd(&s_misc[0], (u32)__popcll(m));
-                        base = __shfl(base, leader);
-                    }
-                    if (live) {
-                        u32 idx = base + (u32)__popcll(m & lanemask_lt());
-#pragma unroll
-                        for (int j = 0; j < W; j++) s_stage[(size_t)j * pa.max_win + idx] = key[j];
-                        s_sdig[idx] = (u32)(hash_key<W>(key) >> pa.shift) & 255u;
-                    }
-                }
-                if constexpr (SINK == SINK_TABLE) {
-                    bool done = true, claimed = false;
-                    if (live) {
-                        if constexpr (W == 1)
-                            done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
-                        else
-                            done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
-                    }
-                    u64 cm = __ballot(claimed);
-                    if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
-                        atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-                    // spill: wave-aggregated reservation in the spill buffer
-                    bool spill = !done;
-                    if (__ballot(spill)) {
-                        u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
-                        if (spill) {
-                            if (idx < a.spill_cap) {
-#pragma unroll
-                                for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
-                            } else {
-                                atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                    if constexpr (SINK == SINK_TABLE) {
+                        bool done = true, claimed = false;
+                        if (live) {
+                            if constexpr (W == 1)
+                                done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
+                            else
+                                done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
+                        }
+                        u64 cm = __ballot(claimed);
+                        if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                            atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+                        // spill: wave-aggregated reservation in the spill buffer
+                        bool spill = !done;
+                        if (__ballot(spill)) {
+                            u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
+                            if (spill) {
+                                if (idx < a.spill_cap) {
+    #pragma unroll
+                                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
+                                } else {
+                                    atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                                }
                             }
                         }
                     }
-                }
-                // advance to this lane's next window (stride 256 windows)
-                p += kBlock;
-                while (p >= nw) {
-                    p -= nw;
-                    r++;
+                    // roll one base in
+#pragma unroll
+                    for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
+                    raw[W - 1] = (raw[W - 1] << 2) | (tail >> 62);
+                    tail <<= 2;
                 }
             }
             __syncthreads();
 
             if constexpr (SINK == SINK_SCATTER) {
-                // LDS counting sort of the staged keys by digit, then writes in
-                // digit order: consecutive lanes -> consecutive addresses of a
-                // digit's run in this segment's slice
+                // flush when the next tile might not fit, and at the segment end:
+                // order the staged keys by digit through a permutation, then write
+                // each digit's run with consecutive lanes
                 const u32 n = s_misc[0];
-                for (u32 i = tid; i < n; i += kBlock) atomicAdd(&s_cnt[s_sdig[i]], 1u);
-                __syncthreads();
-                u32 tot;
-                u32 st = block_excl_scan(s_cnt[tid], scan_tmp, &tot);
-                s_start[tid] = st;
-                s_fill[tid] = st;
-                __syncthreads();
-                for (u32 i = tid; i < n; i += kBlock) {
-                    u32 d = s_sdig[i];
-                    u32 q = atomicAdd(&s_fill[d], 1u);
+                if (tile + 1 == t_end || n + (u32)pa.max_win > (u32)pa.scap) {
+                    u32 tot;
+                    u32 st = block_excl_scan(s_cnt[tid], scan_tmp, &tot);
+                    s_start[tid] = st;
+                    s_fill[tid] = st;
+                    __syncthreads();
+                    for (u32 i = tid; i < n; i += kBlock) {
+                        u32 q = atomicAdd(&s_fill[s_dig[i]], 1u);
+                        s_perm[q] = (unsigned short)i;
+                    }
+                    __syncthreads();
+                    for (u32 q = tid; q < n; q += kBlock) {
+                        const u32 i = s_perm[q];
+                        const u32 d = s_dig[i];
+                        const u64 g = s_cur[d] + (q - s_start[d]);
 #pragma unroll
-                    for (int j = 0; j < W; j++) s_sorted[(size_t)j * pa.max_win + q] = s_stage[(size_t)j * pa.max_win + i];
-                    s_odig[q] = d;
+                        for (int j = 0; j < W; j++) pa.out[(u64)j * pa.out_stride + g] = s_stage[(size_t)j * pa.scap + i];
+                    }
+                    __syncthreads();
+                    s_cur[tid] += s_cnt[tid];
+                    s_cnt[tid] = 0;
+                    if (tid == 0) s_misc[0] = 0;
+                    __syncthreads();
                 }
-                __syncthreads();
-                for (u32 q = tid; q < n; q += kBlock) {
-                    u32 d = s_odig[q];
-                    u64 g = s_cur[d] + (q - s_start[d]);
-#pragma unroll
-                    for (int j = 0; j < W; j++) pa.out[(u64)j * pa.out_stride + g] = s_sorted[(size_t)j * pa.max_win + q];
-                }
-                __syncthreads();
-                s_cur[tid] += s_cnt[tid];
-                s_cnt[tid] = 0;
-                if (tid == 0) s_misc[0] = 0;
-                __syncthreads();
             }
         }
         if constexpr (SINK == SINK_HIST) {
@@ -544,19 +586,28 @@ hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s)
     return hipGetLastError();
 }
 
+// LDS of one P2 workgroup; two workgroups per CU
+constexpr size_t kPartLds = 76 * 1024;
+
 PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     PartGeom p;
     CountGeom g = count_geometry(L, k);
-    // P1 and P2 share this tile geometry; R is limited so that P2's staging
-    // (two W-word key copies + digits per window) keeps the block <= ~72 KiB
-    // (two workgroups per CU)
+    // P1 and P2 share this tile geometry. P2 stages keys over several tiles
+    // (scap >= 2 tiles where possible) before writing them in digit order, so
+    // each digit run written is long enough to fill whole cache lines.
     const int W = (k + 31) / 32;
     const int nw = L - k + 1;
-    auto lds = [&](int r) {
-        size_t front = (size_t)r * g.raw_stride + (size_t)r * g.NG * 8 + (size_t)r * 8 + 16;
-        return ((front + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, r * nw);
+    auto front = [&](int r) {
+        size_t f = (size_t)r * g.raw_stride + (size_t)r * g.NG * 8 + (size_t)r * 8 + 16;
+        return ((f + 15) & ~(size_t)15) + 16;
     };
-    while (g.R > 1 && lds(g.R) > 72 * 1024) g.R--;
+    const size_t per_key = (size_t)W * 8 + 1 + 2 + 1;
+    while (g.R > 1 && front(g.R) + sink_lds_host(W, SINK_SCATTER, 2 * g.R * nw) > kPartLds) g.R--;
+    g.R = balance_reads(g.R, nw);
+    size_t room = kPartLds > front(g.R) + 4096 ? kPartLds - front(g.R) - 4096 : 0;
+    int scap = (int)(room / per_key);
+    if (scap > 65535) scap = 65535;  // u16 permutation indices
+    if (scap < g.R * nw) scap = g.R * nw;
     g.lds = (((size_t)g.R * g.raw_stride + (size_t)g.R * g.NG * 8 + (size_t)g.R * 8 + 16) + 15) & ~(size_t)15;
     p.geom = g;
     u64 tiles = (n_reads + g.R - 1) / g.R;
@@ -565,7 +616,8 @@ PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     p.seg_tiles = (int)seg_tiles;
     p.nseg = (tiles + seg_tiles - 1) / seg_tiles;
     p.max_win = g.R * nw;
-    p.lds_scatter = lds(g.R);
+    p.scap = scap;
+    p.lds_scatter = front(g.R) + sink_lds_host(W, SINK_SCATTER, scap);
     return p;
 }
 
@@ -582,7 +634,8 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
     pa.seg_tiles = pg.seg_tiles;
     pa.shift = shift;
     pa.max_win = pg.max_win;
-    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_HIST, pg.max_win);
+    pa.scap = pg.scap;
+    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_HIST, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
     KC_FRONT_SWITCH(SINK_HIST, grid, lds, s, a, pa)
     return hipGetLastError();
@@ -604,7 +657,8 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa.seg_tiles = pg.seg_tiles;
     pa.shift = shift;
     pa.max_win = pg.max_win;
-    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.max_win);
+    pa.scap = pg.scap;
+    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
     KC_FRONT_SWITCH(SINK_SCATTER, grid, lds, s, a, pa)
     return hipGetLastError();
@@ -1382,14 +1436,14 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
     u32* lstate = lcnt + a.lcap;                              // lcap (W >= 2)
     u32* misc = lstate + (W >= 2 ? a.lcap : 0);               // scan scratch (16) + base (2)
     const int tid = threadIdx.x;
-    for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
-        for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+    for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
-            for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
-            lcnt[i] = 0;
-            if constexpr (W >= 2) lstate[i] = 0;
-        }
-        __syncthreads();
+        for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+        lcnt[i] = 0;
+        if constexpr (W >= 2) lstate[i] = 0;
+    }
+    __syncthreads();
+    for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         const u64 lo = a.starts[b], hi = a.starts[b + 1];
         constexpr int U = 4;  // independent key loads in flight per thread
         for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
@@ -1463,6 +1517,11 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     for (int j = 0; j < W; j++) a.rec_keys[(u64)j * a.rec_cap + q] = lkeys[(size_t)j * a.lcap + i];
                     a.rec_cnts[q] = lcnt[i];
                 }
+                // leave the slot empty for the next bucket
+#pragma unroll
+                for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+                lcnt[i] = 0;
+                if constexpr (W >= 2) lstate[i] = 0;
             }
             pos += rt;
         }
