@@ -135,6 +135,8 @@ void kc_destroy(kc_ctx* ctx);
 const char* kc_strerror(kc_status s);
 const char* kc_last_error(const kc_ctx* ctx);
 int32_t kc_abi_version(void);
+/* Number of visible HIP devices (0 when none; never fails). */
+int32_t kc_device_count(void);
 /* Forget every count (table, spill runs, stats); keeps allocations. */
 kc_status kc_reset(kc_ctx* ctx);
 

@@ -116,6 +116,7 @@ def lib() -> ctypes.CDLL:
         "kc_strerror": ([ctypes.c_int], ctypes.c_char_p),
         "kc_last_error": ([vp], ctypes.c_char_p),
         "kc_abi_version": ([], ctypes.c_int32),
+        "kc_device_count": ([], ctypes.c_int32),
         "kc_reset": ([vp], ctypes.c_int),
         "kc_count_chunk": ([vp, ctypes.c_char_p, i64, i64], ctypes.c_int),
         "kc_count_chunk_device": ([vp, vp, i64, i64], ctypes.c_int),

@@ -521,6 +521,12 @@ extern "C" {
 
 int32_t kc_abi_version(void) { return KC_ABI_VERSION; }
 
+int32_t kc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
 const char* kc_strerror(kc_status s) {
     switch (s) {
     case KC_OK: return "ok";

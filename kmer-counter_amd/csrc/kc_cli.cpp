@@ -310,12 +310,18 @@ int main(int argc, char** argv) {
     }
     std::vector<InputFile> files = list_inputs(o.input_dir);
 
-    // one context per GPU; blocks are dealt round-robin (read-shard, no collective)
+    // one context per GPU; blocks are dealt round-robin (read-shard, no
+    // collective). With fewer devices than gpus=N, contexts share devices.
+    int ndev = kc_device_count();
+    if (ndev <= 0) {
+        fprintf(stderr, "kmer-counter: no HIP device\n");
+        return 1;
+    }
     std::vector<GpuWork> gw(o.gpus);
     for (int g = 0; g < o.gpus; g++) {
         kc_config cfg;
         memset(&cfg, 0, sizeof(cfg));
-        cfg.device = g;
+        cfg.device = g % ndev;
         cfg.kmer_length = o.kmer_length;
         cfg.line_length = files.empty() ? o.kmer_length : files[0].L;
         cfg.gpu_memory_limit = (uint64_t)o.gpu_memory_limit;
@@ -332,6 +338,7 @@ int main(int argc, char** argv) {
         size_t n;
         int64_t L;
     };
+    size_t next_block = 0;
     for (const InputFile& f : files) {
         if (f.L < o.kmer_length) continue;
         bool exact = o.input_mode == "exact";
@@ -359,9 +366,11 @@ int main(int argc, char** argv) {
             std::vector<std::thread> th;
             std::vector<kc_status> st(o.gpus, KC_OK);
             bool fallback = false;
+            const size_t shift = next_block;  // deal blocks round-robin across files too
+            next_block += blocks.size();
             for (int g = 0; g < o.gpus; g++) {
-                th.emplace_back([&, g]() {
-                    for (size_t i = g; i < blocks.size(); i += o.gpus) {
+                th.emplace_back([&, g, shift]() {
+                    for (size_t i = (g + o.gpus - shift % o.gpus) % o.gpus; i < blocks.size(); i += o.gpus) {
                         uint64_t nr = 0;
                         kc_status s = kc_count_fastq(gw[g].ctx, m.p + blocks[i].first,
                                                        blocks[i].second - blocks[i].first, f.L, &nr);

@@ -372,24 +372,60 @@ static int64_t o_ref_reduce(unsigned char* recs, int64_t bytes, int rs) {
     return keep + rs;
 }
 
-/* Runs processKMers' data path for one chunk; returns the reduced record bytes
- * in *out (caller frees). */
-static int64_t o_ref_process_chunk(const char* chunk, int64_t size, int64_t L, int64_t k, unsigned char** out) {
+/* Per-worker buffers of processKMers' data path, allocated once and reused
+ * per chunk like the reference's per-stream buffers (PrepareGPU allocates
+ * h_output once; processKMers memsets it per chunk, GPUHandler.cu:406,490). */
+typedef struct o_ws {
+    unsigned char *buf, *filt, *recs;
+    size_t cap_buf, cap_recs;
+} o_ws;
+
+static void o_ws_fit(o_ws* w, size_t buf, size_t recs) {
+    if (buf > w->cap_buf) {
+        free(w->buf);
+        free(w->filt);
+        w->buf = (unsigned char*)malloc(buf);
+        w->filt = (unsigned char*)malloc(buf);
+        w->cap_buf = buf;
+    }
+    if (recs > w->cap_recs) {
+        free(w->recs);
+        w->recs = (unsigned char*)malloc(recs);
+        w->cap_recs = recs;
+    }
+}
+
+static void o_ws_free(o_ws* w) {
+    free(w->buf);
+    free(w->filt);
+    free(w->recs);
+    memset(w, 0, sizeof(*w));
+}
+
+/* Runs processKMers' data path for one chunk; the reduced records are left at
+ * the start of w->recs and their byte length is returned. */
+static int64_t o_ref_process_chunk_ws(o_ws* w, const char* chunk, int64_t size, int64_t L, int64_t k) {
     int W = o_words(k);
     int rs = 8 * W + 4;
     int64_t n = size / L;
     int64_t per_read = (L - k + 1) * rs;
-    unsigned char* buf = (unsigned char*)malloc((size_t)size + 64);
-    unsigned char* filt = (unsigned char*)calloc((size_t)size + 64, 1);
-    unsigned char* recs = (unsigned char*)calloc((size_t)(n * per_read) + 1, 1);
-    memcpy(buf, chunk, (size_t)size);
-    memset(buf + size, 0, 64);
-    for (int64_t r = 0; r < n; r++) o_ref_encode(buf, filt, r * L, L);
-    for (int64_t r = 0; r < n; r++) o_ref_extract(buf, filt, r * L, k, recs + r * per_read);
-    int64_t bytes = o_ref_reduce(recs, n * per_read, rs);
-    free(buf);
-    free(filt);
-    *out = recs;
+    o_ws_fit(w, (size_t)size + 64, (size_t)(n * per_read) + 1);
+    memcpy(w->buf, chunk, (size_t)size);
+    memset(w->buf + size, 0, 64);
+    memset(w->filt, 0, (size_t)size + 64);
+    memset(w->recs, 0, (size_t)(n * per_read));
+    for (int64_t r = 0; r < n; r++) o_ref_encode(w->buf, w->filt, r * L, L);
+    for (int64_t r = 0; r < n; r++) o_ref_extract(w->buf, w->filt, r * L, k, w->recs + r * per_read);
+    return o_ref_reduce(w->recs, n * per_read, rs);
+}
+
+static int64_t o_ref_process_chunk(const char* chunk, int64_t size, int64_t L, int64_t k, unsigned char** out) {
+    o_ws w;
+    memset(&w, 0, sizeof(w));
+    int64_t bytes = o_ref_process_chunk_ws(&w, chunk, size, L, k);
+    *out = w.recs;
+    w.recs = NULL;
+    o_ws_free(&w);
     return bytes;
 }
 
@@ -577,6 +613,8 @@ typedef struct o_pool {
 static void* o_worker(void* arg) {
     o_pool* pl = (o_pool*)arg;
     int W = o_words(pl->k), rs = 8 * W + 4;
+    o_ws ws;
+    memset(&ws, 0, sizeof(ws));
     for (;;) {
         pthread_mutex_lock(&pl->mu);
         while (!pl->head && !pl->closed) pthread_cond_wait(&pl->cv, &pl->mu);
@@ -589,8 +627,8 @@ static void* o_worker(void* arg) {
         }
         pthread_mutex_unlock(&pl->mu);
         if (!j) break;
-        unsigned char* recs = NULL;
-        int64_t bytes = o_ref_process_chunk(j->data, j->size, j->L, pl->k, &recs);
+        int64_t bytes = o_ref_process_chunk_ws(&ws, j->data, j->size, j->L, pl->k);
+        const unsigned char* recs = ws.recs;
         uint64_t key[O_MAXW];
         for (int64_t off = 0; off < bytes; off += rs) {
             uint32_t c;
@@ -598,12 +636,15 @@ static void* o_worker(void* arg) {
             memcpy(&c, recs + off + 8 * W, 4);
             o_table_add(pl->table, key, c);
         }
-        free(recs);
         free(j->data);
         free(j);
     }
+    o_ws_free(&ws);
     return NULL;
 }
+
+int64_t oracle_refcpu_run(const char* fastq, int64_t n_bytes, int64_t k, int64_t gpu_memory_limit, int threads,
+                          unsigned char** out, uint64_t* windows);
 
 /* Runs the whole reference count path over one in-memory FASTQ file with
  * `threads` workers. Writes the sorted SortedKMerFile bytes into *out (malloc;
@@ -611,6 +652,14 @@ static void* o_worker(void* arg) {
  * the number of k-mer windows processed. */
 int64_t oracle_refcpu_count(const char* fastq, int64_t n_bytes, int64_t k, int64_t gpu_memory_limit, int threads,
                             unsigned char** out, uint64_t* windows) {
+    return oracle_refcpu_run(fastq, n_bytes, k, gpu_memory_limit, threads, out, windows);
+}
+
+/* out == NULL: stop once the hash table is complete (the reference's work
+ * before DumpResults, which writes in hash order) and return the number of
+ * distinct keys; used to time the CPU baseline. */
+int64_t oracle_refcpu_run(const char* fastq, int64_t n_bytes, int64_t k, int64_t gpu_memory_limit, int threads,
+                          unsigned char** out, uint64_t* windows) {
     if (k < 1 || k > 32 * O_MAXW || threads < 1) return -1;
     int W = o_words(k), rs = 8 * W + 4;
     o_table* t = (o_table*)calloc(1, sizeof(*t));
@@ -667,6 +716,17 @@ int64_t oracle_refcpu_count(const char* fastq, int64_t n_bytes, int64_t k, int64
     /* dump: gather entries and sort by key words */
     int64_t total = 0;
     for (int i = 0; i < O_SHARDS; i++) total += t->sh[i].n;
+    if (!out) {
+        for (int i = 0; i < O_SHARDS; i++) {
+            free(t->sh[i].keys);
+            free(t->sh[i].cnts);
+            free(t->sh[i].used);
+            pthread_mutex_destroy(&t->sh[i].mu);
+        }
+        free(t);
+        if (windows) *windows = nwin;
+        return total;
+    }
     size_t ent = (size_t)W * 8 + 8;
     unsigned char* tmp = (unsigned char*)malloc(ent * (size_t)(total ? total : 1));
     int64_t m = 0;

@@ -33,6 +33,8 @@ def lib():
         L.oracle_count_fastq.restype = i64
         L.oracle_refcpu_count.argtypes = [ctypes.c_char_p, i64, i64, i64, ctypes.c_int, P(vp), P(u64)]
         L.oracle_refcpu_count.restype = i64
+        L.oracle_refcpu_run.argtypes = [ctypes.c_char_p, i64, i64, i64, ctypes.c_int, vp, P(u64)]
+        L.oracle_refcpu_run.restype = i64
         L.oracle_free.argtypes = [vp]
         L.oracle_acc_new.argtypes = [i64]
         L.oracle_acc_new.restype = vp
@@ -103,6 +105,17 @@ def refcpu(data: bytes, k: int, gpu_memory_limit: int = 100000000, threads: int 
     res = ctypes.string_at(out, n * rs_of(k)) if n else b""
     L.oracle_free(out)
     return res, win.value
+
+
+def refcpu_count_only(data: bytes, k: int, gpu_memory_limit: int = 100000000, threads: int = 1):
+    """refcpu up to the complete hash table (no sorted dump). Returns
+    (distinct keys, windows)."""
+    L = lib()
+    win = ctypes.c_uint64()
+    n = L.oracle_refcpu_run(data, len(data), k, gpu_memory_limit, threads, None, ctypes.byref(win))
+    if n < 0:
+        raise ValueError("bad oracle arguments")
+    return n, win.value
 
 
 def chunks_of(data: bytes, chunk: int):

@@ -219,6 +219,24 @@ def test_cli_auto_falls_back_to_exact_on_malformed_input(kca, orc, tmp_path):
     assert out.read_bytes() == want
 
 
+def test_cli_multi_context(kca, orc, tmp_path):
+    """gpus=3: three device contexts (sharing the one GPU of a 1-GPU box) count
+    round-robin blocks of several files; their sorted runs are k-way merged."""
+    d = tmp_path / "in"
+    d.mkdir()
+    texts = []
+    for i in range(5):
+        t = kca.synth_fastq(2000, 150, seed=30 + i, n_rate=0.001)
+        (d / f"f{i}.fq").write_bytes(t)
+        texts.append(t)
+    out = tmp_path / "o.bin"
+    subprocess.run([kca.CLI_PATH, "kmerLength=31", f"inputFileLocation={d}", f"outputFile={out}",
+                    f"tempFileLocation={tmp_path}", "gpus=3", "quiet=1"], check=True, capture_output=True)
+    want = orc.count_chunks([(c, ll) for t in texts for c, ll in orc.chunks_of(t, orc.chunk_size(150, 31, 100000000))],
+                            31)
+    assert out.read_bytes() == want
+
+
 def test_cli_spill_and_merge_knobs(kca, orc, tmp_path):
     fq = kca.synth_fastq(30000, 100, seed=8, n_rate=0.001).decode()
     d = _write_dir(tmp_path, "in", fq)
