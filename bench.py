@@ -7,11 +7,15 @@ per GPU, FASTQ text resident in HBM (generated on the device, untimed), in-HBM
 hash table only. One step = one full count of the GPU's reads: clear the table,
 index the FASTQ block (K1), encode + window + insert every k-mer (K2), compact
 and radix-sort the table into SortedKMerFile records (K3/K4). N GPUs: one
-process per GPU, each counts its own disjoint 50M-read shard (read-shard,
-weak scaling, no collective on the data path); the per-GPU sorted runs are what
-the host k-way merge would combine (not timed).
+process per GPU, each counts its own disjoint 50M-read shard (weak scaling),
+then by default (`--exchange alltoall`) the ranks exchange
+their sorted (key, count) records by key-space owner with one RCCL
+all-to-all and each merges what it receives on the device, so the node's
+SortedKMerFile is the concatenation of the ranks' runs — all inside the timed
+step. `--exchange none` is the read-shard mode (cfg3): no collective, the
+per-GPU runs are left for the host k-way merge (not timed).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--exchange alltoall|none] [--no-cpu]
 
 Prints one JSON line on rank 0 (contract in the task statement).
 """
@@ -97,6 +101,8 @@ def main():
     ap.add_argument("--engine", default="partition", choices=["partition", "table"])
     ap.add_argument("--cpu-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
+                    help="N>1: key-space all-to-all (cfg4) or read-shard only (cfg3); ignored at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,10 +129,22 @@ def main():
     first = shard_first(rank, args.reads)
     ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first)
 
+    exchange = args.exchange if world > 1 else "none"
+    xdev = None
+    if exchange == "alltoall":
+        import torch
+        xdev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", device)
+    xch_ms = [0.0]
+
     def step():
         ctx.reset()
         ctx.count_fastq_device(ptr, nbytes)
-        return ctx.finish()
+        n = ctx.finish()
+        if exchange == "alltoall":
+            t = time.perf_counter()
+            n = kca.keyspace_exchange(ctx, dist, xdev)
+            xch_ms[0] += (time.perf_counter() - t) * 1e3
+        return n
 
     def barrier_sync():
         if dist is not None:
@@ -138,6 +156,7 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier_sync()
+    xch_ms[0] = 0.0
     t0 = time.perf_counter()
     insert_ms = 0.0
     launches = 0
@@ -189,19 +208,29 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(kca, args.cpu_reads, L, k, args.genome, args.seed, 0)
 
+    base = (f"k={k}, {args.reads} x {L} bp reads per GPU sampled from a {args.genome} bp random genome "
+            f"(seed {args.seed}), FASTQ in HBM, in-HBM hash table")
+    if world == 1:
+        workload, parallelism = "cfg2: " + base, "single GPU"
+    elif exchange == "alltoall":
+        workload = (f"cfg4 pattern at {world} GPUs: " + base + "; key-space all-to-all of the sorted (key, count) "
+                    "records + per-GPU merge inside the step (output = concatenation of the ranks' runs)")
+        parallelism = f"read-shard count + key-space all-to-all x{world}"
+    else:
+        workload = f"cfg3 pattern at {world} GPUs: " + base + "; per-GPU sorted runs, host merge not timed"
+        parallelism = f"read-shard x{world}"
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": f"cfg2: k={k}, {args.reads} x {L} bp reads per GPU sampled from a "
-                                   f"{args.genome} bp random genome (seed {args.seed}), FASTQ in HBM, "
-                                   f"in-HBM hash table", "k": k, "read_length": L, "reads_per_gpu": args.reads,
-                       "parallelism": f"read-shard x{world}", "gpu_memory_limit": args.mem},
+            "config": {"workload": workload, "k": k, "read_length": L, "reads_per_gpu": args.reads,
+                       "parallelism": parallelism, "gpu_memory_limit": args.mem},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "breakdown_ms_per_step": {"insert": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
                                       "finish": finish_ms / args.steps,
+                                      "exchange_rank0": xch_ms[0] / args.steps,
                                       "partition_passes": [round(x / args.steps, 3) for x in part_ms]},
             "engine": args.engine,
             "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"],

@@ -182,6 +182,24 @@ kc_status kc_write_output(kc_ctx* ctx, const char* path, uint32_t merge_fan_in, 
 kc_status kc_write_runs(kc_ctx* ctx, const char* prefix, uint32_t* n_runs);
 kc_status kc_get_stats(const kc_ctx* ctx, kc_stats* out);
 
+/* ---- key-space partition across GPUs ----------------------
+ * owner(key) = ((word0 >> 32) * world) >> 32 is monotone in the key, so after
+ * every rank sends owner o the records of its sorted table run that o owns and
+ * o merges what it receives, the ranks' outputs concatenated in rank order
+ * are the global SortedKMerFile. The exchange itself is the caller's
+ * (an RCCL all-to-all; bench.py uses torch.distributed). */
+/* counts[o] = records of the finished table run owned by rank o; the run's
+ * packed bytes (kc_device_records) hold them as consecutive slices. */
+kc_status kc_owner_counts(kc_ctx* ctx, uint32_t world, uint64_t* counts);
+/* Replaces the finished ctx's table run by the sorted, summed merge of
+ * n_records packed records (SortedKMerFile layout, any order, duplicates
+ * allowed, u32 counts wrap) in device memory of the ctx's device. The ctx
+ * stays finished; kc_reset starts a new count. KC_ERR_STATE before kc_finish
+ * or when spill runs exist. */
+kc_status kc_merge_records_device(kc_ctx* ctx, const void* d_packed, uint64_t n_records);
+/* Device->device copy on the ctx's stream (exchange staging). */
+kc_status kc_copy_device(kc_ctx* ctx, void* d_dst, const void* d_src, uint64_t n_bytes);
+
 /* ---- host merge of sorted runs (KMerFileMerger / KMerFileMergeHandler) ---- */
 kc_status kc_merge_files(const char* const* inputs, uint32_t n_inputs, const char* output,
                          int64_t kmer_length, uint32_t merge_fan_in, uint32_t merge_threads);

@@ -135,6 +135,9 @@ def lib() -> ctypes.CDLL:
         "kc_synth_fastq_device": ([vp, P(_Synth), P(vp), P(u64)], ctypes.c_int),
         "kc_synth_free": ([vp, vp], ctypes.c_int),
         "kc_copy_to_host": ([vp, vp, vp, u64], ctypes.c_int),
+        "kc_owner_counts": ([vp, u32, P(u64)], ctypes.c_int),
+        "kc_merge_records_device": ([vp, vp, u64], ctypes.c_int),
+        "kc_copy_device": ([vp, vp, vp, u64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -179,6 +182,7 @@ class Context:
         self.k = kmer_length
         self.W = (kmer_length + 31) // 32
         self.rs = 8 * self.W + 4
+        self._device = device
         self._tmp = temp_dir.encode() if temp_dir else None
         if engine not in ("partition", "table"):
             raise ValueError("engine must be 'partition' or 'table'")
@@ -264,6 +268,46 @@ class Context:
         self._chk(self._L.kc_copy_records(self._h, buf, n * self.rs))
         return buf.raw[: n * self.rs]
 
+    def device_records(self):
+        """(device pointer, bytes) of the finished table run's packed records."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_device_records(self._h, ctypes.byref(p), ctypes.byref(n)))
+        return p.value or 0, n.value
+
+    def owner_counts(self, world: int) -> List[int]:
+        """Records of the finished table run per key-space owner (kc_owner_counts)."""
+        arr = (ctypes.c_uint64 * world)()
+        self._chk(self._L.kc_owner_counts(self._h, world, arr))
+        return list(arr)
+
+    def export_records(self, dst) -> int:
+        """Copy the finished table run's packed records into the torch uint8
+        tensor `dst` (device or host); returns the record count."""
+        n = self.finish()
+        nb = n * self.rs
+        if dst.numel() < nb:
+            raise ValueError("destination too small")
+        if dst.is_cuda:
+            ptr, _ = self.device_records()
+            self._chk(self._L.kc_copy_device(self._h, ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(ptr), nb))
+        else:
+            self._chk(self._L.kc_copy_records(self._h, ctypes.c_void_p(dst.data_ptr()), nb))
+        return n
+
+    def merge_records(self, src, n_records: int) -> int:
+        """Replace the table run by the sorted, summed merge of n_records packed
+        records held in the torch uint8 tensor `src` (host tensors are staged
+        to this ctx's device first); returns the merged record count."""
+        if n_records * self.rs > src.numel():
+            raise ValueError("source too small")
+        if not src.is_cuda:
+            import torch
+
+            src = src.to(torch.device("cuda", self._device))
+        self._chk(self._L.kc_merge_records_device(self._h, ctypes.c_void_p(src.data_ptr()), n_records))
+        return self.finish()
+
     def write_output(self, path: str, fan_in: int = 2, threads: int = 2):
         self.finish()
         self._chk(self._L.kc_write_output(self._h, path.encode(), fan_in, threads))
@@ -287,6 +331,47 @@ class Context:
         s = Stats()
         self._chk(self._L.kc_get_stats(self._h, ctypes.byref(s)))
         return s.as_dict()
+
+
+def owner_of(key0: int, world: int) -> int:
+    """Key-space owner of a key: ((word0 >> 32) * world) >> 32,
+    the top log2(world) bits of word 0 when world is a power of two; monotone
+    in the key, so owner order is SortedKMerFile order (kc.h kc_owner_counts)."""
+    return ((key0 >> 32) * world) >> 32
+
+
+def keyspace_exchange(run, dist, device) -> int:
+    """Key-space partition step of cfg4: every rank has counted its
+    own reads into a finished sorted run; rank o ends up owning the keys with
+    owner_of(key) == o, summed over all ranks, so the ranks' outputs
+    concatenated in rank order are the whole node's SortedKMerFile.
+
+    `run` is a Context (or anything with finish/owner_counts/export_records/
+    merge_records and rs); `dist` an initialised torch.distributed (RCCL on
+    GPUs: `device` is the rank's cuda device and the records never leave HBM;
+    gloo: `device` is cpu and the records are staged through host memory).
+    One all-to-all of world u64 counts, then one all-to-all of the packed
+    records (12 B per record at k<=32). Returns the rank's merged record count.
+    """
+    import torch
+
+    world = dist.get_world_size()
+    rs = run.rs
+    n = run.finish()
+    counts = run.owner_counts(world)
+    send = torch.empty(n * rs, dtype=torch.uint8, device=device)
+    run.export_records(send)
+    sc = torch.tensor(counts, dtype=torch.int64, device=device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc)
+    rcounts = [int(x) for x in rc.tolist()]
+    m = sum(rcounts)
+    recv = torch.empty(m * rs, dtype=torch.uint8, device=device)
+    dist.all_to_all_single(recv, send, [c * rs for c in rcounts], [c * rs for c in counts])
+    if recv.is_cuda:
+        torch.cuda.current_stream(recv.device).synchronize()  # RCCL ran on torch's stream
+    del send
+    return run.merge_records(recv, m)
 
 
 class Options:

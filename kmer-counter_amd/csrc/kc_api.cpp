@@ -721,6 +721,8 @@ kc_status kc_check_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, ui
     return fastq_host(c, fastq, n, L, n_reads, false);
 }
 
+static kc_status sort_reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, bool dups, uint64_t* n_out);
+
 // Finish of the partition engine: LDS records + fallback-table records + key 0
 // -> radix sort -> (sum duplicates when several batches or the fallback table
 // contributed) -> pack.
@@ -756,10 +758,20 @@ static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
     uint64_t n = 0;
     HIPCHK(c, hipMemcpyAsync(&n, cursor, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return sort_reduce_pack(c, out_cap, n, c->batches > 1 || t > 0, n_out);
+}
+
+// fin_keys[0]/fin_cnts[0] hold n records at stride out_cap: radix sort, sum
+// equal keys when `dups` may exist, pack into fin_packed.
+static kc_status sort_reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, bool dups, uint64_t* n_out) {
+    kc_status s;
+    const int W = c->W;
+    uint64_t* k0 = (uint64_t*)c->fin_keys[0].p;
+    uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
     int which = 0;
     if ((s = sort_records(c, k0, (uint64_t*)c->fin_keys[1].p, c0, (uint32_t*)c->fin_cnts[1].p, out_cap, n, &which)))
         return s;
-    if ((c->batches > 1 || t > 0) && n > 1) {
+    if (dups && n > 1) {
         uint64_t* ks = (uint64_t*)c->fin_keys[which].p;
         uint32_t* cs = (uint32_t*)c->fin_cnts[which].p;
         uint64_t* ko = (uint64_t*)c->fin_keys[which ^ 1].p;
@@ -1031,6 +1043,58 @@ kc_status kc_synth_fastq_device(kc_ctx* c, const kc_synth_spec* sp, void** d_out
 kc_status kc_synth_free(kc_ctx* c, void* d_buf) {
     if (!c) return KC_ERR_ARG;
     if (d_buf) HIPCHK(c, hipFree(d_buf));
+    return KC_OK;
+}
+
+kc_status kc_owner_counts(kc_ctx* c, uint32_t world, uint64_t* counts) {
+    if (!c || world == 0 || !counts) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist: the key-space exchange needs one run");
+    kc_status s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if ((s = ensure(c, c->part_starts, ((size_t)world + 1) * 8))) return s;
+    HIPCHK(c, launch_owner_bounds(c->fin_packed.p, c->rs, c->n_records, world, (uint64_t*)c->part_starts.p, c->stream));
+    std::vector<uint64_t> b(world + 1);
+    HIPCHK(c, hipMemcpyAsync(b.data(), c->part_starts.p, (world + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (uint32_t o = 0; o < world; o++) counts[o] = b[o + 1] - b[o];
+    return KC_OK;
+}
+
+kc_status kc_merge_records_device(kc_ctx* c, const void* d_packed, uint64_t n_records) {
+    if (!c || (!d_packed && n_records)) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist");
+    kc_status s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const uint64_t out_cap = n_records + 1;
+    const int W = c->W;
+    for (int i = 0; i < 2; i++) {
+        if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
+            return s;
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_unpack(W, d_packed, n_records, (uint64_t*)c->fin_keys[0].p, out_cap,
+                            (uint32_t*)c->fin_cnts[0].p, c->stream));
+    uint64_t n = 0;
+    if ((s = sort_reduce_pack(c, out_cap, n_records, true, &n))) return s;
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    c->st.finish_ms += t;
+    c->n_records = n;
+    c->st.output_records = n;
+    c->finished = true;
+    return KC_OK;
+}
+
+kc_status kc_copy_device(kc_ctx* c, void* d_dst, const void* d_src, uint64_t n) {
+    if (!c || (n && (!d_dst || !d_src))) return KC_ERR_ARG;
+    if (n == 0) return KC_OK;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipMemcpyAsync(d_dst, d_src, n, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return KC_OK;
 }
 

@@ -132,6 +132,13 @@ hipError_t launch_rle_counts(const uint32_t* head_idx, uint64_t m, uint64_t n, u
 hipError_t launch_pack(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n, void* out,
                        hipStream_t s);
 
+// Key-space partition: bounds[o] = first packed record with owner >= o
+// (o in [0, world]); unpack packed records into SoA.
+hipError_t launch_owner_bounds(const void* packed, int rs, uint64_t n, uint32_t world, uint64_t* bounds,
+                               hipStream_t s);
+hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, uint64_t stride, uint32_t* cnts,
+                         hipStream_t s);
+
 // FASTQ block index (K1).
 uint64_t fq_chunks(const void* base, uint64_t n);
 hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hipStream_t s);

@@ -1600,6 +1600,62 @@ hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const
 }
 
 // ---------------------------------------------------------------------------
+// Key-space partition: owner(key) = ((word0 >> 32) * world)
+// >> 32 is monotone in the key, so the owners of a sorted record run are
+// contiguous ranges; received runs are unpacked, re-sorted and summed.
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void owner_bounds_k(const uint8_t* __restrict__ packed, int rs, u64 n,
+                                                         u32 world, u64* __restrict__ bounds) {
+    for (u32 o = blockIdx.x * kBlock + threadIdx.x; o <= world; o += gridDim.x * kBlock) {
+        u64 lo = 0, hi = n;
+        while (lo < hi) {
+            u64 mid = (lo + hi) >> 1;
+            const u32* w = (const u32*)(packed + mid * (u64)rs);
+            u64 top = w[1];  // high half of word 0 (little endian)
+            u32 owner = (u32)((top * world) >> 32);
+            if (owner < o)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        bounds[o] = lo;
+    }
+}
+
+hipError_t launch_owner_bounds(const void* packed, int rs, uint64_t n, uint32_t world, uint64_t* bounds,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(owner_bounds_k, dim3(1), dim3(kBlock), 0, s, (const uint8_t*)packed, rs, n, world, bounds);
+    return hipGetLastError();
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void unpack_records_k(const u32* __restrict__ in, u64 n, u64* __restrict__ keys,
+                                                           u64 stride, u32* __restrict__ cnts) {
+    constexpr int RW = 2 * W + 1;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        const u32* r = in + i * RW;
+#pragma unroll
+        for (int j = 0; j < W; j++) keys[(u64)j * stride + i] = (u64)r[2 * j] | ((u64)r[2 * j + 1] << 32);
+        cnts[i] = r[2 * W];
+    }
+}
+
+hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, uint64_t stride, uint32_t* cnts,
+                         hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    int g = grid_for(n);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(unpack_records_k<1>, dim3(g), dim3(kBlock), 0, s, (const u32*)packed, n, keys, stride, cnts); break;
+    case 2: hipLaunchKernelGGL(unpack_records_k<2>, dim3(g), dim3(kBlock), 0, s, (const u32*)packed, n, keys, stride, cnts); break;
+    case 3: hipLaunchKernelGGL(unpack_records_k<3>, dim3(g), dim3(kBlock), 0, s, (const u32*)packed, n, keys, stride, cnts); break;
+    case 4: hipLaunchKernelGGL(unpack_records_k<4>, dim3(g), dim3(kBlock), 0, s, (const u32*)packed, n, keys, stride, cnts); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // K1: FASTQ block index. The block is viewed through 16-byte-aligned 64 KiB
 // chunks of the address space; fq_count counts '\n' per chunk, a device scan
 // turns counts into each chunk's first line index, and fq_emit re-reads the

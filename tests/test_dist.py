@@ -66,3 +66,109 @@ def test_shards_are_disjoint_and_cover(kca):
     per = 1000
     parts = [kca.synth_fastq(per, 100, 7, first_read=bench.shard_first(r, per)) for r in range(3)]
     assert b"".join(parts) == kca.synth_fastq(3 * per, 100, 7)
+
+
+class _OracleRun:
+    """Test stand-in for a finished Context on a rank without a GPU: holds the
+    oracle's sorted run and implements the four methods keyspace_exchange
+    uses (finish/owner_counts/export_records/merge_records) on the host, so
+    the protocol (count all-to-all, contiguous owner slices, record
+    all-to-all, merge on the owner) is exercised over gloo. The device side
+    of the same methods is tests/test_gpu_parity.py::test_keyspace_*."""
+
+    def __init__(self, records: bytes, k: int, kca):
+        self.W = (k + 31) // 32
+        self.rs = 8 * self.W + 4
+        self.data = records
+        self.kca = kca
+
+    def _keys(self, data):
+        import numpy as np
+        n = len(data) // self.rs
+        a = np.frombuffer(data, dtype=np.uint8).reshape(n, self.rs)
+        return a, n
+
+    def finish(self):
+        return len(self.data) // self.rs
+
+    def owner_counts(self, world):
+        a, n = self._keys(self.data)
+        counts = [0] * world
+        for i in range(n):
+            key0 = int.from_bytes(a[i, 0:8].tobytes(), "little")
+            counts[self.kca.owner_of(key0, world)] += 1
+        return counts
+
+    def export_records(self, dst):
+        import torch
+        dst[: len(self.data)] = torch.frombuffer(bytearray(self.data), dtype=torch.uint8)
+        return self.finish()
+
+    def merge_records(self, src, m):
+        raw = bytes(src[: m * self.rs].numpy().tobytes())
+        acc = {}
+        for i in range(m):
+            r = raw[i * self.rs:(i + 1) * self.rs]
+            key = tuple(int.from_bytes(r[8 * j:8 * j + 8], "little") for j in range(self.W))
+            acc[key] = (acc.get(key, 0) + int.from_bytes(r[-4:], "little")) & 0xFFFFFFFF
+        out = bytearray()
+        for key in sorted(acc):
+            for w in key:
+                out += w.to_bytes(8, "little")
+            out += acc[key].to_bytes(4, "little")
+        self.data = bytes(out)
+        return len(acc)
+
+
+def _ks_worker(rank, world, port, tmpdir, per, k):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import oracle
+    from conftest import load_pkg
+    from test_dist import _OracleRun
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kca = load_pkg()
+    fq = kca.synth_fastq(per, 150, 2, genome_length=200_000, first_read=bench.shard_first(rank, per))
+    run = _OracleRun(oracle.count_fastq(fq, k), k, kca)
+    n = kca.keyspace_exchange(run, dist, torch.device("cpu"))
+    assert n == run.finish()
+    with open(os.path.join(tmpdir, f"owned{rank}"), "wb") as f:
+        f.write(run.data)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 31), (3, 55)])
+def test_keyspace_exchange_concatenates_to_whole(kca, orc, tmp_path, world, k):
+    """cfg4: after the exchange every rank holds only its own key range, and
+    the ranks' outputs concatenated in rank order are the whole stream's
+    SortedKMerFile (no merge)."""
+    per = 800
+    mp.spawn(_ks_worker, args=(world, _free_port(), str(tmp_path), per, k), nprocs=world, join=True)
+    parts = [(tmp_path / f"owned{r}").read_bytes() for r in range(world)]
+    whole = kca.synth_fastq(world * per, 150, 2, genome_length=200_000)
+    assert b"".join(parts) == orc.count_fastq(whole, k)
+    rs = 8 * ((k + 31) // 32) + 4
+    for r, p in enumerate(parts):
+        assert len(p) > 0
+        for i in range(0, len(p), rs):
+            assert kca.owner_of(int.from_bytes(p[i:i + 8], "little"), world) == r
+
+
+def test_owner_of_is_monotone_and_top_bits(kca):
+    import random
+    rng = random.Random(4)
+    keys = sorted(rng.getrandbits(64) for _ in range(2000)) + [0, (1 << 64) - 1]
+    keys.sort()
+    for world in (1, 2, 3, 5, 8):
+        owners = [kca.owner_of(x, world) for x in keys]
+        assert owners == sorted(owners) and owners[0] == 0 and owners[-1] == world - 1
+    assert all(kca.owner_of(x, 8) == x >> 61 for x in keys)

@@ -272,3 +272,105 @@ def test_config2_full_size_properties(kca):
     idx = np.searchsorted(recs["k"], keys)
     assert np.all(recs["k"][idx] == keys)
     assert np.all(recs["c"][idx] >= np.array([cnt[key] for key in cnt], dtype=np.uint32))
+
+
+def _owner_slices(kca, recs, rs, world):
+    out = [bytearray() for _ in range(world)]
+    for i in range(0, len(recs), rs):
+        out[kca.owner_of(int.from_bytes(recs[i:i + 8], "little"), world)] += recs[i:i + rs]
+    return [bytes(o) for o in out]
+
+
+@pytest.mark.parametrize("k,world", [(31, 3), (55, 2), (21, 8), (100, 5)])
+def test_keyspace_split_and_merge_device(kca, orc, k, world, engine):
+    """cfg4 device side in one process: `world` contexts count disjoint shards;
+    kc_owner_counts splits each sorted run into contiguous owner slices; owner
+    o's context merges (kc_merge_records_device) the slices it would receive;
+    the owners' runs concatenated are the oracle count of the whole stream."""
+    import torch
+
+    per, L = 1500, 150
+    dev = torch.device("cuda", 0)
+    shards = [kca.synth_fastq(per, L, 11, n_rate=0.001, genome_length=100_000, first_read=r * per)
+              for r in range(world)]
+    ctxs = [kca.Context(kmer_length=k, line_length=L, engine=engine) for _ in range(world)]
+    try:
+        slices = []
+        for c, fq in zip(ctxs, shards):
+            c.count_fastq(fq)
+            recs = c.records()
+            counts = c.owner_counts(world)
+            sl = _owner_slices(kca, recs, c.rs, world)
+            assert counts == [len(s) // c.rs for s in sl]
+            assert b"".join(sl) == recs
+            t = torch.empty(len(recs), dtype=torch.uint8, device=dev)
+            assert c.export_records(t) == len(recs) // c.rs
+            assert bytes(t.cpu().numpy().tobytes()) == recs
+            slices.append(sl)
+        owned = []
+        for o, c in enumerate(ctxs):
+            buf = b"".join(slices[r][o] for r in range(world))
+            src = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(dev) if buf else \
+                torch.empty(0, dtype=torch.uint8, device=dev)
+            n = c.merge_records(src, len(buf) // c.rs)
+            got = c.records()
+            assert n == len(got) // c.rs
+            owned.append(got)
+        assert b"".join(owned) == orc.count_fastq(b"".join(shards), k)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_merge_records_device_sums_shuffled_duplicates(kca, orc):
+    """kc_merge_records_device takes records in any order with repeated keys:
+    shuffled records of two runs (and a run merged with itself) come back
+    sorted with summed counts; u32 wrap as in the reference's uint32 counts."""
+    import torch
+
+    k, L = 55, 120
+    a = orc.count_fastq(kca.synth_fastq(3000, L, 5, n_rate=0.002), k)
+    b = orc.count_fastq(kca.synth_fastq(3000, L, 6, n_rate=0.002), k)
+    rs = orc.rs_of(k)
+    recs = [a[i:i + rs] for i in range(0, len(a), rs)] + [b[i:i + rs] for i in range(0, len(b), rs)]
+    random.Random(3).shuffle(recs)
+    with kca.Context(kmer_length=k, line_length=L) as ctx:
+        ctx.count_fastq(kca.synth_fastq(3000, L, 5, n_rate=0.002))
+        ctx.count_fastq(kca.synth_fastq(3000, L, 6, n_rate=0.002))
+        want = ctx.records()
+        src = torch.frombuffer(bytearray(b"".join(recs)), dtype=torch.uint8).cuda()
+        assert ctx.merge_records(src, len(recs)) * rs == len(want)
+        assert ctx.records() == want
+        big = bytearray(want[:rs])
+        big[-4:] = (0xFFFFFFFF).to_bytes(4, "little")
+        two = torch.frombuffer(bytearray(bytes(big) * 2), dtype=torch.uint8).cuda()
+        assert ctx.merge_records(two, 2) == 1
+        assert ctx.records() == bytes(big[:-4]) + (0xFFFFFFFE).to_bytes(4, "little")
+        assert ctx.merge_records(torch.empty(0, dtype=torch.uint8).cuda(), 0) == 0
+        assert ctx.records() == b""
+
+
+def test_keyspace_exchange_rccl_world1(kca, orc):
+    """keyspace_exchange over RCCL (backend nccl) at world size 1: the count
+    all-to-all, the record all-to-all and the device merge run on HBM-resident
+    tensors; the result is the rank's own count. Ranks > 1 are covered by the
+    gloo tests in tests/test_dist.py (the 1-GPU box cannot host two RCCL ranks)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        fq = kca.synth_fastq(4000, 150, 9, n_rate=0.001)
+        with kca.Context(kmer_length=31, line_length=150) as ctx:
+            ctx.count_fastq(fq)
+            n = kca.keyspace_exchange(ctx, dist, torch.device("cuda", 0))
+            got = ctx.records()
+        assert got == orc.count_fastq(fq, 31) and n * 12 == len(got)
+    finally:
+        dist.destroy_process_group()
