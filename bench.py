@@ -92,18 +92,26 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=50_000_000, help="reads per GPU")
-    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="SURVEY §8d preset: 2 = k=31, 50M x 150 bp from a 250 Mbp genome (the metric's "
+                         "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality)")
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--L", type=int, default=150)
-    ap.add_argument("--genome", type=int, default=250_000_000)
-    ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--mem", type=int, default=160 << 30, help="gpuMemoryLimit per GPU (bytes)")
+    ap.add_argument("--genome", type=int, default=None, help="0 = iid uniform reads")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--mem", type=int, default=None, help="gpuMemoryLimit per GPU (bytes)")
     ap.add_argument("--engine", default="partition", choices=["partition", "table"])
     ap.add_argument("--cpu-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
                     help="N>1: key-space all-to-all (cfg4) or read-shard only (cfg3); ignored at N=1")
     args = ap.parse_args()
+    preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
+              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=64 << 30)}[args.config]
+    for key, v in preset.items():
+        if getattr(args, key) is None:
+            setattr(args, key, v)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -192,7 +200,7 @@ def main():
     kmers_per_launch = windows_per_gpu * args.steps / max(1, launches)
     achieved = b_per_kmer * kmers_per_launch / (avg_launch_ms / 1e3) / 1e9
     traffic = load_traffic()
-    kernel = "count_front<1,SINK_SCATTER> (P2)" if args.engine == "partition" else "count_front<1,SINK_TABLE>"
+    kernel = f"count_front<{W},SINK_SCATTER> (P2)" if args.engine == "partition" else f"count_front<{W},SINK_TABLE>"
     step_s = elapsed / args.steps
     path_achieved = b_per_kmer * windows_per_gpu / step_s / 1e9
     t_bytes = None
@@ -208,10 +216,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(kca, args.cpu_reads, L, k, args.genome, args.seed, 0)
 
-    base = (f"k={k}, {args.reads} x {L} bp reads per GPU sampled from a {args.genome} bp random genome "
-            f"(seed {args.seed}), FASTQ in HBM, in-HBM hash table")
+    src = (f"sampled from a {args.genome} bp random genome" if args.genome else "of iid uniform bases")
+    base = (f"k={k}, {args.reads} x {L} bp reads per GPU {src} (seed {args.seed}), FASTQ in HBM, "
+            f"in-HBM count")
     if world == 1:
-        workload, parallelism = "cfg2: " + base, "single GPU"
+        workload, parallelism = f"cfg{args.config}: " + base, "single GPU"
     elif exchange == "alltoall":
         workload = (f"cfg4 pattern at {world} GPUs: " + base + "; key-space all-to-all of the sorted (key, count) "
                     "records + per-GPU merge inside the step (output = concatenation of the ranks' runs)")

@@ -197,6 +197,11 @@ kc_status kc_owner_counts(kc_ctx* ctx, uint32_t world, uint64_t* counts);
  * stays finished; kc_reset starts a new count. KC_ERR_STATE before kc_finish
  * or when spill runs exist. */
 kc_status kc_merge_records_device(kc_ctx* ctx, const void* d_packed, uint64_t n_records);
+/* The same exchange between n contexts of one process (the CLI's gpus=N
+ * exchange=alltoall): context o ends up owning owner_of == o, so writing the
+ * contexts' runs one after another in order is the whole SortedKMerFile.
+ * Slices move by hipMemcpyPeer. Every ctx finished, same k, no spill runs. */
+kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n);
 /* Device->device copy on the ctx's stream (exchange staging). */
 kc_status kc_copy_device(kc_ctx* ctx, void* d_dst, const void* d_src, uint64_t n_bytes);
 

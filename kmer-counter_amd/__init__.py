@@ -138,6 +138,7 @@ def lib() -> ctypes.CDLL:
         "kc_owner_counts": ([vp, u32, P(u64)], ctypes.c_int),
         "kc_merge_records_device": ([vp, vp, u64], ctypes.c_int),
         "kc_copy_device": ([vp, vp, vp, u64], ctypes.c_int),
+        "kc_exchange_contexts": ([P(vp), u32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -338,6 +339,16 @@ def owner_of(key0: int, world: int) -> int:
     the top log2(world) bits of word 0 when world is a power of two; monotone
     in the key, so owner order is SortedKMerFile order (kc.h kc_owner_counts)."""
     return ((key0 >> 32) * world) >> 32
+
+
+def exchange_contexts(ctxs) -> None:
+    """kc_exchange_contexts: the key-space exchange between contexts of one
+    process; afterwards ctxs[o] holds the keys with owner_of(key) == o."""
+    L = lib()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    st = L.kc_exchange_contexts(arr, len(ctxs))
+    if st:
+        raise KcError(st, f"{L.kc_strerror(st).decode()}: {L.kc_last_error(ctxs[0]._h).decode()}")
 
 
 def keyspace_exchange(run, dist, device) -> int:

@@ -423,21 +423,44 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
             c->part_ms[3] += t;
 
+            // Records: at most one LDS table per bucket unless buckets were
+            // split into sub-range passes (high cardinality); on overflow P5
+            // reruns with a bigger buffer (safe while nothing went to the
+            // fallback table or the spill, whose inserts are not idempotent).
             uint64_t lslots = (uint64_t)bucket_lds_slots(W);
             uint64_t bound = (uint64_t)nb * lslots;
-            if ((s = grow_records(c, c->rec_n + (n < bound ? n : bound)))) return s;
-            // keys_a is free after P3: it takes P5's spills (capacity >= n)
-            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_count_buckets(W, c->keys_b, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
-                                           c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
-                                           c->keys_a, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
-                                           c->n_cu, c->stream));
-            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-            HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
-            if ((s = sync_stats(c))) return s;
-            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-            c->part_ms[4] += t;
-            if (c->stats_h[ST_ERR] & ERR_REC_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
+            if (bound > n) bound = n;
+            const uint64_t rec0 = c->rec_n;
+            const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
+            for (;;) {
+                if ((s = grow_records(c, rec0 + bound))) return s;
+                // keys_a is free after P3: it takes P5's spills (capacity >= n)
+                HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                HIPCHK(c, launch_count_buckets(W, c->keys_b, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
+                                               c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
+                                               c->keys_a, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
+                                               c->n_cu, c->stream));
+                HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+                if ((s = sync_stats(c))) return s;
+                HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                c->part_ms[4] += t;
+                if (getenv("KC_DEBUG"))
+                    fprintf(stderr, "kc: P5 n=%llu passes=%llu aborts=%llu max_m=%llu records=%llu %.3f ms\n",
+                            (unsigned long long)n, (unsigned long long)c->stats_h[ST_P5_PASSES],
+                            (unsigned long long)c->stats_h[ST_P5_ABORTS], (unsigned long long)c->stats_h[ST_P5_MAXM],
+                            (unsigned long long)c->rec_n, t);
+                if (!(c->stats_h[ST_ERR] & ERR_REC_OVERFLOW)) break;
+                if (bound >= n || c->stats_h[ST_CLAIMED] != claimed0 || c->stats_h[ST_SPILL2_FILL])
+                    return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
+                bound = n;
+                uint64_t err = c->stats_h[ST_ERR] & ~(uint64_t)ERR_REC_OVERFLOW;
+                HIPCHK(c, hipMemcpyAsync(c->stats + ST_ERR, &err, 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec0, 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                c->stats_h[ST_ERR] = err;
+                c->rec_n = rec0;
+            }
             if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
             uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
             if (n2) {
@@ -1086,6 +1109,68 @@ kc_status kc_merge_records_device(kc_ctx* c, const void* d_packed, uint64_t n_re
     c->n_records = n;
     c->st.output_records = n;
     c->finished = true;
+    return KC_OK;
+}
+
+kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n) {
+    if (!ctxs || n == 0) return KC_ERR_ARG;
+    for (uint32_t r = 0; r < n; r++) {
+        if (!ctxs[r] || ctxs[r]->W != ctxs[0]->W) return KC_ERR_ARG;
+        if (!ctxs[r]->finished) return fail(ctxs[r], KC_ERR_STATE, "call kc_finish first");
+        if (!ctxs[r]->runs.empty()) return fail(ctxs[r], KC_ERR_STATE, "spill runs exist");
+    }
+    const uint64_t rs = (uint64_t)ctxs[0]->rs;
+    std::vector<std::vector<uint64_t>> cnt(n, std::vector<uint64_t>(n));
+    kc_status s;
+    for (uint32_t r = 0; r < n; r++)
+        if ((s = kc_owner_counts(ctxs[r], n, cnt[r].data()))) return s;
+    // Gather every owner's slices before any merge: a merge overwrites the
+    // owner's own packed run, which the other owners still read from.
+    std::vector<void*> recv(n, nullptr);
+    std::vector<uint64_t> m(n, 0);
+    auto release = [&]() {
+        for (uint32_t o = 0; o < n; o++)
+            if (recv[o]) {
+                (void)hipSetDevice(ctxs[o]->cfg.device);
+                (void)hipFree(recv[o]);
+            }
+    };
+    for (uint32_t o = 0; o < n; o++) {
+        kc_ctx* co = ctxs[o];
+        for (uint32_t r = 0; r < n; r++) m[o] += cnt[r][o];
+        hipError_t e = hipSetDevice(co->cfg.device);
+        if (e == hipSuccess) e = hipMalloc(&recv[o], m[o] * rs + 16);
+        uint64_t off = 0;
+        for (uint32_t r = 0; r < n && e == hipSuccess; r++) {
+            uint64_t src = 0;
+            for (uint32_t p = 0; p < o; p++) src += cnt[r][p];
+            uint64_t bytes = cnt[r][o] * rs;
+            if (bytes)
+                e = hipMemcpyPeerAsync((uint8_t*)recv[o] + off, co->cfg.device,
+                                       (const uint8_t*)ctxs[r]->fin_packed.p + src * rs, ctxs[r]->cfg.device, bytes,
+                                       co->stream);
+            off += bytes;
+        }
+        if (e != hipSuccess) {
+            release();
+            return fail(co, KC_ERR_HIP, hipGetErrorString(e));
+        }
+    }
+    for (uint32_t o = 0; o < n; o++) {
+        hipError_t e = hipSetDevice(ctxs[o]->cfg.device);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctxs[o]->stream);
+        if (e != hipSuccess) {
+            release();
+            return fail(ctxs[o], KC_ERR_HIP, hipGetErrorString(e));
+        }
+    }
+    for (uint32_t o = 0; o < n; o++) {
+        if ((s = kc_merge_records_device(ctxs[o], recv[o], m[o]))) {
+            release();
+            return s;
+        }
+    }
+    release();
     return KC_OK;
 }
 

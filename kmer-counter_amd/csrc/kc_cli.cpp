@@ -7,7 +7,9 @@
 // Keys and defaults follow getOptions (main.cpp:25-70) and Options()
 // (Options.cpp:16-22): every argv (argv[0] included) is prefix-matched, unknown
 // keys are ignored, the last occurrence wins. Additive keys (not in the
-// reference): gpus=N, inputMode=auto|fastq|exact, tableBytes=B, quiet=1.
+// reference): gpus=N, exchange=none|alltoall (key-space exchange between the
+// GPUs' runs, output by concatenation; runs that spilled fall back to the
+// k-way merge), inputMode=auto|fastq|exact, tableBytes=B, quiet=1.
 //
 // Input (InputFileHandler.cpp:22-47): every directory entry whose name does
 // not start with '.', in readdir order; L of a file = length of its line 2
@@ -50,6 +52,7 @@ struct Options {
     uint32_t merge_threads = 2;
     // additive
     int gpus = 1;
+    std::string exchange = "none";
     std::string input_mode = "auto";
     uint64_t table_bytes = 0;
     bool quiet = false;
@@ -91,10 +94,15 @@ Options parse(int argc, char** argv) {
         }
         if (starts(a, "gpus=")) o.gpus = atoi(a + 5);
         if (starts(a, "inputMode=")) o.input_mode = a + 10;
+        if (starts(a, "exchange=")) o.exchange = a + 9;
         if (starts(a, "tableBytes=")) o.table_bytes = strtoull(a + 11, nullptr, 10);
         if (starts(a, "quiet=")) o.quiet = atoi(a + 6) != 0;
     }
     if (o.gpus < 1) o.gpus = 1;
+    if (o.exchange != "none" && o.exchange != "alltoall") {
+        fprintf(stderr, "exchange must be none or alltoall\n");
+        exit(1);
+    }
     return o;
 }
 
@@ -404,9 +412,34 @@ int main(int argc, char** argv) {
         kc_status s = kc_finish(w.ctx, &n);
         if (s) die(w.ctx, s, "finish");
     }
+    bool spilled = false;
+    for (auto& w : gw) {
+        kc_stats st;
+        kc_get_stats(w.ctx, &st);
+        spilled |= st.spill_runs > 0;
+    }
     if (o.gpus == 1) {
         kc_status s = kc_write_output(gw[0].ctx, o.output_file.c_str(), o.mergers_at_once, o.merge_threads);
         if (s) die(gw[0].ctx, s, "write output");
+    } else if (o.exchange == "alltoall" && !spilled) {
+        // key-space exchange: context g owns the g-th key range, so the output
+        // is the contexts' runs written one after another (no host merge)
+        std::vector<kc_ctx*> cs;
+        for (auto& w : gw) cs.push_back(w.ctx);
+        kc_status s = kc_exchange_contexts(cs.data(), (uint32_t)cs.size());
+        if (s) die(cs[0], s, "exchange");
+        FILE* out = fopen(o.output_file.c_str(), "wb");
+        if (!out) die(nullptr, KC_ERR_IO, o.output_file.c_str());
+        std::vector<char> buf;
+        for (auto& w : gw) {
+            uint64_t n = 0;
+            kc_finish(w.ctx, &n);
+            uint64_t rs = 8 * (uint64_t)((o.kmer_length + 31) / 32) + 4;
+            buf.resize(n * rs + 1);
+            if ((s = kc_copy_records(w.ctx, buf.data(), n * rs))) die(w.ctx, s, "copy records");
+            if (n && fwrite(buf.data(), 1, n * rs, out) != n * rs) die(nullptr, KC_ERR_IO, o.output_file.c_str());
+        }
+        if (fclose(out)) die(nullptr, KC_ERR_IO, o.output_file.c_str());
     } else {
         std::vector<std::string> all;
         for (auto& w : gw) {

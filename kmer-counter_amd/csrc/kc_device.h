@@ -16,6 +16,9 @@ enum Stat : int {
     ST_ERR = 5,          // bit set: ERR_* below
     ST_SPILL_FILL = 6,   // next free spill index (may exceed capacity on overflow)
     ST_SPILL2_FILL = 7,  // partition engine P5: keys spilled into the free key buffer
+    ST_P5_PASSES = 8,    // P5 sub-range passes emitted (diagnostic)
+    ST_P5_ABORTS = 9,    // P5 passes aborted on a full LDS table (diagnostic)
+    ST_P5_MAXM = 10,     // largest sub-range split m used (diagnostic)
     ST_N = 16
 };
 

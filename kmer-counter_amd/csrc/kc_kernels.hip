@@ -191,9 +191,14 @@ __device__ __forceinline__ bool insert_w1(u64 key, u64* __restrict__ table, u64 
 template <int W>
 __device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict__ table, u64 cap, u32 limit,
                                             bool* claimed) {
+    // One attempt per iteration and no spin inside divergent code: a lane that
+    // finds the slot being published (state 1) retries it next iteration. The
+    // claimer publishes within its own iteration, so a lane of the same
+    // wavefront can never wait on a masked-off claimer.
     constexpr int SW = (W <= 3) ? 4 : 8;
     u64 s = __umul64hi(hash_key<W>(key), cap);
-    for (u32 pr = 0; pr < limit; ++pr) {
+    u32 pr = 0, waits = 0;
+    for (;;) {
         u64* slot = table + SW * s;
         u32* cnt = (u32*)(slot + W);
         u32* state = cnt + 1;
@@ -212,11 +217,9 @@ __device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict
             }
             st = prev;
         }
-        u32 spins = 0;
-        while (st == 1u) {
-            if (++spins > 4096u) return false;
-            __builtin_amdgcn_s_sleep(1);
-            st = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == 1u) {
+            if (++waits > (1u << 22)) return false;  // claimer lost: treat as a full probe
+            continue;
         }
         bool eq = true;
 #pragma unroll
@@ -226,9 +229,9 @@ __device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict
             atomicAdd(cnt, 1u);
             return true;
         }
+        if (++pr >= limit) return false;
         if (++s == cap) s = 0;
     }
-    return false;
 }
 
 __device__ __forceinline__ u32 bytes_to_codes(u32 word, int nvalid, u32* bad_bits) {
@@ -1387,17 +1390,27 @@ struct BucketArgs {
     u32 probe_limit;
 };
 
+// `frac` is a 48-bit uniform hash fraction; slot = frac * lcap >> 48.
+// *claimed is set when this key took an empty slot.
 template <int W>
-__device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 h, u64* lkeys, u32* lcnt, u32* lstate, u32 lcap) {
-    u32 slot = (u32)(((h & 0xffffffffffffull) * (u64)lcap) >> 48);
-    for (u32 pr = 0; pr < lcap; ++pr) {
-        if constexpr (W == 1) {
+__device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* lkeys, u32* lcnt, u32* lstate,
+                                           u32 lcap, u32 max_probe, bool* claimed) {
+    u32 slot = (u32)((frac * (u64)lcap) >> 48);
+    if constexpr (W == 1) {
+        for (u32 pr = 0; pr < max_probe; ++pr) {
             u64 old = atomicCAS((unsigned long long*)&lkeys[slot], 0ull, (unsigned long long)key[0]);
             if (old == 0ull || old == key[0]) {
                 atomicAdd(&lcnt[slot], 1u);
+                *claimed = old == 0ull;
                 return true;
             }
-        } else {
+            if (++slot == lcap) slot = 0;
+        }
+        return false;
+    } else {
+        // as insert_wide: one attempt per iteration, no divergent spin
+        u32 pr = 0;
+        for (;;) {
             u32 st = __hip_atomic_load(&lstate[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (st == 0u) {
                 u32 prev = atomicCAS(&lstate[slot], 0u, 1u);
@@ -1406,15 +1419,12 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 h, u64* lkey
                     for (int j = 0; j < W; j++) lkeys[(size_t)j * lcap + slot] = key[j];
                     atomicAdd(&lcnt[slot], 1u);
                     __hip_atomic_store(&lstate[slot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    *claimed = true;
                     return true;
                 }
                 st = prev;
             }
-            u32 spins = 0;
-            while (st == 1u) {
-                if (++spins > (1u << 20)) return false;
-                st = __hip_atomic_load(&lstate[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
+            if (st == 1u) continue;  // being published: retry the same slot
             bool eq = true;
 #pragma unroll
             for (int j = 0; j < W; j++) eq = eq && lkeys[(size_t)j * lcap + slot] == key[j];
@@ -1422,11 +1432,23 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 h, u64* lkey
                 atomicAdd(&lcnt[slot], 1u);
                 return true;
             }
+            if (++pr >= max_probe) return false;
+            if (++slot == lcap) slot = 0;
         }
-        if (++slot == lcap) slot = 0;
     }
-    return false;
 }
+
+// P5: one 1024-thread block per bucket at a time counts the bucket's keys in
+// an LDS open-addressed table and emits (key, count) records. A bucket with
+// more distinct keys than the table holds (high-cardinality input, SURVEY
+// cfg5) is counted in m sub-range passes: pass j takes the keys whose hash
+// fraction ((h & 2^48-1) * m) >> 48 equals j and slots them by the remaining
+// fraction bits, so every pass uses the whole table. m starts at 1; a pass
+// whose table passes ~81% fill aborts, the LDS table is cleared and m grows
+// by a power of two (estimated from fill / keys scanned), so finished
+// sub-ranges stay valid. Only at m == kMaxSub do keys that miss the table go
+// to the global fallback table and then to the spill buffer.
+constexpr u32 kMaxSub = 1024;
 
 template <int W>
 __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
@@ -1434,7 +1456,10 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
     u64* lkeys = (u64*)smem;                                  // W x lcap
     u32* lcnt = (u32*)(lkeys + (size_t)W * a.lcap);           // lcap
     u32* lstate = lcnt + a.lcap;                              // lcap (W >= 2)
-    u32* misc = lstate + (W >= 2 ? a.lcap : 0);               // scan scratch (16) + base (2)
+    u32* misc = lstate + (W >= 2 ? a.lcap : 0);               // scan scratch (16), base (2), fill, abort, m
+    u32* lfill = misc + 20;
+    u32* labort = misc + 21;
+    u32* lnext = misc + 22;
     const int tid = threadIdx.x;
     for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
@@ -1442,96 +1467,168 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         lcnt[i] = 0;
         if constexpr (W >= 2) lstate[i] = 0;
     }
+    if (tid == 0) {
+        *lfill = 0;
+        *labort = 0;
+    }
     __syncthreads();
+    const u32 limit = (a.lcap * 13u) >> 4;
+    const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;  // tiny test tables: global fallback only
+    constexpr u64 M48 = 0xffffffffffffull;
     for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        // a full record buffer ends the launch early (the host reruns P5)
+        if (tid == 0)
+            *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) &
+                           ERR_REC_OVERFLOW);
+        __syncthreads();
+        const bool stop = *lnext != 0u;
+        __syncthreads();
+        if (stop) return;
         const u64 lo = a.starts[b], hi = a.starts[b + 1];
-        constexpr int U = 4;  // independent key loads in flight per thread
-        for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
-            u64 key[U][W];
-            bool live[U];
+        u32 m = 1, sub = 0;
+        while (sub < m) {
+            const bool last = m >= mmax;
+            u64 scanned = 0;
+            constexpr int U = 4;  // independent key loads in flight per thread
+            for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
+                if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                scanned += (u64)U * kBucketBlock;
+                u64 key[U][W];
+                bool live[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const u64 i = base + (u64)u * kBucketBlock + tid;
-                live[u] = i < hi;
+                for (int u = 0; u < U; u++) {
+                    const u64 i = base + (u64)u * kBucketBlock + tid;
+                    live[u] = i < hi;
 #pragma unroll
-                for (int j = 0; j < W; j++) key[u][j] = live[u] ? a.keys[(u64)j * a.stride + i] : 0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                bool done = true, claimed = false;
-                if (live[u]) {
-                    u64 h = hash_key<W>(key[u]);
-                    if (!lds_insert<W>(key[u], h, lkeys, lcnt, lstate, a.lcap)) {
-                        if constexpr (W == 1)
-                            done = insert_w1(key[u][0], a.table, a.cap, a.probe_limit, &claimed);
-                        else
-                            done = insert_wide<W>(key[u], a.table, a.cap, a.probe_limit, &claimed);
-                    }
+                    for (int j = 0; j < W; j++) key[u][j] = live[u] ? a.keys[(u64)j * a.stride + i] : 0ull;
                 }
-                u64 cm = __ballot(claimed);
-                if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
-                    atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-                bool spill = !done;
-                if (__ballot(spill)) {
-                    u64 idx = wave_reserve(a.spill_ctr, spill);
-                    if (spill) {
-                        if (idx < a.spill_cap) {
 #pragma unroll
-                            for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[u][j];
-                        } else {
-                            atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                for (int u = 0; u < U; u++) {
+                    bool done = true, claimed = false, lclaim = false, full = false;
+                    // once the pass is aborted the rest of it is skipped: a
+                    // full table would make every further key probe all slots
+                    if (live[u] && (last || !*(volatile u32*)labort)) {
+                        const u64 x = (hash_key<W>(key[u]) & M48) * (u64)m;
+                        if ((u32)(x >> 48) == sub) {
+                            if (!lds_insert<W>(key[u], x & M48, lkeys, lcnt, lstate, a.lcap,
+                                               last ? a.lcap : (a.lcap < 256u ? a.lcap : 256u), &lclaim)) {
+                                if (!last) {
+                                    full = true;
+                                } else if constexpr (W == 1) {
+                                    done = insert_w1(key[u][0], a.table, a.cap, a.probe_limit, &claimed);
+                                } else {
+                                    done = insert_wide<W>(key[u], a.table, a.cap, a.probe_limit, &claimed);
+                                }
+                            }
+                        }
+                    }
+                    const u64 lm = __ballot(lclaim);
+                    const u64 fm = __ballot(full);
+                    const int leader = (int)lane_id() == 0;
+                    if (!last && (lm || fm) && leader) {
+                        u32 f = atomicAdd(lfill, (u32)__popcll(lm)) + (u32)__popcll(lm);
+                        if (fm || f > limit) atomicOr(labort, 1u);
+                    }
+                    if (last) {
+                        u64 cm = __ballot(claimed);
+                        if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                            atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+                        bool spill = !done;
+                        if (__ballot(spill)) {
+                            u64 idx = wave_reserve(a.spill_ctr, spill);
+                            if (spill) {
+                                if (idx < a.spill_cap) {
+#pragma unroll
+                                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[u][j];
+                                } else {
+                                    atomicOr((unsigned long long*)&a.stats[ST_ERR],
+                                             (unsigned long long)ERR_SPILL_OVERFLOW);
+                                }
+                            }
                         }
                     }
                 }
             }
-        }
-        __syncthreads();
-        // emit the occupied slots in slot order: count, one reservation, then
-        // rounds of 1024 consecutive slots with a block scan, so consecutive
-        // lanes write consecutive records
-        u32 mine = 0;
-        for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
-            bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
-            mine += occ ? 1u : 0u;
-        }
-        u32 total;
-        (void)block_excl_scan_n<kBucketBlock>(mine, misc, &total);
-        if (tid == 0) {
-            u64 base = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
-            *(u64*)(misc + 16) = base;
-            if (base + total > a.rec_cap)
-                atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
-        }
-        __syncthreads();
-        u64 pos = *(u64*)(misc + 16);
-        for (u32 r0 = 0; r0 < a.lcap; r0 += kBucketBlock) {
-            const u32 i = r0 + tid;
-            bool occ = false;
-            if (i < a.lcap) occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
-            u32 rt;
-            u32 before = block_excl_scan_n<kBucketBlock>(occ ? 1u : 0u, misc, &rt);
-            if (occ) {
-                u64 q = pos + before;
-                if (q < a.rec_cap) {
-#pragma unroll
-                    for (int j = 0; j < W; j++) a.rec_keys[(u64)j * a.rec_cap + q] = lkeys[(size_t)j * a.lcap + i];
-                    a.rec_cnts[q] = lcnt[i];
+            __syncthreads();
+            const bool aborted = *labort != 0u;  // every thread reads before tid 0 resets it
+            __syncthreads();
+            if (aborted) {
+                // finer split: m' = m * 2^s from the fill rate seen so far
+                if (tid == 0) {
+                    const u64 est = (u64)(*lfill) * m * (hi - lo) / (scanned ? scanned : 1);
+                    u32 nm = m * 2;
+                    while (nm < mmax && (u64)nm * ((u64)limit * 7 / 8) < est) nm *= 2;
+                    *lnext = nm < mmax ? nm : mmax;
+                    *lfill = 0;
+                    *labort = 0;
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_ABORTS], 1ull);
+                    atomicMax((unsigned long long*)&a.stats[ST_P5_MAXM], (unsigned long long)*lnext);
                 }
-                // leave the slot empty for the next bucket
+                for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
-                for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
-                lcnt[i] = 0;
-                if constexpr (W >= 2) lstate[i] = 0;
+                    for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+                    lcnt[i] = 0;
+                    if constexpr (W >= 2) lstate[i] = 0;
+                }
+                __syncthreads();
+                const u32 nm = *lnext;
+                sub *= nm / m;
+                m = nm;
+                __syncthreads();
+                continue;
             }
-            pos += rt;
+            // emit the occupied slots in slot order: count, one reservation,
+            // then rounds of 1024 consecutive slots with a block scan, so
+            // consecutive lanes write consecutive records
+            u32 mine = 0;
+            for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+                bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
+                mine += occ ? 1u : 0u;
+            }
+            u32 total;
+            (void)block_excl_scan_n<kBucketBlock>(mine, misc, &total);
+            if (tid == 0) {
+                u64 rbase = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
+                *(u64*)(misc + 16) = rbase;
+                atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                if (rbase + total > a.rec_cap)
+                    atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                *lfill = 0;
+            }
+            __syncthreads();
+            u64 pos = *(u64*)(misc + 16);
+            for (u32 r0 = 0; r0 < a.lcap; r0 += kBucketBlock) {
+                const u32 i = r0 + tid;
+                bool occ = false;
+                if (i < a.lcap) occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
+                u32 rt;
+                u32 before = block_excl_scan_n<kBucketBlock>(occ ? 1u : 0u, misc, &rt);
+                if (occ) {
+                    u64 q = pos + before;
+                    if (q < a.rec_cap) {
+#pragma unroll
+                        for (int j = 0; j < W; j++)
+                            a.rec_keys[(u64)j * a.rec_cap + q] = lkeys[(size_t)j * a.lcap + i];
+                        a.rec_cnts[q] = lcnt[i];
+                    }
+                    // leave the slot empty for the next pass
+#pragma unroll
+                    for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+                    lcnt[i] = 0;
+                    if constexpr (W >= 2) lstate[i] = 0;
+                }
+                pos += rt;
+            }
+            __syncthreads();
+            ++sub;
         }
-        __syncthreads();
     }
 }
 
 size_t bucket_lds_bytes(int W) {
     size_t lcap = (size_t)bucket_lds_slots(W);
-    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + 18 * 4 + 16;
+    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + 24 * 4 + 16;
 }
 
 hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, const uint64_t* starts,

@@ -374,3 +374,57 @@ def test_keyspace_exchange_rccl_world1(kca, orc):
         assert got == orc.count_fastq(fq, 31) and n * 12 == len(got)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_exchange_contexts_in_process(kca, orc, k):
+    """kc_exchange_contexts: four contexts of one process (hipMemcpyPeer
+    slices), each then owns one key range; concatenation = whole count."""
+    shards = [kca.synth_fastq(1200, 150, 21 + r, n_rate=0.002, genome_length=50_000) for r in range(4)]
+    ctxs = [kca.Context(kmer_length=k, line_length=150) for _ in shards]
+    try:
+        for c, fq in zip(ctxs, shards):
+            c.count_fastq(fq)
+            c.finish()
+        kca.exchange_contexts(ctxs)
+        parts = [c.records() for c in ctxs]
+    finally:
+        for c in ctxs:
+            c.close()
+    assert b"".join(parts) == orc.count_fastq(b"".join(shards), k)
+    assert all(parts)
+
+
+@pytest.mark.parametrize("mem", [100000000, 1048576])
+def test_cli_exchange_alltoall(kca, orc, tmp_path, mem):
+    """exchange=alltoall with gpus=3: output by concatenation of the contexts'
+    key ranges; with a 1 MiB gpuMemoryLimit the contexts spill and the CLI
+    takes the k-way merge instead. Same bytes either way."""
+    d = tmp_path / "in"
+    d.mkdir()
+    texts = []
+    for i in range(4):
+        t = kca.synth_fastq(3000, 150, seed=50 + i, n_rate=0.001)
+        (d / f"f{i}.fq").write_bytes(t)
+        texts.append(t)
+    out = tmp_path / "o.bin"
+    subprocess.run([kca.CLI_PATH, "kmerLength=31", f"inputFileLocation={d}", f"outputFile={out}",
+                    f"tempFileLocation={tmp_path}", "gpus=3", "exchange=alltoall", f"gpuMemoryLimit={mem}",
+                    "quiet=1"], check=True, capture_output=True)
+    want = orc.count_chunks([(c, ll) for t in texts for c, ll in orc.chunks_of(t, orc.chunk_size(150, 31, mem))], 31)
+    assert out.read_bytes() == want
+
+
+@pytest.mark.parametrize("k,slots", [(31, 64), (55, 64), (31, 128), (100, 96)])
+def test_partition_subrange_passes(kca, orc, k, slots):
+    """High cardinality per bucket (SURVEY cfg5 shape, scaled down by a small
+    LDS table): buckets overflow the table and are counted in m sub-range
+    passes, still entirely in LDS (no spill, no fallback-table claims)."""
+    n, L = 40000, 150
+    fq = kca.synth_fastq(n, L, seed=k + slots, n_rate=0.0005)
+    with kca.Context(kmer_length=k, line_length=L, lds_slots=slots) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert got == orc.count_fastq(fq, k)
+    assert st["spilled_kmers"] == 0 and st["table_used"] == 0
