@@ -61,6 +61,7 @@ struct kc_ctx {
     uint64_t* keys_a = nullptr;    // W x key_cap
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
+    DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
     uint64_t* rec_keys = nullptr;  // W x rec_cap
     uint32_t* rec_cnts = nullptr;
     uint64_t rec_cap = 0;
@@ -343,9 +344,10 @@ static kc_status grow_records(kc_ctx* c, uint64_t need) {
 static const int kBucketBits = 16;
 
 // Engine "partition": per batch of reads
-//   P1 hist   : digit (hash >> 48) & 255 per segment of reads
+//   P1 hist   : digit (word0 >> 48) & 255 per segment of reads
 //   P2 scatter: keys to their digit's region (LDS counting sort per tile)
-//   P3        : stable radix pass on digit (hash >> 56) -> grouped by bucket = hash >> 48
+//   P3        : stable radix pass on digit (word0 >> 56) -> grouped by bucket =
+//               word0 >> 48, the key's first 8 bases: buckets are in key order
 //   P4        : bucket ranges (binary search)
 //   P5        : per-bucket LDS hash count -> (key, count) records
 static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
@@ -379,7 +381,12 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         if ((s = ensure(c, c->part_hist, hn * 8)) || (s = ensure(c, c->part_base, hn * 8)) ||
             (s = ensure(c, c->part_tmp, scan_tmp_elems(hn) * 8)))
             return s;
+        const uint64_t ng = nr * (uint64_t)groups_per_read((int)L);
+        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
+        l.codes = (const uint32_t*)c->part_codes.p;
+        l.inval = (const uint16_t*)c->part_inval.p;
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
         HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 48, c->stream));
         HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn, (uint64_t*)c->part_tmp.p,
                                   c->stream));
@@ -402,12 +409,17 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         c->st.insert_launches++;
         c->st.insert_ms += t;
 
+        if (getenv("KC_P2_SKIP")) {  // timing experiment: keys are invalid, stop after P2
+            c->batches++;
+            done += nr;
+            continue;
+        }
         if (n > 0) {
             int grid = sort_grid(n);
             if ((s = ensure(c, c->part_sort_hist, (size_t)sort_hist_elems(grid) * 8))) return s;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
             HIPCHK(c, launch_sort_pass(W, c->keys_a, c->keys_b, nullptr, nullptr, c->key_cap, n, 0, 56,
-                                       (uint64_t*)c->part_sort_hist.p, grid, true, c->stream));
+                                       (uint64_t*)c->part_sort_hist.p, grid, false, c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -649,6 +661,8 @@ void kc_destroy(kc_ctx* c) {
     if (c->rec_cnts) (void)hipFree(c->rec_cnts);
     if (c->rec_cursor) (void)hipFree(c->rec_cursor);
     release(c->part_hist);
+    release(c->part_codes);
+    release(c->part_inval);
     release(c->part_base);
     release(c->part_tmp);
     release(c->part_starts);

@@ -49,7 +49,15 @@ struct CountLaunch {
     uint64_t spill_cap;
     uint64_t* stats;          // ST_N counters
     uint32_t probe_limit;
+    const uint32_t* codes = nullptr;   // partition engine: reads encoded by kernel E
+    const uint16_t* inval = nullptr;   //   (groups_per_read(L) words per read)
 };
+
+// E: encode the launch's reads once into 2-bit codes (u32 per 16 bases, first
+// base highest) and not-ACGT masks (u16 per 16 bases); read r of the launch at
+// r * groups_per_read(L). P1 and P2 read these instead of the FASTQ text.
+int groups_per_read(int L);
+hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s);
 
 // Tile geometry of count_kmers for (L, k); also used to size dynamic LDS.
 struct CountGeom {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kc_device.h"
+#include <cstdlib>
 #include "kc_synth.h"
 
 namespace kc {
@@ -273,12 +274,17 @@ struct PartArgs {
     int shift;        // digit = (hash >> shift) & 255
     int max_win;      // windows per tile (R * windows per read)
     int scap;         // SCATTER staging capacity (keys, >= max_win)
+    int skip;         // timing experiments only (KC_P2_SKIP): 1 flush writes, 2 staging, 4 whole sink
+    const u32* codes; // CODES front end: encoded reads (kernel E), G u32 per read
+    const unsigned short* inval;  //      not-ACGT masks, G u16 per read
+    int G;            //                  16-base groups per read
 };
 
 static size_t sink_lds_host(int W, int sink, int scap) {
     if (sink == SINK_HIST) return 256 * 4;
     if (sink == SINK_SCATTER)
-        return 256 * 8 + 3 * 256 * 4 + 32 + (size_t)W * 8 * scap + (((size_t)scap + 15) & ~(size_t)15) + 2 * (size_t)scap;
+        return 256 * 8 + 3 * 256 * 4 + 16 + 32 + (size_t)W * 8 * (scap + 1) + (((size_t)scap + 1 + 15) & ~(size_t)15) +
+               2 * (size_t)scap;
     return 0;
 }
 
@@ -292,7 +298,9 @@ __device__ __forceinline__ u64 code_word(const u32* cr, int b) {
     return o ? ((hi << (2 * o)) | (u64)(cr[g + 2] >> (32 - 2 * o))) : hi;
 }
 
-template <int W, int SINK>
+constexpr int kPrefetch = 4;  // code words prefetched per thread (CODES front end)
+
+template <int W, int SINK, bool CODES>
 __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* raw = smem;
@@ -307,13 +315,13 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
     unsigned char* sk = smem + sk_off;
     u32* s_hist = (u32*)sk;                      // HIST
     u64* s_cur = (u64*)sk;                       // SCATTER: global cursor of each digit's run
-    u32* s_cnt = (u32*)(s_cur + 256);            //          staged keys per digit
-    u32* s_start = s_cnt + 256;                  //          digit start in the flush order
+    u32* s_cnt = (u32*)(s_cur + 256);            //          staged keys per digit (+ trash counter 256)
+    u32* s_start = s_cnt + 256 + 4;              //          digit start in the flush order
     u32* s_fill = s_start + 256;                 //          rank cursor
     u32* s_misc = s_fill + 256;                  //          [0] staged count, [4..7] scan scratch
-    u64* s_stage = (u64*)(s_misc + 8);           //          W x scap staged keys
-    unsigned char* s_dig = (unsigned char*)(s_stage + (size_t)W * pa.scap);  // scap digits
-    unsigned short* s_perm = (unsigned short*)(s_dig + ((pa.scap + 15) & ~15)); // scap flush order
+    u64* s_stage = (u64*)(s_misc + 8);           //          W x (scap + 1) staged keys (slot scap: trash)
+    unsigned char* s_dig = (unsigned char*)(s_stage + (size_t)W * (pa.scap + 1));  // scap + 1 digits
+    unsigned short* s_perm = (unsigned short*)(s_dig + ((pa.scap + 1 + 15) & ~15)); // scap flush order
     u32* scan_tmp = s_misc + 4;
 
     const int tid = threadIdx.x;
@@ -329,6 +337,29 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
     u64 my_valid = 0;
     bool my_hole = false;
 
+    // CODES: the next tile's code words are loaded into registers while the
+    // current tile is processed (software pipelining across tiles and units)
+    u32 pf_code[kPrefetch];
+    u32 pf_inv[kPrefetch];
+    auto prefetch = [&](u64 tile) {
+        const u64 r0 = tile * (u64)a.R;
+        const int nr = (tile < ntiles) ? (int)min((u64)a.R, a.n_reads - r0) : 0;
+#pragma unroll
+        for (int j = 0; j < kPrefetch; j++) {
+            const int it = tid + j * kBlock;
+            const int r = it / NG, g = it - r * NG;
+            u32 cw = 0, iv = 0;
+            if (r < nr && g < pa.G) {
+                const u64 idx = (r0 + (u64)r) * (u64)pa.G + (u64)g;
+                cw = __builtin_nontemporal_load(pa.codes + idx);
+                iv = __builtin_nontemporal_load(pa.inval + idx);
+            }
+            pf_code[j] = cw;
+            pf_inv[j] = iv;
+        }
+    };
+    if constexpr (CODES) prefetch(blockIdx.x * per_unit);
+
     for (u64 unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
         if constexpr (SINK == SINK_HIST) {
             s_hist[tid] = 0;
@@ -342,6 +373,36 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
             const u64 r0 = tile * (u64)a.R;
             const int nr = (int)min((u64)a.R, a.n_reads - r0);
 
+            if constexpr (CODES) {
+                // 1-2. code words of the tile (prefetched) into LDS; groups past
+                //      the read end are zero (A, valid), as the encoder leaves them
+#pragma unroll
+                for (int j = 0; j < kPrefetch; j++) {
+                    const int it = tid + j * kBlock;
+                    if (it < nr * NG) {
+                        codes[it] = pf_code[j];
+                        inval[it] = pf_inv[j];
+                    }
+                }
+                for (int it = tid + kPrefetch * kBlock; it < nr * NG; it += kBlock) {
+                    const int r = it / NG, g = it - r * NG;
+                    u32 cw = 0, iv = 0;
+                    if (g < pa.G) {
+                        const u64 idx = (r0 + (u64)r) * (u64)pa.G + (u64)g;
+                        cw = pa.codes[idx];
+                        iv = pa.inval[idx];
+                    }
+                    codes[it] = cw;
+                    inval[it] = iv;
+                }
+                if (tid < nr) rflag[tid] = 0;
+                __syncthreads();
+                // issue the next tile's loads now; they land during this tile
+                prefetch(tile + 1 < t_end ? tile + 1 : (unit + gridDim.x) * per_unit);
+                for (int it = tid; it < nr * NG; it += kBlock)
+                    if (inval[it]) atomicOr(&rflag[it / NG], 1u);
+                __syncthreads();
+            } else {
             // 1. stage the raw text of the tile's reads into LDS
             for (int it = tid; it < nr * nch; it += kBlock) {
                 int r = it / nch, c = it - r * nch;
@@ -388,6 +449,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                 if (iv) atomicOr(&rflag[r], 1u);
             }
             __syncthreads();
+            }
 
             // 3. windows -> keys -> sink. A lane takes a run of kRoll consecutive
             //    windows of one read: the first key is funnel-shifted out of the
@@ -396,109 +458,211 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
             //    tail word; past the read end it is 0, as in the reference).
             const int nchr = (nw + kRoll - 1) / kRoll;
             const int total = nr * nchr;
-            for (int c = tid; c - (tid & 63) < total; c += kBlock) {
-                // the loop bound is wave-uniform so every lane reaches the ballots
-                const bool cact = c < total;
-                int r = 0, p0 = 0;
-                u64 raw[W];
-                u64 tail = 0;
-                bool clean = true;
+            if constexpr (SINK == SINK_SCATTER) {
+                // Two phases per run of kRoll windows. A: roll the windows once
+                // to get the lane's live mask (valid, non-zero keys). One LDS
+                // reservation per wave covers all kRoll steps: step s of the
+                // wave owns [soff[s], soff[s] + popc(ballot_s)) and a lane's
+                // slot in it is its rank among the step's live lanes, so
+                // consecutive lanes write consecutive slots. B: roll again and
+                // stage. No LDS round trip inside a step.
+                for (int c = tid; c - (tid & 63) < total; c += kBlock) {
+                    const bool cact = c < total;
+                    int r = 0, p0 = 0;
+                    u64 raw[W];
+                    u64 tail = 0;
+                    bool clean = true;
 #pragma unroll
-                for (int j = 0; j < W; j++) raw[j] = 0;
-                if (cact) {
-                    r = c / nchr;
-                    p0 = (c - r * nchr) * kRoll;
-                    const u32* cr = codes + r * NG;
+                    for (int j = 0; j < W; j++) raw[j] = 0;
+                    if (cact) {
+                        r = c / nchr;
+                        p0 = (c - r * nchr) * kRoll;
+                        const u32* cr = codes + r * NG;
 #pragma unroll
-                    for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
-                    tail = code_word(cr, p0 + 32 * W);
-                    clean = rflag[r] == 0;
-                }
-#pragma unroll 1
-                for (int sstep = 0; sstep < kRoll; sstep++) {
-                    const int p = p0 + sstep;
-                    const bool active = cact && p < nw;
-                    u64 key[W];
+                        for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
+                        tail = code_word(cr, p0 + 32 * W);
+                        clean = rflag[r] == 0;
+                    }
+                    u32 livem = 0, zeros = 0, valids = 0;
+                    {
+                        u64 kr[W];
+                        u64 tl = tail;
 #pragma unroll
-                    for (int j = 0; j < W; j++) key[j] = active ? raw[j] : 0ull;
-                    key[W - 1] &= last_mask;
-                    bool valid = active;
-                    if (active && !clean) {
-                        const u32* ir = inval + r * NG;
-                        const int last = p + k - 1;
-                        for (int gg = p >> 4; gg <= (last >> 4); gg++) {
-                            int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
-                            u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
-                            if (ir[gg] & rm) valid = false;
+                        for (int j = 0; j < W; j++) kr[j] = raw[j];
+#pragma unroll
+                        for (int sstep = 0; sstep < kRoll; sstep++) {
+                            const int p = p0 + sstep;
+                            const bool active = cact && p < nw;
+                            bool valid = active;
+                            if (active && !clean) {
+                                const u32* ir = inval + r * NG;
+                                const int last = p + k - 1;
+                                for (int gg = p >> 4; gg <= (last >> 4); gg++) {
+                                    int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
+                                    u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
+                                    if (ir[gg] & rm) valid = false;
+                                }
+                            }
+                            bool is_zero = (kr[W - 1] & last_mask) == 0ull;
+#pragma unroll
+                            for (int j = 0; j < W - 1; j++) is_zero = is_zero && (kr[j] == 0ull);
+                            my_hole |= active && !valid;
+                            valids += valid ? 1u : 0u;
+                            zeros += (valid && is_zero) ? 1u : 0u;
+                            livem |= (valid && !is_zero ? 1u : 0u) << sstep;
+#pragma unroll
+                            for (int j = 0; j < W - 1; j++) kr[j] = (kr[j] << 2) | (kr[j + 1] >> 62);
+                            kr[W - 1] = (kr[W - 1] << 2) | (tl >> 62);
+                            tl <<= 2;
                         }
                     }
-                    my_hole |= active && !valid;
-                    bool is_zero = true;
+                    my_valid += valids;
+                    if (__ballot(zeros != 0u)) {
+                        wave_add(&a.stats[ST_KEY0], zeros);
+                        if (lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                    }
+                    // per-step ballots -> step offsets (scalar) -> one reservation
+                    u64 bal[kRoll];
+                    u32 soff[kRoll];
+                    u32 wtot = 0;
+#pragma unroll
+                    for (int sstep = 0; sstep < kRoll; sstep++) {
+                        bal[sstep] = __ballot((livem >> sstep) & 1u);
+                        soff[sstep] = wtot;
+                        wtot += (u32)__popcll(bal[sstep]);
+                    }
+                    if (wtot == 0 || (pa.skip & 6)) continue;
+                    u32 wbase = 0;
+                    if (lane_id() == 0) wbase = atomicAdd(&s_misc[0], wtot);
+                    wbase = __builtin_amdgcn_readfirstlane(wbase);
+                    const u64 lt = lanemask_lt();
+#pragma unroll
+                    for (int sstep = 0; sstep < kRoll; sstep++) {
+                        // branch-free: a lane without a live key writes the trash
+                        // slot scap and bumps the trash counter 256 (no exec-mask
+                        // juggling on the scalar unit)
+                        const bool lv = (livem >> sstep) & 1u;
+                        u64 key[W];
+#pragma unroll
+                        for (int j = 0; j < W; j++) key[j] = raw[j];
+                        key[W - 1] &= last_mask;
+                        const u32 idx = lv ? wbase + soff[sstep] + (u32)__popcll(bal[sstep] & lt) : (u32)pa.scap;
+                        const u32 d = (u32)(key[0] >> pa.shift) & 255u;
+#pragma unroll
+                        for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
+                        s_dig[idx] = (unsigned char)d;
+                        atomicAdd(&s_cnt[lv ? d : 256u], 1u);
+#pragma unroll
+                        for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
+                        raw[W - 1] = (raw[W - 1] << 2) | (tail >> 62);
+                        tail <<= 2;
+                    }
+                }
+            } else {
+                for (int c = tid; c - (tid & 63) < total; c += kBlock) {
+                    // the loop bound is wave-uniform so every lane reaches the ballots
+                    const bool cact = c < total;
+                    int r = 0, p0 = 0;
+                    u64 raw[W];
+                    u64 tail = 0;
+                    bool clean = true;
     #pragma unroll
-                    for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
-                    const bool live = valid && !is_zero;
-
-                    if constexpr (SINK == SINK_HIST) {
-                        if (live) atomicAdd(&s_hist[(u32)(hash_key<W>(key) >> pa.shift) & 255u], 1u);
-                    } else {
-                        // key 0^W: one atomic per wave
-                        u64 zmask = __ballot(valid && is_zero);
-                        if (zmask) {
-                            if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
-                                atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
-                                atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                    for (int j = 0; j < W; j++) raw[j] = 0;
+                    if (cact) {
+                        r = c / nchr;
+                        p0 = (c - r * nchr) * kRoll;
+                        const u32* cr = codes + r * NG;
+    #pragma unroll
+                        for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
+                        tail = code_word(cr, p0 + 32 * W);
+                        clean = rflag[r] == 0;
+                    }
+    #pragma unroll 1
+                    for (int sstep = 0; sstep < kRoll; sstep++) {
+                        const int p = p0 + sstep;
+                        const bool active = cact && p < nw;
+                        u64 key[W];
+    #pragma unroll
+                        for (int j = 0; j < W; j++) key[j] = active ? raw[j] : 0ull;
+                        key[W - 1] &= last_mask;
+                        bool valid = active;
+                        if (active && !clean) {
+                            const u32* ir = inval + r * NG;
+                            const int last = p + k - 1;
+                            for (int gg = p >> 4; gg <= (last >> 4); gg++) {
+                                int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
+                                u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
+                                if (ir[gg] & rm) valid = false;
                             }
                         }
-                        if (valid) my_valid++;
-                    }
-                    if constexpr (SINK == SINK_SCATTER) {
-                        // stage the key (wave-aggregated LDS reservation)
-                        u64 m = __ballot(live);
-                        u32 base = 0;
-                        if (m) {
-                            int leader = __ffsll((long long)m) - 1;
-                            if ((int)lane_id() == leader) base = atomicAdd(&s_misc[0], (u32)__popcll(m));
-                            base = __shfl(base, leader);
+                        my_hole |= active && !valid;
+                        bool is_zero = true;
+        #pragma unroll
+                        for (int j = 0; j < W; j++) is_zero = is_zero && (key[j] == 0ull);
+                        const bool live = valid && !is_zero;
+
+                        if constexpr (SINK == SINK_HIST) {
+                            if (live) atomicAdd(&s_hist[(u32)(key[0] >> pa.shift) & 255u], 1u);
+                        } else {
+                            // key 0^W: one atomic per wave
+                            u64 zmask = __ballot(valid && is_zero);
+                            if (zmask) {
+                                if ((int)lane_id() == __ffsll((long long)zmask) - 1) {
+                                    atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)__popcll(zmask));
+                                    atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                                }
+                            }
+                            if (valid) my_valid++;
                         }
-                        if (live) {
-                            u32 idx = base + (u32)__popcll(m & lanemask_lt());
-                            const u32 d = (u32)(hash_key<W>(key) >> pa.shift) & 255u;
-    #pragma unroll
-                            for (int j = 0; j < W; j++) s_stage[(size_t)j * pa.scap + idx] = key[j];
-                            s_dig[idx] = (unsigned char)d;
-                            atomicAdd(&s_cnt[d], 1u);
+                        if constexpr (SINK == SINK_SCATTER) {
+                            // stage the key (wave-aggregated LDS reservation)
+                            u64 m = __ballot(live);
+                            u32 base = 0;
+                            if (m) {
+                                int leader = __ffsll((long long)m) - 1;
+                                if ((int)lane_id() == leader) base = atomicAdd(&s_misc[0], (u32)__popcll(m));
+                                base = __shfl(base, leader);
+                            }
+                            if (live) {
+                                u32 idx = base + (u32)__popcll(m & lanemask_lt());
+                                const u32 d = (u32)(key[0] >> pa.shift) & 255u;
+        #pragma unroll
+                                for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
+                                s_dig[idx] = (unsigned char)d;
+                                atomicAdd(&s_cnt[d], 1u);
+                            }
                         }
-                    }
-                    if constexpr (SINK == SINK_TABLE) {
-                        bool done = true, claimed = false;
-                        if (live) {
-                            if constexpr (W == 1)
-                                done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
-                            else
-                                done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
-                        }
-                        u64 cm = __ballot(claimed);
-                        if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
-                            atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-                        // spill: wave-aggregated reservation in the spill buffer
-                        bool spill = !done;
-                        if (__ballot(spill)) {
-                            u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
-                            if (spill) {
-                                if (idx < a.spill_cap) {
-    #pragma unroll
-                                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
-                                } else {
-                                    atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                        if constexpr (SINK == SINK_TABLE) {
+                            bool done = true, claimed = false;
+                            if (live) {
+                                if constexpr (W == 1)
+                                    done = insert_w1(key[0], a.table, a.cap, a.probe_limit, &claimed);
+                                else
+                                    done = insert_wide<W>(key, a.table, a.cap, a.probe_limit, &claimed);
+                            }
+                            u64 cm = __ballot(claimed);
+                            if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
+                                atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+                            // spill: wave-aggregated reservation in the spill buffer
+                            bool spill = !done;
+                            if (__ballot(spill)) {
+                                u64 idx = wave_reserve(&a.stats[ST_SPILL_FILL], spill);
+                                if (spill) {
+                                    if (idx < a.spill_cap) {
+        #pragma unroll
+                                        for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[j];
+                                    } else {
+                                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                                    }
                                 }
                             }
                         }
+                        // roll one base in
+    #pragma unroll
+                        for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
+                        raw[W - 1] = (raw[W - 1] << 2) | (tail >> 62);
+                        tail <<= 2;
                     }
-                    // roll one base in
-#pragma unroll
-                    for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
-                    raw[W - 1] = (raw[W - 1] << 2) | (tail >> 62);
-                    tail <<= 2;
                 }
             }
             __syncthreads();
@@ -523,8 +687,9 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                         const u32 i = s_perm[q];
                         const u32 d = s_dig[i];
                         const u64 g = s_cur[d] + (q - s_start[d]);
+                        if (pa.skip & 1) continue;
 #pragma unroll
-                        for (int j = 0; j < W; j++) pa.out[(u64)j * pa.out_stride + g] = s_stage[(size_t)j * pa.scap + i];
+                        for (int j = 0; j < W; j++) pa.out[(u64)j * pa.out_stride + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
                     }
                     __syncthreads();
                     s_cur[tid] += s_cnt[tid];
@@ -566,12 +731,12 @@ static CountArgs make_args(const CountLaunch& l, const CountGeom& g) {
     return a;
 }
 
-#define KC_FRONT_SWITCH(SINKV, GRID, LDS, S, A, PA)                                                                  \
+#define KC_FRONT_SWITCH(SINKV, CODESV, GRID, LDS, S, A, PA)                                                          \
     switch (W) {                                                                                                     \
-    case 1: hipLaunchKernelGGL((count_front<1, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
-    case 2: hipLaunchKernelGGL((count_front<2, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
-    case 3: hipLaunchKernelGGL((count_front<3, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
-    case 4: hipLaunchKernelGGL((count_front<4, SINKV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;             \
+    case 1: hipLaunchKernelGGL((count_front<1, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
+    case 2: hipLaunchKernelGGL((count_front<2, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
+    case 3: hipLaunchKernelGGL((count_front<3, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
+    case 4: hipLaunchKernelGGL((count_front<4, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
     default: return hipErrorInvalidValue;                                                                            \
     }
 
@@ -585,7 +750,53 @@ hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s)
     u64 tiles = (l.n_reads + g.R - 1) / g.R;
     int grid = (int)hmin(tiles, (u64)grid_cap);
     int W = (l.k + 31) / 32;
-    KC_FRONT_SWITCH(SINK_TABLE, grid, g.lds, s, a, pa)
+    KC_FRONT_SWITCH(SINK_TABLE, false, grid, g.lds, s, a, pa)
+    return hipGetLastError();
+}
+
+int groups_per_read(int L) { return (L + 15) / 16; }
+
+// E: one thread per (read, 16-base group). Bytes past the read end encode as A
+// with a clear mask bit, exactly as the LDS encoder of the text front end.
+__global__ __launch_bounds__(kBlock) void encode_reads_k(const uint8_t* __restrict__ base,
+                                                         const u64* __restrict__ seq_off, u64 read0, u64 n_reads,
+                                                         int L, int G, u32* __restrict__ codes,
+                                                         unsigned short* __restrict__ inval) {
+    const u64 total = n_reads * (u64)G;
+    for (u64 it = (u64)blockIdx.x * kBlock + threadIdx.x; it < total; it += (u64)gridDim.x * kBlock) {
+        const u64 r = it / (u64)G;
+        const int g = (int)(it - r * (u64)G);
+        const u64 gr = read0 + r;
+        const u64 off = (seq_off ? seq_off[gr] : gr * (u64)L) + 16 * (u64)g;
+        const int nb = min(16, L - 16 * g);
+        const uintptr_t addr = (uintptr_t)(base + off);
+        const u32* dw = (const u32*)(addr & ~(uintptr_t)3);
+        const int sh = (int)(addr & 3);
+        // only dwords holding a byte of this group are read (no load past the text)
+        u32 d[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) d[i] = (4 * i < sh + nb) ? __builtin_nontemporal_load(dw + i) : 0u;
+        const u32 x0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+        const u32 x1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+        const u32 x2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+        const u32 x3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+        u32 b0, b1, b2, b3;
+        const u32 c0 = bytes_to_codes(x0, nb, &b0);
+        const u32 c1 = bytes_to_codes(x1, nb - 4, &b1);
+        const u32 c2 = bytes_to_codes(x2, nb - 8, &b2);
+        const u32 c3 = bytes_to_codes(x3, nb - 12, &b3);
+        codes[it] = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+        inval[it] = (unsigned short)((b0 << 12) | (b1 << 8) | (b2 << 4) | b3);
+    }
+}
+
+hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s) {
+    if (l.n_reads == 0) return hipSuccess;
+    const int G = groups_per_read(l.L);
+    const u64 total = l.n_reads * (u64)G;
+    const int grid = (int)hmin((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(encode_reads_k, dim3(grid), dim3(kBlock), 0, s, l.base, l.seq_off, l.read0, l.n_reads, l.L, G,
+                       codes, (unsigned short*)inval);
     return hipGetLastError();
 }
 
@@ -595,6 +806,9 @@ constexpr size_t kPartLds = 76 * 1024;
 PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     PartGeom p;
     CountGeom g = count_geometry(L, k);
+    g.raw_stride = 0;  // CODES front end: no raw text in LDS
+    g.R = 64;
+    while (g.R > 1 && g.R * g.NG > kPrefetch * kBlock) g.R--;
     // P1 and P2 share this tile geometry. P2 stages keys over several tiles
     // (scap >= 2 tiles where possible) before writing them in digit order, so
     // each digit run written is long enough to fill whole cache lines.
@@ -633,6 +847,10 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
     PartArgs zero_pa = {};
     pa = zero_pa;
     pa.hist = hist;
+    pa.codes = l.codes;
+    pa.inval = (const unsigned short*)l.inval;
+    pa.G = groups_per_read(l.L);
+    if (!l.codes || !l.inval) return hipErrorInvalidValue;
     pa.nseg = pg.nseg;
     pa.seg_tiles = pg.seg_tiles;
     pa.shift = shift;
@@ -640,7 +858,7 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
     pa.scap = pg.scap;
     size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_HIST, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
-    KC_FRONT_SWITCH(SINK_HIST, grid, lds, s, a, pa)
+    KC_FRONT_SWITCH(SINK_HIST, true, grid, lds, s, a, pa)
     return hipGetLastError();
 }
 
@@ -656,14 +874,22 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa.base = base;
     pa.out = out;
     pa.out_stride = out_stride;
+    pa.codes = l.codes;
+    pa.inval = (const unsigned short*)l.inval;
+    pa.G = groups_per_read(l.L);
+    if (!l.codes || !l.inval) return hipErrorInvalidValue;
     pa.nseg = pg.nseg;
     pa.seg_tiles = pg.seg_tiles;
     pa.shift = shift;
     pa.max_win = pg.max_win;
     pa.scap = pg.scap;
+    {
+        const char* e = getenv("KC_P2_SKIP");
+        pa.skip = e ? atoi(e) : 0;
+    }
     size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
-    KC_FRONT_SWITCH(SINK_SCATTER, grid, lds, s, a, pa)
+    KC_FRONT_SWITCH(SINK_SCATTER, true, grid, lds, s, a, pa)
     return hipGetLastError();
 }
 
@@ -1313,7 +1539,7 @@ __global__ __launch_bounds__(kBlock) void bucket_bounds_k(const u64* __restrict_
             u64 k[W];
 #pragma unroll
             for (int j = 0; j < W; j++) k[j] = keys[(u64)j * stride + mid];
-            if ((hash_key<W>(k) >> (64 - bits)) < b)
+            if ((k[0] >> (64 - bits)) < b)
                 lo = mid + 1;
             else
                 hi = mid;
@@ -1509,9 +1735,10 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     // once the pass is aborted the rest of it is skipped: a
                     // full table would make every further key probe all slots
                     if (live[u] && (last || !*(volatile u32*)labort)) {
-                        const u64 x = (hash_key<W>(key[u]) & M48) * (u64)m;
-                        if ((u32)(x >> 48) == sub) {
-                            if (!lds_insert<W>(key[u], x & M48, lkeys, lcnt, lstate, a.lcap,
+                        // sub-range by the key bits below the bucket prefix (key
+                        // order), slot by the hash
+                        if ((u32)(((key[u][0] & M48) * (u64)m) >> 48) == sub) {
+                            if (!lds_insert<W>(key[u], hash_key<W>(key[u]) & M48, lkeys, lcnt, lstate, a.lcap,
                                                last ? a.lcap : (a.lcap < 256u ? a.lcap : 256u), &lclaim)) {
                                 if (!last) {
                                     full = true;

@@ -428,3 +428,71 @@ def test_partition_subrange_passes(kca, orc, k, slots):
         st = ctx.stats()
     assert got == orc.count_fastq(fq, k)
     assert st["spilled_kmers"] == 0 and st["table_used"] == 0
+
+
+def _u64_sortable(lo32, hi32):
+    """(hi << 32 | lo) as int64 whose signed order is the unsigned order."""
+    import torch
+    v = (hi32.to(torch.int64) << 32) | (lo32.to(torch.int64) & 0xFFFFFFFF)
+    return v ^ (-(1 << 63))
+
+
+@pytest.mark.slow
+def test_config5_full_size_properties(kca):
+    """BASELINE config 5 (k=55 two-word keys, 20M x 150 bp iid reads, ~1.92e9
+    distinct): the high-cardinality path (P5 sub-range passes) at full size,
+    checked on the device: keys strictly ascending (two-word order), counts
+    sum to the valid windows, no spill, and every k-mer of sampled reads is
+    present with a count no lower than its multiplicity in the sample."""
+    import torch
+
+    n, L, k = 20_000_000, 150, 55
+    dev = torch.device("cuda", 0)
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=64 << 30) as ctx:
+        ptr, nb = ctx.synth_device(n, L, 5, 0, 0.0, 0)
+        assert ctx.count_fastq_device(ptr, nb) == n
+        ctx.free_device(ptr)
+        nrec = ctx.finish()
+        st = ctx.stats()
+        assert st["spilled_kmers"] == 0 and st["valid_kmers"] == n * (L - k + 1)
+        rec = torch.empty(nrec * 20, dtype=torch.uint8, device=dev)
+        ctx.export_records(rec)
+    words = rec.view(torch.int32).view(nrec, 5)
+    total = 0
+    prev = None
+    step = 100_000_000
+    for s0 in range(0, nrec, step):
+        w = words[s0:s0 + step]
+        a = _u64_sortable(w[:, 0], w[:, 1])
+        b = _u64_sortable(w[:, 2], w[:, 3])
+        if prev is not None:
+            a = torch.cat([prev[0], a])
+            b = torch.cat([prev[1], b])
+        asc = (a[1:] > a[:-1]) | ((a[1:] == a[:-1]) & (b[1:] > b[:-1]))
+        assert bool(asc.all())
+        total += int(w[:, 4].to(torch.int64).sum())
+        prev = (a[-1:], b[-1:])
+        del a, b, asc
+    assert total == n * (L - k + 1)
+    sample = kca.synth_fastq(1000, L, 5, first_read=n - 1000).decode()
+    cnt = kp.count_reads(kp.fastq_reads(sample), k)
+    keys = list(cnt)
+    a_all = _u64_sortable(words[:, 0], words[:, 1])
+    qa = torch.tensor([(key[0] ^ (1 << 63)) - (1 << 64) if (key[0] ^ (1 << 63)) >= (1 << 63)
+                       else (key[0] ^ (1 << 63)) for key in keys], dtype=torch.int64, device=dev)
+    idx = torch.searchsorted(a_all, qa).cpu().tolist()
+    for key, i in zip(keys, idx):
+        found = False
+        j = i
+        while j < nrec:
+            r = words[j].cpu().tolist()
+            w0 = (r[0] & 0xFFFFFFFF) | ((r[1] & 0xFFFFFFFF) << 32)
+            if w0 != key[0]:
+                break
+            w1 = (r[2] & 0xFFFFFFFF) | ((r[3] & 0xFFFFFFFF) << 32)
+            if w1 == key[1]:
+                assert (r[4] & 0xFFFFFFFF) >= cnt[key]
+                found = True
+                break
+            j += 1
+        assert found, key
