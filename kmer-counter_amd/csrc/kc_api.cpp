@@ -62,6 +62,8 @@ struct kc_ctx {
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
+    // P5 segment descriptors (see finish_part_sorted) and their sort scratch
+    DevBuf desc_key, desc_start, desc_len, desc_k2, desc_v, desc_v2, desc_lens, desc_offs;
     uint64_t* rec_keys = nullptr;  // W x rec_cap
     uint32_t* rec_cnts = nullptr;
     uint64_t rec_cap = 0;
@@ -147,10 +149,10 @@ static uint32_t probe_limit(const kc_ctx* c) {
 // Sorts n SoA records (keys at `stride`) in place-or-swap; returns which buffer
 // holds the result (0 = a, 1 = b).
 static kc_status sort_records(kc_ctx* c, uint64_t* ka, uint64_t* kb, uint32_t* va, uint32_t* vb, uint64_t stride,
-                              uint64_t n, int* which) {
+                              uint64_t n, int* which, int words = 0) {
     *which = 0;
     if (n <= 1) return KC_OK;
-    const int W = c->W;
+    const int W = words ? words : c->W;
     kc_status s = ensure(c, c->fin_misc, 2 * W * 8);
     if (s) return s;
     std::vector<uint64_t> init(2 * W);
@@ -342,6 +344,7 @@ static kc_status grow_records(kc_ctx* c, uint64_t need) {
 }
 
 static const int kBucketBits = 16;
+static const uint64_t kDescCap = 1u << 20;  // P5 segment descriptors kept for the sorted finish
 
 // Engine "partition": per batch of reads
 //   P1 hist   : digit (word0 >> 48) & 255 per segment of reads
@@ -444,6 +447,10 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             if (bound > n) bound = n;
             const uint64_t rec0 = c->rec_n;
             const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
+            const uint64_t desc0 = c->stats_h[ST_DESC_FILL];
+            if ((s = ensure(c, c->desc_key, kDescCap * 8)) || (s = ensure(c, c->desc_start, kDescCap * 8)) ||
+                (s = ensure(c, c->desc_len, kDescCap * 4)))
+                return s;
             for (;;) {
                 if ((s = grow_records(c, rec0 + bound))) return s;
                 // keys_a is free after P3: it takes P5's spills (capacity >= n)
@@ -451,7 +458,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, launch_count_buckets(W, c->keys_b, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
                                                c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
                                                c->keys_a, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
-                                               c->n_cu, c->stream));
+                                               c->n_cu, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,
+                                               (uint32_t*)c->desc_len.p, kDescCap, c->stream));
                 HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                 HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
                 if ((s = sync_stats(c))) return s;
@@ -469,7 +477,9 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 uint64_t err = c->stats_h[ST_ERR] & ~(uint64_t)ERR_REC_OVERFLOW;
                 HIPCHK(c, hipMemcpyAsync(c->stats + ST_ERR, &err, 8, hipMemcpyHostToDevice, c->stream));
                 HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec0, 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->stats + ST_DESC_FILL, &desc0, 8, hipMemcpyHostToDevice, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
+                c->stats_h[ST_DESC_FILL] = desc0;
                 c->stats_h[ST_ERR] = err;
                 c->rec_n = rec0;
             }
@@ -663,6 +673,9 @@ void kc_destroy(kc_ctx* c) {
     release(c->part_hist);
     release(c->part_codes);
     release(c->part_inval);
+    DevBuf* dbufs[] = {&c->desc_key, &c->desc_start, &c->desc_len, &c->desc_k2, &c->desc_v, &c->desc_v2,
+                       &c->desc_lens, &c->desc_offs};
+    for (DevBuf* b : dbufs) release(*b);
     release(c->part_base);
     release(c->part_tmp);
     release(c->part_starts);
@@ -760,6 +773,55 @@ kc_status kc_check_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, ui
 
 static kc_status sort_reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, bool dups, uint64_t* n_out);
 
+// Sorted finish of the partition engine (one batch, every key counted in LDS):
+// the records of each P5 pass form one key-ordered segment; the descriptors
+// (bucket << 48 | first key fraction) are sorted, their lengths scanned into
+// output offsets, and seg_sort sorts every segment into place. Key 0, the
+// smallest key, goes first. No global radix sort.
+static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) {
+    kc_status s;
+    const int W = c->W;
+    const uint64_t nrec = c->rec_n;
+    const bool key0 = c->stats_h[ST_KEY0_PRESENT] != 0;
+    const uint64_t off0 = key0 ? 1 : 0;
+    const uint64_t n = nrec + off0;
+    const uint64_t out_cap = n + 1;
+    if ((s = ensure(c, c->fin_keys[0], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[0], out_cap * 4)))
+        return s;
+    uint64_t* k0 = (uint64_t*)c->fin_keys[0].p;
+    uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
+    if (ndesc) {
+        if ((s = ensure(c, c->desc_k2, ndesc * 8)) || (s = ensure(c, c->desc_v, ndesc * 4)) ||
+            (s = ensure(c, c->desc_v2, ndesc * 4)) || (s = ensure(c, c->desc_lens, ndesc * 8)) ||
+            (s = ensure(c, c->desc_offs, ndesc * 8)) || (s = ensure(c, c->rle_tmp, scan_tmp_elems(ndesc) * 8)))
+            return s;
+        HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, ndesc, c->stream));
+        int which = 0;
+        if ((s = sort_records(c, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_k2.p, (uint32_t*)c->desc_v.p,
+                              (uint32_t*)c->desc_v2.p, ndesc, ndesc, &which, 1)))
+            return s;
+        const uint32_t* order = (const uint32_t*)(which ? c->desc_v2.p : c->desc_v.p);
+        HIPCHK(c, launch_desc_prep(order, (const uint32_t*)c->desc_len.p, ndesc, (uint64_t*)c->desc_lens.p,
+                                   c->stream));
+        HIPCHK(c, launch_scan_u64((const uint64_t*)c->desc_lens.p, (uint64_t*)c->desc_offs.p, ndesc,
+                                  (uint64_t*)c->rle_tmp.p, c->stream));
+        HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, order, (const uint64_t*)c->desc_start.p,
+                                  (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, k0 + off0,
+                                  c0 + off0, out_cap, c->stats, c->n_cu, c->stream));
+    }
+    if (key0) {
+        for (int j = 0; j < W; j++) HIPCHK(c, hipMemsetAsync(k0 + (size_t)j * out_cap, 0, 8, c->stream));
+        uint32_t kc0 = (uint32_t)c->stats_h[ST_KEY0];
+        HIPCHK(c, hipMemcpyAsync(c0, &kc0, 4, hipMemcpyHostToDevice, c->stream));
+    }
+    if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
+    HIPCHK(c, launch_pack(W, k0, out_cap, c0, n, c->fin_packed.p, c->stream));
+    if ((s = sync_stats(c))) return s;
+    if (c->stats_h[ST_ERR] & ERR_SEG_TOO_LONG) return fail(c, KC_ERR_INTERNAL, "segment longer than its LDS sort");
+    *n_out = n;
+    return KC_OK;
+}
+
 // Finish of the partition engine: LDS records + fallback-table records + key 0
 // -> radix sort -> (sum duplicates when several batches or the fallback table
 // contributed) -> pack.
@@ -768,6 +830,9 @@ static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
     const int W = c->W;
     const uint64_t nrec = c->rec_n;
     const uint64_t claimed = c->stats_h[ST_CLAIMED];
+    const uint64_t ndesc = c->stats_h[ST_DESC_FILL];
+    if (c->batches <= 1 && claimed == 0 && c->runs.empty() && ndesc <= kDescCap && !getenv("KC_NO_SEGSORT"))
+        return finish_part_sorted(c, ndesc, n_out);
     const uint64_t out_cap = nrec + claimed + 1;
     for (int i = 0; i < 2; i++) {
         if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))

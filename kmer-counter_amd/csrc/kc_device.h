@@ -19,6 +19,7 @@ enum Stat : int {
     ST_P5_PASSES = 8,    // P5 sub-range passes emitted (diagnostic)
     ST_P5_ABORTS = 9,    // P5 passes aborted on a full LDS table (diagnostic)
     ST_P5_MAXM = 10,     // largest sub-range split m used (diagnostic)
+    ST_DESC_FILL = 11,   // P5 segment descriptors written (may exceed capacity)
     ST_N = 16
 };
 
@@ -29,7 +30,8 @@ enum ErrBits : uint64_t {
     ERR_FQ_SEQ_LEN = 8,     // sequence line length != L
     ERR_FQ_TOO_MANY = 16,   // more records than the index buffer holds
     ERR_FQ_NO_FINAL_NL = 32, // block does not end with '\n'
-    ERR_REC_OVERFLOW = 64    // partition engine: record buffer too small
+    ERR_REC_OVERFLOW = 64,   // partition engine: record buffer too small
+    ERR_SEG_TOO_LONG = 128   // seg_sort: a segment longer than its LDS capacity
 };
 
 // Slot stride (uint64 words) of the open-addressed table for W key words:
@@ -98,7 +100,18 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
+                                uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
                                 hipStream_t s);
+// Finish without a global sort (see kc_kernels.hip): lens_sorted[i] = len[order[i]];
+// seg_sort writes each descriptor's records sorted at out_off[i].
+hipError_t launch_desc_prep(const uint32_t* order, const uint32_t* len, uint64_t n, uint64_t* lens_sorted,
+                            hipStream_t s);
+size_t seg_sort_lds(int W);
+hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s);
+hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, uint64_t rstride, const uint32_t* order,
+                           const uint64_t* dstart, const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc,
+                           uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, int grid,
+                           hipStream_t s);
 // segmented sum of sorted records (out_cnts zeroed by the caller)
 hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n,
                              const uint32_t* flags, const uint32_t* pos, uint64_t* out_keys, uint64_t ostride,

@@ -1614,6 +1614,10 @@ struct BucketArgs {
     u64* spill_ctr;
     u64* stats;
     u32 probe_limit;
+    u64* desc_key;    // segment descriptors: bucket << 48 | first key fraction of the pass
+    u64* desc_start;  //   first record
+    u32* desc_len;    //   records
+    u64 desc_cap;
 };
 
 // `frac` is a 48-bit uniform hash fraction; slot = frac * lcap >> 48.
@@ -1819,6 +1823,16 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                 u64 rbase = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
                 *(u64*)(misc + 16) = rbase;
                 atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                if (total) {
+                    // the pass's records are the keys of bucket b whose next
+                    // log2(m) bits equal sub: one key-ordered segment
+                    const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
+                    if (di < a.desc_cap) {
+                        a.desc_key[di] = ((u64)b << 48) | ((u64)sub << (48 - __builtin_ctz(m)));
+                        a.desc_start[di] = rbase;
+                        a.desc_len[di] = total;
+                    }
+                }
                 if (rbase + total > a.rec_cap)
                     atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
                 *lfill = 0;
@@ -1862,8 +1876,13 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
+                                uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
                                 hipStream_t s) {
     BucketArgs a;
+    a.desc_key = desc_key;
+    a.desc_start = desc_start;
+    a.desc_len = desc_len;
+    a.desc_cap = desc_cap;
     a.keys = keys;
     a.stride = stride;
     a.starts = starts;
@@ -1920,6 +1939,364 @@ hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const
     case 4: hipLaunchKernelGGL(reduce_add_k<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, flags, pos, out_keys, ostride, out_cnts); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Finish of the partition engine without a global sort. Buckets are key
+// prefixes and every P5 pass is a key sub-range of its bucket, so the records
+// of each pass (a segment, <= one LDS table) sorted in place and laid out in
+// descriptor order are the whole sorted run.
+//   desc_prep : sorted descriptor order -> lengths in that order
+//   seg_sort  : one 1024-thread block per segment: LSD radix over the bytes
+//               that vary inside the segment, stable wave-private ranking (8
+//               ballots), exchange through LDS; writes SoA records at the
+//               segment's output offset (counts gathered by original index)
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void desc_prep_k(const u32* __restrict__ order, const u32* __restrict__ len,
+                                                      u64 n, u64* __restrict__ lens_sorted) {
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock)
+        lens_sorted[i] = len[order[i]];
+}
+
+__global__ __launch_bounds__(kBlock) void iota_k(u32* out, u64 n) {
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) out[i] = (u32)i;
+}
+
+hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(iota_k, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_desc_prep(const uint32_t* order, const uint32_t* len, uint64_t n, uint64_t* lens_sorted,
+                            hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(desc_prep_k, dim3(grid_for(n)), dim3(kBlock), 0, s, order, len, n, lens_sorted);
+    return hipGetLastError();
+}
+
+constexpr int kSegBlock = 1024;
+constexpr u32 kMaxBin = 64;  // seg_sort MSD fast path: largest bin sorted by insertion
+constexpr int kSegWaves = kSegBlock / 64;
+
+template <int W>
+struct SegCfg {
+    static constexpr int CAP = (W == 1) ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));  // >= bucket_lds_slots
+    static constexpr int ITEMS = CAP / kSegBlock;
+};
+
+size_t seg_sort_lds(int W) {
+    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));
+    return (size_t)cap * (8 * W + 2) + (size_t)2 * kSegWaves * 256 * 4 + 512 * 4 + 2 * 4 * kSegWaves * 8 + 64;
+}
+
+template <int W>
+__global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ rkeys, const u32* __restrict__ rcnts,
+                                                        u64 rstride, const u32* __restrict__ order,
+                                                        const u64* __restrict__ dstart, const u32* __restrict__ dlen,
+                                                        const u64* __restrict__ out_off, u64 ndesc,
+                                                        u64* __restrict__ okeys, u32* __restrict__ ocnts,
+                                                        u64 ostride, u64* __restrict__ stats) {
+    constexpr int CAP = SegCfg<W>::CAP;
+    constexpr int ITEMS = SegCfg<W>::ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* skey = (u64*)smem;                                 // W x CAP
+    unsigned short* sidx = (unsigned short*)(skey + (size_t)W * CAP);  // CAP
+    u32* wcnt = (u32*)(sidx + CAP);                         // kSegWaves x 256
+    u32* woff = wcnt + kSegWaves * 256;                     // kSegWaves x 256
+    u32* dtot = woff + kSegWaves * 256;                     // 256 digit totals
+    u32* dst0 = dtot + 256;                                 // 256 digit starts
+    u64* red = (u64*)(dst0 + 256);                          // 2W x kSegWaves reduction scratch
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const u64 lt = lanemask_lt();
+    for (int i = tid; i < kSegWaves * 256; i += kSegBlock) wcnt[i] = 0;
+    __syncthreads();
+    for (u64 di = blockIdx.x; di < ndesc; di += gridDim.x) {
+        const u32 o = order[di];
+        const u64 st = dstart[o];
+        const u32 len = dlen[o];
+        const u64 obase = out_off[di];
+        if (len > (u32)CAP) {
+            if (tid == 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_SEG_TOO_LONG);
+            continue;
+        }
+        // blocked-by-wave, lane-striped items over R = ceil(len / 1024) rounds:
+        // position p = wave*64*R + it*64 + lane, so every wave holds a share
+        const int R = (int)((len + kSegBlock - 1) / kSegBlock);
+        u64 key[ITEMS][W];
+        unsigned short idx[ITEMS];
+        u64 orr[W], andd[W];
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            orr[j] = 0;
+            andd[j] = ~0ull;
+        }
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+            const bool ok = it < R && p < len;
+#pragma unroll
+            for (int j = 0; j < W; j++) {
+                key[it][j] = ok ? rkeys[(u64)j * rstride + st + p] : ~0ull;
+                if (ok) {
+                    orr[j] |= key[it][j];
+                    andd[j] &= key[it][j];
+                }
+            }
+            idx[it] = (unsigned short)p;
+        }
+        // bytes that vary inside the segment
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            for (int o2 = 32; o2 >= 1; o2 >>= 1) {
+                orr[j] |= __shfl_xor(orr[j], o2);
+                andd[j] &= __shfl_xor(andd[j], o2);
+            }
+            if (lane == 0) {
+                red[j * kSegWaves + wave] = orr[j];
+                red[(W + j) * kSegWaves + wave] = andd[j];
+            }
+        }
+        __syncthreads();
+        u64 diff[W];
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            u64 oo = 0, aa = ~0ull;
+            for (int w = 0; w < kSegWaves; w++) {
+                oo |= red[j * kSegWaves + w];
+                aa &= red[(W + j) * kSegWaves + w];
+            }
+            diff[j] = oo ^ aa;
+        }
+        __syncthreads();
+        // MSD fast path: one LDS counting pass on the 12 most significant
+        // varying bits (keys are distinct, so an unstable rank is fine), then
+        // every thread insertion-sorts its 4 bins. Bins larger than kMaxBin
+        // (skewed keys) fall back to the LSD passes below.
+        int hw = -1, hb = 0;
+#pragma unroll
+        for (int j = W - 1; j >= 0; j--)
+            if (diff[j]) {
+                hw = j;
+                hb = 63 - __builtin_clzll(diff[j]);
+            }
+        bool fast = hw >= 0;
+        if (fast) {
+            const int lo = hb >= 11 ? hb - 11 : 0;
+            u32* bcnt = wcnt;  // 4096 bins (wcnt/woff area)
+            for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
+            if (tid == 0) dtot[0] = 0;
+            __syncthreads();
+            u32 dig[ITEMS], rank[ITEMS];
+#pragma unroll
+            for (int it = 0; it < ITEMS; it++) {
+                if (it >= R) break;
+                const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+                u64 kw = key[it][0];
+#pragma unroll
+                for (int jj = 1; jj < W; jj++)
+                    if (jj == hw) kw = key[it][jj];
+                dig[it] = (u32)(kw >> lo) & 4095u;
+                if (p < len) rank[it] = atomicAdd(&bcnt[dig[it]], 1u);
+            }
+            __syncthreads();
+            // bin starts: 4 bins per thread, block-wide exclusive scan
+            const u32 c0 = bcnt[4 * tid], c1 = bcnt[4 * tid + 1], c2 = bcnt[4 * tid + 2], c3 = bcnt[4 * tid + 3];
+            const u32 mx = max(max(c0, c1), max(c2, c3));
+            const u32 sum = c0 + c1 + c2 + c3;
+            u32 inc = sum;
+#pragma unroll
+            for (int o2 = 1; o2 < 64; o2 <<= 1) {
+                const u32 y = __shfl_up(inc, o2);
+                if (lane >= o2) inc += y;
+            }
+            if (lane == 63) dst0[wave] = inc;
+            if (mx > kMaxBin) atomicOr(&dtot[0], 1u);
+            __syncthreads();
+            u32 wpre = 0;
+            for (int w = 0; w < wave; w++) wpre += dst0[w];
+            const u32 ex = wpre + inc - sum;
+            bcnt[4 * tid] = ex;
+            bcnt[4 * tid + 1] = ex + c0;
+            bcnt[4 * tid + 2] = ex + c0 + c1;
+            bcnt[4 * tid + 3] = ex + c0 + c1 + c2;
+            fast = dtot[0] == 0;
+            __syncthreads();
+            if (fast) {
+#pragma unroll
+                for (int it = 0; it < ITEMS; it++) {
+                    if (it >= R) break;
+                    const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+                    if (p < len) {
+                        const u32 q = bcnt[dig[it]] + rank[it];
+#pragma unroll
+                        for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + q] = key[it][jj];
+                        sidx[q] = idx[it];
+                    }
+                }
+                __syncthreads();
+                // insertion sort of this thread's 4 bins [4t, 4t+4)
+                const u32 bs = bcnt[4 * tid];
+                const u32 be = bs + sum;
+                const u32 b1 = bs + c0, b2 = b1 + c1, b3 = b2 + c2;
+                for (int q = 0; q < 4; q++) {
+                    const u32 s0 = q == 0 ? bs : (q == 1 ? b1 : (q == 2 ? b2 : b3));
+                    const u32 e0 = q == 0 ? b1 : (q == 1 ? b2 : (q == 2 ? b3 : be));
+                    for (u32 x = s0 + 1; x < e0; x++) {
+                        u64 kx[W];
+#pragma unroll
+                        for (int jj = 0; jj < W; jj++) kx[jj] = skey[(size_t)jj * CAP + x];
+                        const unsigned short ix = sidx[x];
+                        u32 y = x;
+                        while (y > s0) {
+                            bool less = false, eq = true;
+#pragma unroll
+                            for (int jj = 0; jj < W; jj++) {
+                                const u64 ky = skey[(size_t)jj * CAP + y - 1];
+                                if (eq && kx[jj] != ky) {
+                                    less = kx[jj] < ky;
+                                    eq = false;
+                                }
+                            }
+                            if (!less) break;
+#pragma unroll
+                            for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = skey[(size_t)jj * CAP + y - 1];
+                            sidx[y] = sidx[y - 1];
+                            y--;
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = kx[jj];
+                        sidx[y] = ix;
+                    }
+                }
+                __syncthreads();
+                for (u32 p = tid; p < len; p += kSegBlock) {
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) okeys[(u64)jj * ostride + obase + p] = skey[(size_t)jj * CAP + p];
+                    ocnts[obase + p] = rcnts[st + sidx[p]];
+                }
+                // bins were counted in wcnt: the LSD path expects it zeroed
+                for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
+                __syncthreads();
+                continue;
+            }
+            for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
+            __syncthreads();
+        }
+        for (int j = W - 1; j >= 0; j--) {
+            u64 dj = 0;
+#pragma unroll
+            for (int jj = 0; jj < W; jj++)
+                if (jj == j) dj = diff[jj];
+            for (int sh = 0; sh < 64; sh += 8) {
+                if (((dj >> sh) & 0xffull) == 0) continue;  // block-uniform
+                u32 dig[ITEMS], rank[ITEMS];
+#pragma unroll
+                for (int it = 0; it < ITEMS; it++) {
+                    if (it >= R) break;  // block-uniform
+                    const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+                    const bool ok = p < len;
+                    u64 kw = key[it][0];
+#pragma unroll
+                    for (int jj = 1; jj < W; jj++)
+                        if (jj == j) kw = key[it][jj];
+                    const u32 d = (u32)(kw >> sh) & 255u;
+                    dig[it] = d;
+                    u64 peers = __ballot(ok);
+#pragma unroll
+                    for (int bb = 0; bb < 8; bb++) {
+                        const u64 m = __ballot((d >> bb) & 1u);
+                        peers &= ((d >> bb) & 1u) ? m : ~m;
+                    }
+                    const u32 before = (u32)__popcll(peers & lt);
+                    const u32 base = ok ? wcnt[wave * 256 + d] : 0u;
+                    if (ok && before == 0) wcnt[wave * 256 + d] = base + (u32)__popcll(peers);
+                    rank[it] = base + before;
+                }
+                __syncthreads();
+                if (tid < 256) {
+                    u32 run = 0;
+                    for (int w = 0; w < kSegWaves; w++) {
+                        const u32 cc = wcnt[w * 256 + tid];
+                        woff[w * 256 + tid] = run;
+                        wcnt[w * 256 + tid] = 0;
+                        run += cc;
+                    }
+                    dtot[tid] = run;
+                }
+                __syncthreads();
+                if (wave == 0) {
+                    // exclusive scan of the 256 digit totals: 4 per lane, no barrier
+                    const u32 v0 = dtot[4 * lane], v1 = dtot[4 * lane + 1], v2 = dtot[4 * lane + 2],
+                              v3 = dtot[4 * lane + 3];
+                    const u32 sum = v0 + v1 + v2 + v3;
+                    u32 inc = sum;
+#pragma unroll
+                    for (int o2 = 1; o2 < 64; o2 <<= 1) {
+                        const u32 y = __shfl_up(inc, o2);
+                        if (lane >= o2) inc += y;
+                    }
+                    const u32 ex = inc - sum;
+                    dst0[4 * lane] = ex;
+                    dst0[4 * lane + 1] = ex + v0;
+                    dst0[4 * lane + 2] = ex + v0 + v1;
+                    dst0[4 * lane + 3] = ex + v0 + v1 + v2;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int it = 0; it < ITEMS; it++) {
+                    const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+                    if (it < R && p < len) {
+                        const u32 q = dst0[dig[it]] + woff[wave * 256 + dig[it]] + rank[it];
+#pragma unroll
+                        for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + q] = key[it][jj];
+                        sidx[q] = idx[it];
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int it = 0; it < ITEMS; it++) {
+                    const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+                    if (it < R && p < len) {
+#pragma unroll
+                        for (int jj = 0; jj < W; jj++) key[it][jj] = skey[(size_t)jj * CAP + p];
+                        idx[it] = sidx[p];
+                    }
+                }
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < ITEMS; it++) {
+            const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
+            if (it < R && p < len) {
+#pragma unroll
+                for (int jj = 0; jj < W; jj++) okeys[(u64)jj * ostride + obase + p] = key[it][jj];
+                ocnts[obase + p] = rcnts[st + idx[it]];
+            }
+        }
+    }
+}
+
+hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, uint64_t rstride, const uint32_t* order,
+                           const uint64_t* dstart, const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc,
+                           uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, int grid,
+                           hipStream_t s) {
+    if (ndesc == 0) return hipSuccess;
+    size_t lds = (seg_sort_lds(W) + 15) & ~(size_t)15;
+#define KC_SEG(WW)                                                                                                 \
+    hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds, s, rkeys, rcnts, rstride, order, dstart, \
+                       dlen, out_off, ndesc, okeys, ocnts, ostride, stats)
+    switch (W) {
+    case 1: KC_SEG(1); break;
+    case 2: KC_SEG(2); break;
+    case 3: KC_SEG(3); break;
+    case 4: KC_SEG(4); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef KC_SEG
     return hipGetLastError();
 }
 
