@@ -41,12 +41,13 @@ def load_pkg():
     return mod
 
 
-def cpu_baseline(kca, reads, L, k, genome, seed, first):
+def cpu_baseline(kca, reads, L, k, genome, seed, first, threads=None):
     """The CPU port of the reference pipeline (oracle refcpu) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: timed as the CPU baseline only
 
-    threads = min(16, os.cpu_count() or 1)
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
     fq = kca.synth_fastq(reads, L, seed, genome_length=genome, first_read=first)
     t0 = time.perf_counter()
     distinct, windows = oracle.refcpu_count_only(fq, k, gpu_memory_limit=100000000, threads=threads)
@@ -191,30 +192,63 @@ def main():
     total_kmers = windows_per_gpu * world * args.steps
     value = total_kmers / elapsed
 
-    # roofline of the dominant kernel (count_kmers): algorithmic bytes per k-mer
-    # = FASTQ bytes per k-mer (read once) + 8W key bytes + 8 count bytes (read +
-    # write of the u32); per launch = that x the launch's k-mers.
+    # Rooflines. Each main kernel of the partition engine is priced by its own
+    # algorithmic HBM bytes: P2 reads the encoded reads
+    # (6 B per 16 bases) and writes 8W B per key; the P3 scatter reads and
+    # writes 8W B per key; P5 reads 8W B per key and writes 8W+4 B per
+    # distinct record. `roofline` is the one with the longest launch; each
+    # achieved = algorithmic bytes per launch / its HIP-event launch time on
+    # the ctx stream. `path_achieved` is SURVEY §8d's whole-path figure:
+    # k-mers/s per GPU x (FASTQ bytes per k-mer + 8W + 8).
     W = (k + 31) // 32
-    b_per_kmer = nbytes / windows_per_gpu + 8 * W + 8
-    avg_launch_ms = insert_ms / max(1, launches)
-    kmers_per_launch = windows_per_gpu * args.steps / max(1, launches)
-    achieved = b_per_kmer * kmers_per_launch / (avg_launch_ms / 1e3) / 1e9
+    G = (L + 15) // 16
+    steps = args.steps
+    windows_step = windows_per_gpu
+    keys_step = st["keys"] or windows_step  # ctx stats are per step (reset at each step)
+    recs_step = st["output_records"]
+    kernels = {}
+    if args.engine == "partition":
+        p5_per_step = max(1, st["p5_launches"])
+        specs = [
+            ("P2", f"count_front<{W},SINK_SCATTER,CODES>", part_ms[1], launches, windows_step,
+             "k-mers", (G * 6) / max(1, L - k + 1) + 8 * W),
+            ("P3", f"p3_scatter_k<{W}>", part_ms[2], steps * st["batches"], keys_step, "keys", 16 * W),
+            ("P5", f"count_buckets<{W}>", part_ms[4], steps * p5_per_step, keys_step, "keys",
+             8 * W + (8 * W + 4) * recs_step / max(1, keys_step)),
+        ]
+    else:
+        specs = [("insert", f"count_front<{W},SINK_TABLE>", insert_ms, launches, windows_step, "k-mers",
+                  nbytes / windows_per_gpu + 8 * W + 8)]
+    for tag, name, ms_total, nl, units_step, unit_name, bpu in specs:
+        nl = max(1, nl)
+        avg = ms_total / nl
+        units = units_step * steps / nl
+        ach = bpu * units / (avg / 1e3) / 1e9 if avg > 0 else 0.0
+        kernels[tag] = {"kernel": name, "avg_launch_ms": round(avg, 3), "units_per_launch": int(units),
+                        "unit": unit_name, "algorithmic_bytes_per_unit": round(bpu, 3),
+                        "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 4)}
+    dom = max(kernels, key=lambda t: kernels[t]["avg_launch_ms"])
+    d = kernels[dom]
     traffic = load_traffic()
-    kernel = f"count_front<{W},SINK_SCATTER> (P2)" if args.engine == "partition" else f"count_front<{W},SINK_TABLE>"
-    step_s = elapsed / args.steps
-    path_achieved = b_per_kmer * windows_per_gpu / step_s / 1e9
     t_bytes = None
-    if traffic and traffic.get("kernel") == kernel and traffic.get("reads_per_gpu") == args.reads:
-        t_bytes = traffic.get("bytes_per_launch")
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": t_bytes,
-                "kernel": kernel, "avg_launch_ms": round(avg_launch_ms, 3),
-                "algorithmic_bytes_per_kmer": round(b_per_kmer, 3), "kmers_per_launch": int(kmers_per_launch),
-                "path_achieved": round(path_achieved, 2), "path_frac": round(path_achieved / HBM_PEAK_GBS, 4)}
+    if traffic and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
+        t_bytes = traffic.get("kernels", {}).get(dom, {}).get("bytes_per_launch")
+    b_path = nbytes / windows_per_gpu + 8 * W + 8
+    step_s = elapsed / args.steps
+    path_achieved = b_path * windows_per_gpu / step_s / 1e9
+    roofline = {"bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d["frac"], "traffic": t_bytes, "kernel": f"{dom}: {d['kernel']}",
+                "avg_launch_ms": d["avg_launch_ms"], "units_per_launch": d["units_per_launch"],
+                "unit_of_work": d["unit"], "algorithmic_bytes_per_unit": d["algorithmic_bytes_per_unit"],
+                "path_achieved": round(path_achieved, 2), "path_frac": round(path_achieved / HBM_PEAK_GBS, 4),
+                "path_bytes_per_kmer": round(b_path, 3), "kernels": kernels}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(kca, args.cpu_reads, L, k, args.genome, args.seed, 0)
+        t1 = cpu_baseline(kca, max(1, args.cpu_reads // 10), L, k, args.genome, args.seed, 0, threads=1)
+        cpu["value_t1"] = t1["value"]
+        cpu["sample_t1"] = t1["sample"]
 
     src = (f"sampled from a {args.genome} bp random genome" if args.genome else "of iid uniform bases")
     base = (f"k={k}, {args.reads} x {L} bp reads per GPU {src} (seed {args.seed}), FASTQ in HBM, "
@@ -237,7 +271,7 @@ def main():
                        "parallelism": parallelism, "gpu_memory_limit": args.mem},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "breakdown_ms_per_step": {"insert": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
+            "breakdown_ms_per_step": {"p2_scatter": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
                                       "finish": finish_ms / args.steps,
                                       "exchange_rank0": xch_ms[0] / args.steps,
                                       "partition_passes": [round(x / args.steps, 3) for x in part_ms]},

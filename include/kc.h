@@ -113,9 +113,15 @@ typedef struct kc_stats {
     double decode_ms;          /* FASTQ index + validate kernels */
     double finish_ms;          /* compact + sort + pack */
     double last_count_ms;      /* device time of the last kc_count_* call */
-    double part_ms[5];         /* partition engine: hist, scatter, radix pass,
-                                  bucket bounds, LDS bucket count (summed) */
+    double part_ms[5];         /* partition engine (summed device time): [0] encode
+                                  (E) + P1 digit histogram, [1] P2 scatter,
+                                  [2] P3 regional scatter kernel, [3] P3 tile
+                                  histograms + scan + P4 bucket bounds, [4] P5
+                                  LDS bucket count */
     uint64_t batches;          /* partition engine batches */
+    uint64_t keys;             /* partition engine: keys partitioned (valid,
+                                  non-zero windows) since the last reset */
+    uint64_t p5_launches;      /* P5 launches (reruns on record overflow included) */
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". */

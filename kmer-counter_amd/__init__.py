@@ -71,6 +71,8 @@ class Stats(ctypes.Structure):
         ("last_count_ms", ctypes.c_double),
         ("part_ms", ctypes.c_double * 5),
         ("batches", ctypes.c_uint64),
+        ("keys", ctypes.c_uint64),
+        ("p5_launches", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -71,7 +71,9 @@ struct kc_ctx {
     uint64_t rec_n = 0;              // host copy after each batch
     uint64_t batches = 0;
     int n_cu = 256;
-    double part_ms[5] = {0, 0, 0, 0, 0};  // P1, P2, P3, P4, P5
+    double part_ms[5] = {0, 0, 0, 0, 0};  // E+P1, P2, P3 scatter, P3 hist + P4, P5
+    uint64_t part_keys = 0;               // keys partitioned since the last reset
+    uint64_t p5_launches = 0;
 
     // scratch (grown on demand)
     DevBuf in_stage;        // host-pointer inputs
@@ -349,7 +351,7 @@ static const uint64_t kDescCap = 1u << 20;  // P5 segment descriptors kept for t
 // Engine "partition": per batch of reads
 //   P1 hist   : digit (word0 >> 48) & 255 per segment of reads
 //   P2 scatter: keys to their digit's region (LDS counting sort per tile)
-//   P3        : stable radix pass on digit (word0 >> 56) -> grouped by bucket =
+//   P3        : regional scatter on digit (word0 >> 56) -> grouped by bucket =
 //               word0 >> 48, the key's first 8 bases: buckets are in key order
 //   P4        : bucket ranges (binary search)
 //   P5        : per-bucket LDS hash count -> (key, count) records
@@ -418,15 +420,36 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             continue;
         }
         if (n > 0) {
-            int grid = sort_grid(n);
-            if ((s = ensure(c, c->part_sort_hist, (size_t)sort_hist_elems(grid) * 8))) return s;
+            // P3 tiles: regions (P2 digits) cut into tiles of their own
+            std::vector<uint64_t> rt(2 * 257);
+            HIPCHK(c, hipMemcpy2DAsync(rt.data(), 8, c->part_base.p, pg.nseg * 8, 8, 256, hipMemcpyDeviceToHost,
+                                       c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            rt[256] = n;
+            const uint64_t tile = (uint64_t)p3_tile(W);
+            rt[257] = 0;
+            for (int r = 0; r < 256; r++) rt[257 + r + 1] = rt[257 + r] + (rt[r + 1] - rt[r] + tile - 1) / tile;
+            const uint64_t ntiles = rt[257 + 256];
+            if ((s = ensure(c, c->part_sort_hist, (256 * ntiles + scan_tmp_elems(256 * ntiles) + 2 * 257) * 8)))
+                return s;
+            uint64_t* p3h = (uint64_t*)c->part_sort_hist.p;
+            uint64_t* p3t = p3h + 256 * ntiles + scan_tmp_elems(256 * ntiles);
+            HIPCHK(c, hipMemcpyAsync(p3t, rt.data(), 2 * 257 * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_sort_pass(W, c->keys_a, c->keys_b, nullptr, nullptr, c->key_cap, n, 0, 56,
-                                       (uint64_t*)c->part_sort_hist.p, grid, false, c->stream));
+            HIPCHK(c, launch_p3_hist(W, c->keys_a, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
+                                     c->stream));
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipEventSynchronize(c->ev1));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[3] += t;
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            HIPCHK(c, launch_p3_scatter(W, c->keys_a, c->keys_b, c->key_cap, p3t, p3t + 257, ntiles, p3h, 2 * c->n_cu,
+                                        c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
             c->part_ms[2] += t;
+            c->part_keys += n;
 
             uint32_t nb = 1u << kBucketBits;
             if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8))) return s;
@@ -465,6 +488,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 if ((s = sync_stats(c))) return s;
                 HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
                 c->part_ms[4] += t;
+                c->p5_launches++;
                 if (getenv("KC_DEBUG"))
                     fprintf(stderr, "kc: P5 n=%llu passes=%llu aborts=%llu max_m=%llu records=%llu %.3f ms\n",
                             (unsigned long long)n, (unsigned long long)c->stats_h[ST_P5_PASSES],
@@ -699,6 +723,8 @@ kc_status kc_reset(kc_ctx* c) {
     c->rec_n = 0;
     c->batches = 0;
     for (double& x : c->part_ms) x = 0;
+    c->part_keys = 0;
+    c->p5_launches = 0;
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
@@ -1080,6 +1106,8 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     *out = c->st;
     for (int i = 0; i < 5; i++) out->part_ms[i] = c->part_ms[i];
     out->batches = c->batches;
+    out->keys = c->part_keys;
+    out->p5_launches = c->p5_launches;
     out->table_capacity = c->cap;
     out->valid_kmers = c->stats_h[ST_VALID];
     out->spill_runs = c->runs.size();

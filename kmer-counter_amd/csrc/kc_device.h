@@ -89,6 +89,14 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
 // also counts key 0 / holes / valid windows into l.stats
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
                                uint64_t out_stride, int shift, hipStream_t s);
+// P3 (regional scatter, see kc_kernels.hip): rstart[257] region bounds,
+// tpre[257] tile prefix per region (tiles of p3_tile(W) keys); hist holds
+// 256 * ntiles u64, tmp scan_tmp_elems(256 * ntiles) u64.
+int p3_tile(int W);
+hipError_t launch_p3_hist(int W, const uint64_t* kin, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
+                          uint64_t* hist, uint64_t* tmp, int grid, hipStream_t s);
+hipError_t launch_p3_scatter(int W, const uint64_t* kin, uint64_t* kout, uint64_t stride, const uint64_t* rstart,
+                             const uint64_t* tpre, uint64_t ntiles, const uint64_t* hist, int grid, hipStream_t s);
 // P4: starts[b] for b in [0, 2^bits]: first key index of bucket b (= hash >> (64 - bits))
 hipError_t launch_bucket_bounds(int W, const uint64_t* keys, uint64_t stride, uint64_t n, int bits, uint64_t* starts,
                                 hipStream_t s);

@@ -1563,6 +1563,7 @@ hipError_t launch_bucket_bounds(int W, const uint64_t* keys, uint64_t stride, ui
 }
 
 constexpr int kBucketBlock = 1024;
+constexpr int kBucketWaves = kBucketBlock / 64;
 
 // Exclusive scan across a workgroup of NT threads (NT/64 waves); lds holds
 // NT/64 u32. Returns this thread's exclusive prefix; *total = block sum.
@@ -1618,7 +1619,19 @@ struct BucketArgs {
     u64* desc_start;  //   first record
     u32* desc_len;    //   records
     u64 desc_cap;
+    int skip;         // timing experiments only (KC_P5_SKIP): 1 = no LDS inserts
 };
+
+// 48-bit slot fraction of a key for the P5 LDS table: multiply-shift (the
+// high bits of key * odd constant depend on every key bit); the keys of one
+// bucket share their top 16 bits, which the multiply spreads as well.
+template <int W>
+__device__ __forceinline__ u64 slot_frac(const u64 (&key)[W]) {
+    u64 h = key[0] * 0x9e3779b97f4a7c15ull;
+#pragma unroll
+    for (int j = 1; j < W; j++) h = (h ^ (h >> 29)) + key[j] * 0xc2b2ae3d27d4eb4full;
+    return h >> 16;
+}
 
 // `frac` is a 48-bit uniform hash fraction; slot = frac * lcap >> 48.
 // *claimed is set when this key took an empty slot.
@@ -1627,8 +1640,48 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
                                            u32 lcap, u32 max_probe, bool* claimed) {
     u32 slot = (u32)((frac * (u64)lcap) >> 48);
     if constexpr (W == 1) {
+        if ((lcap & 3u) == 0) {
+            // groups of 4 slots: the home group is read with two 16-byte LDS
+            // loads and a repeat (the common case) resolves with branch-free
+            // compares and one add; probing continues group by group
+            const u32 ng = lcap >> 2;
+            u32 g = (u32)((frac * (u64)ng) >> 48);
+            for (u32 pr = 0; pr < max_probe; pr += 4) {
+                typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+                const volatile v2u64* gp = (const volatile v2u64*)(lkeys + 4 * g);
+                const v2u64 a0 = gp[0], a1 = gp[1];
+                const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
+                int hit = -1, emp = -1;
+#pragma unroll
+                for (int i = 3; i >= 0; i--) {
+                    if (v[i] == key[0]) hit = i;
+                    if (v[i] == 0ull) emp = i;
+                }
+                if (hit >= 0 && (emp < 0 || hit < emp)) {
+                    atomicAdd(&lcnt[4 * g + hit], 1u);
+                    return true;
+                }
+                if (emp >= 0) {
+                    // claim the first empty slot; a lost race re-reads the group
+                    const u64 old =
+                        atomicCAS((unsigned long long*)&lkeys[4 * g + emp], 0ull, (unsigned long long)key[0]);
+                    if (old == 0ull || old == key[0]) {
+                        atomicAdd(&lcnt[4 * g + emp], 1u);
+                        *claimed = old == 0ull;
+                        return true;
+                    }
+                    pr -= 4;  // same group again
+                    continue;
+                }
+                if (++g == ng) g = 0;
+            }
+            return false;
+        }
         for (u32 pr = 0; pr < max_probe; ++pr) {
-            u64 old = atomicCAS((unsigned long long*)&lkeys[slot], 0ull, (unsigned long long)key[0]);
+            // read first: a repeat (the common case) costs a read and one add;
+            // only an EMPTY reading is confirmed by the CAS
+            u64 old = __hip_atomic_load(&lkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old == 0ull) old = atomicCAS((unsigned long long*)&lkeys[slot], 0ull, (unsigned long long)key[0]);
             if (old == 0ull || old == key[0]) {
                 atomicAdd(&lcnt[slot], 1u);
                 *claimed = old == 0ull;
@@ -1690,6 +1743,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
     u32* lfill = misc + 20;
     u32* labort = misc + 21;
     u32* lnext = misc + 22;
+    u32* wtot_l = misc + 24;  // kBucketWaves per-wave record counts
     const int tid = threadIdx.x;
     for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
@@ -1721,6 +1775,15 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             const bool last = m >= mmax;
             u64 scanned = 0;
             constexpr int U = 4;  // independent key loads in flight per thread
+            // software pipeline: the next iteration's keys are loaded before
+            // this iteration's inserts, so HBM latency overlaps LDS work
+            u64 nkey[U][W];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const u64 i = lo + (u64)u * kBucketBlock + tid;
+#pragma unroll
+                for (int j = 0; j < W; j++) nkey[u][j] = i < hi ? a.keys[(u64)j * a.stride + i] : 0ull;
+            }
             for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
                 if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 scanned += (u64)U * kBucketBlock;
@@ -1731,19 +1794,25 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     const u64 i = base + (u64)u * kBucketBlock + tid;
                     live[u] = i < hi;
 #pragma unroll
-                    for (int j = 0; j < W; j++) key[u][j] = live[u] ? a.keys[(u64)j * a.stride + i] : 0ull;
+                    for (int j = 0; j < W; j++) key[u][j] = nkey[u][j];
+                }
+                const u64 nbase = base + (u64)U * kBucketBlock;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const u64 i = nbase + (u64)u * kBucketBlock + tid;
+#pragma unroll
+                    for (int j = 0; j < W; j++) nkey[u][j] = i < hi ? a.keys[(u64)j * a.stride + i] : 0ull;
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     bool done = true, claimed = false, lclaim = false, full = false;
-                    // once the pass is aborted the rest of it is skipped: a
-                    // full table would make every further key probe all slots
-                    if (live[u] && (last || !*(volatile u32*)labort)) {
+                    if (live[u]) {
                         // sub-range by the key bits below the bucket prefix (key
-                        // order), slot by the hash
-                        if ((u32)(((key[u][0] & M48) * (u64)m) >> 48) == sub) {
-                            if (!lds_insert<W>(key[u], hash_key<W>(key[u]) & M48, lkeys, lcnt, lstate, a.lcap,
-                                               last ? a.lcap : (a.lcap < 256u ? a.lcap : 256u), &lclaim)) {
+                        // order), slot by a multiply-shift hash; outside the
+                        // last resort a long probe means "table full" (abort)
+                        if ((u32)(((key[u][0] & M48) * (u64)m) >> 48) == sub && !a.skip) {
+                            if (!lds_insert<W>(key[u], slot_frac<W>(key[u]), lkeys, lcnt, lstate, a.lcap,
+                                               last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u), &lclaim)) {
                                 if (!last) {
                                     full = true;
                                 } else if constexpr (W == 1) {
@@ -1809,57 +1878,70 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                 __syncthreads();
                 continue;
             }
-            // emit the occupied slots in slot order: count, one reservation,
-            // then rounds of 1024 consecutive slots with a block scan, so
-            // consecutive lanes write consecutive records
-            u32 mine = 0;
-            for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
-                bool occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
-                mine += occ ? 1u : 0u;
-            }
-            u32 total;
-            (void)block_excl_scan_n<kBucketBlock>(mine, misc, &total);
-            if (tid == 0) {
-                u64 rbase = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
-                *(u64*)(misc + 16) = rbase;
-                atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
-                if (total) {
-                    // the pass's records are the keys of bucket b whose next
-                    // log2(m) bits equal sub: one key-ordered segment
-                    const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
-                    if (di < a.desc_cap) {
-                        a.desc_key[di] = ((u64)b << 48) | ((u64)sub << (48 - __builtin_ctz(m)));
-                        a.desc_start[di] = rbase;
-                        a.desc_len[di] = total;
+            // emit the occupied slots: wave w owns slots [w*spw, (w+1)*spw);
+            // it counts them with ballots, one 16-entry prefix gives its
+            // output offset, and it writes its records in slot order (no
+            // block-wide scans, two barriers per pass)
+            {
+                const int wave = tid >> 6, lane = (int)lane_id();
+                const u32 spw = (a.lcap + kBucketWaves - 1) / kBucketWaves;
+                const u32 s0 = (u32)wave * spw;
+                const u32 s1 = min(a.lcap, s0 + spw);
+                u32 wc = 0;
+                for (u32 c0 = s0; c0 < s1; c0 += 64) {
+                    const u32 i = c0 + (u32)lane;
+                    const bool occ = i < s1 && ((W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u));
+                    wc += (u32)__popcll(__ballot(occ));
+                }
+                if (lane == 0) wtot_l[wave] = wc;
+                __syncthreads();
+                u32 total = 0, before = 0;
+                for (int w = 0; w < kBucketWaves; w++) {
+                    const u32 v = wtot_l[w];
+                    before += w < wave ? v : 0u;
+                    total += v;
+                }
+                if (tid == 0) {
+                    u64 rbase = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
+                    *(u64*)(misc + 16) = rbase;
+                    if (rbase + total > a.rec_cap)
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                    *lfill = 0;
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                    if (total) {
+                        // the pass's records are the keys of bucket b whose next
+                        // log2(m) bits equal sub: one key-ordered segment
+                        const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
+                        if (di < a.desc_cap) {
+                            a.desc_key[di] = ((u64)b << 48) | ((u64)sub << (48 - __builtin_ctz(m)));
+                            a.desc_start[di] = rbase;
+                            a.desc_len[di] = total;
+                        }
                     }
                 }
-                if (rbase + total > a.rec_cap)
-                    atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
-                *lfill = 0;
-            }
-            __syncthreads();
-            u64 pos = *(u64*)(misc + 16);
-            for (u32 r0 = 0; r0 < a.lcap; r0 += kBucketBlock) {
-                const u32 i = r0 + tid;
-                bool occ = false;
-                if (i < a.lcap) occ = (W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u);
-                u32 rt;
-                u32 before = block_excl_scan_n<kBucketBlock>(occ ? 1u : 0u, misc, &rt);
-                if (occ) {
-                    u64 q = pos + before;
-                    if (q < a.rec_cap) {
+                __syncthreads();
+                u64 pos = *(u64*)(misc + 16) + before;
+                const u64 lt = lanemask_lt();
+                for (u32 c0 = s0; c0 < s1; c0 += 64) {
+                    const u32 i = c0 + (u32)lane;
+                    const bool occ = i < s1 && ((W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u));
+                    const u64 bm = __ballot(occ);
+                    if (occ) {
+                        const u64 q = pos + (u64)__popcll(bm & lt);
+                        if (q < a.rec_cap) {
 #pragma unroll
-                        for (int j = 0; j < W; j++)
-                            a.rec_keys[(u64)j * a.rec_cap + q] = lkeys[(size_t)j * a.lcap + i];
-                        a.rec_cnts[q] = lcnt[i];
+                            for (int j = 0; j < W; j++)
+                                a.rec_keys[(u64)j * a.rec_cap + q] = lkeys[(size_t)j * a.lcap + i];
+                            a.rec_cnts[q] = lcnt[i];
+                        }
+                        // leave the slot empty for the next pass
+#pragma unroll
+                        for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+                        lcnt[i] = 0;
+                        if constexpr (W >= 2) lstate[i] = 0;
                     }
-                    // leave the slot empty for the next pass
-#pragma unroll
-                    for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
-                    lcnt[i] = 0;
-                    if constexpr (W >= 2) lstate[i] = 0;
+                    pos += (u64)__popcll(bm);
                 }
-                pos += rt;
             }
             __syncthreads();
             ++sub;
@@ -1869,7 +1951,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
 
 size_t bucket_lds_bytes(int W) {
     size_t lcap = (size_t)bucket_lds_slots(W);
-    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + 24 * 4 + 16;
+    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + 48 * 4 + 16;
 }
 
 hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, const uint64_t* starts,
@@ -1879,6 +1961,10 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
                                 hipStream_t s) {
     BucketArgs a;
+    {
+        const char* e = getenv("KC_P5_SKIP");
+        a.skip = e ? atoi(e) : 0;
+    }
     a.desc_key = desc_key;
     a.desc_start = desc_start;
     a.desc_len = desc_len;
@@ -1939,6 +2025,204 @@ hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const
     case 4: hipLaunchKernelGGL(reduce_add_k<4>, dim3(g), dim3(kBlock), 0, s, keys, stride, cnts, n, flags, pos, out_keys, ostride, out_cnts); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// P3, regional scatter. After P2 the keys sit in 256 regions by the low bucket
+// byte (word0 bits 48..55). P3 cuts every region into tiles of its own (a tile
+// never straddles two regions) and scatters each tile by the high byte (bits
+// 56..63). Positions come from a digit-major scan of per-tile histograms over
+// region-ordered tiles, which is exactly bucket start + offset, so the order
+// inside a tile does not matter: ranks are plain LDS atomics (no ballots), and
+// a tile of 16K keys (1024 threads) writes digit runs long enough to fill
+// whole lines. The next tile's keys are prefetched into registers.
+// tiles: region r holds tiles [tpre[r], tpre[r+1]); tile i of r starts at
+// rstart[r] + i * TILE.
+// ---------------------------------------------------------------------------
+
+constexpr int kP3Block = 1024;
+
+template <int W>
+struct P3Cfg {
+    static constexpr int KPT = (W == 1) ? 16 : (W == 2 ? 8 : 4);  // keys per thread
+    static constexpr int TILE = kP3Block * KPT;
+};
+
+int p3_tile(int W) { return kP3Block * ((W == 1) ? 16 : (W == 2 ? 8 : 4)); }
+
+__device__ __forceinline__ void p3_tile_range(const u64* __restrict__ rstart, const u64* __restrict__ tpre, u64 t,
+                                              int TILE, u64* lo, u64* hi) {
+    int a = 0, b = 256;  // region r with tpre[r] <= t < tpre[r+1]
+    while (b - a > 1) {
+        const int mid = (a + b) >> 1;
+        if (tpre[mid] <= t)
+            a = mid;
+        else
+            b = mid;
+    }
+    const u64 st = rstart[a] + (t - tpre[a]) * (u64)TILE;
+    *lo = st;
+    *hi = min(st + (u64)TILE, rstart[a + 1]);
+}
+
+// 256-thread blocks, one private histogram per wave (LDS atomics of a wave
+// only collide with its own lanes), summed at the end of the tile
+template <int W>
+__global__ __launch_bounds__(kBlock) void p3_upsweep_k(const u64* __restrict__ keys, const u64* __restrict__ rstart,
+                                                       const u64* __restrict__ tpre, u64 ntiles,
+                                                       u64* __restrict__ hist) {
+    constexpr int TILE = P3Cfg<W>::TILE;
+    __shared__ u32 h[4 * 256];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        for (int i = tid; i < 4 * 256; i += kBlock) h[i] = 0;
+        __syncthreads();
+        u64 lo, hi;
+        p3_tile_range(rstart, tpre, t, TILE, &lo, &hi);
+        u32* hw = h + wave * 256;
+        u64 i = lo + tid;
+        for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
+            const u64 k0 = __builtin_nontemporal_load(keys + i), k1 = __builtin_nontemporal_load(keys + i + kBlock),
+                      k2 = __builtin_nontemporal_load(keys + i + 2 * kBlock),
+                      k3 = __builtin_nontemporal_load(keys + i + 3 * kBlock);
+            atomicAdd(&hw[(u32)(k0 >> 56)], 1u);
+            atomicAdd(&hw[(u32)(k1 >> 56)], 1u);
+            atomicAdd(&hw[(u32)(k2 >> 56)], 1u);
+            atomicAdd(&hw[(u32)(k3 >> 56)], 1u);
+        }
+        for (; i < hi; i += kBlock) atomicAdd(&hw[(u32)(keys[i] >> 56)], 1u);
+        __syncthreads();
+        hist[(u64)tid * ntiles + t] = h[tid] + h[256 + tid] + h[512 + tid] + h[768 + tid];
+        __syncthreads();
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__ kin, u64* __restrict__ kout,
+                                                         u64 stride, const u64* __restrict__ rstart,
+                                                         const u64* __restrict__ tpre, u64 ntiles,
+                                                         const u64* __restrict__ pos) {
+    constexpr int KPT = P3Cfg<W>::KPT;
+    constexpr int TILE = P3Cfg<W>::TILE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* skey = (u64*)smem;                 // W x TILE
+    u32* cnt = (u32*)(skey + (size_t)W * TILE);  // 256
+    u32* dst = cnt + 256;                   // 256 digit starts in the tile
+    u64* gpos = (u64*)(dst + 256);          // 256 global run starts
+    u32* wsum = (u32*)(gpos + 256);         // 16 wave partial sums
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    u64 nk[KPT][W];
+    auto load = [&](u64 t) {
+        u64 lo = 0, hi = 0;
+        if (t < ntiles) p3_tile_range(rstart, tpre, t, TILE, &lo, &hi);
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u64 q = lo + (u64)i * kP3Block + tid;
+#pragma unroll
+            for (int j = 0; j < W; j++) nk[i][j] = q < hi ? __builtin_nontemporal_load(kin + (u64)j * stride + q) : 0ull;
+        }
+    };
+    load(blockIdx.x);
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        u64 lo, hi;
+        p3_tile_range(rstart, tpre, t, TILE, &lo, &hi);
+        const u32 len = (u32)(hi - lo);
+        u64 key[KPT][W];
+#pragma unroll
+        for (int i = 0; i < KPT; i++)
+#pragma unroll
+            for (int j = 0; j < W; j++) key[i][j] = nk[i][j];
+        if (tid < 256) {
+            cnt[tid] = 0;
+            gpos[tid] = pos[(u64)tid * ntiles + t];
+        }
+        __syncthreads();
+        load(t + gridDim.x);  // next tile's keys fly while this one is ranked
+        u32 rank[KPT];
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u32 q = (u32)i * kP3Block + (u32)tid;
+            if (q < len) rank[i] = atomicAdd(&cnt[(u32)(key[i][0] >> 56)], 1u);
+        }
+        __syncthreads();
+        // digit starts inside the tile: 256 counts, wave 0..3 scan
+        if (tid < 256) {
+            const u32 v = cnt[tid];
+            u32 inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            if (lane == 63) wsum[wave] = inc;
+            dst[tid] = inc - v;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            u32 add = 0;
+            for (int w = 0; w < wave; w++) add += wsum[w];
+            dst[tid] += add;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u32 q = (u32)i * kP3Block + (u32)tid;
+            if (q < len) {
+                const u32 at = dst[(u32)(key[i][0] >> 56)] + rank[i];
+#pragma unroll
+                for (int j = 0; j < W; j++) skey[(size_t)j * TILE + at] = key[i][j];
+            }
+        }
+        __syncthreads();
+        for (u32 q = tid; q < len; q += kP3Block) {
+            const u64 k0 = skey[q];
+            const u32 d = (u32)(k0 >> 56);
+            const u64 g = gpos[d] + (q - dst[d]);
+            kout[g] = k0;
+#pragma unroll
+            for (int j = 1; j < W; j++) kout[(u64)j * stride + g] = skey[(size_t)j * TILE + q];
+        }
+        __syncthreads();
+    }
+}
+
+size_t p3_scatter_lds(int W) {
+    return (size_t)W * p3_tile(W) * 8 + 512 * 4 + 256 * 8 + 16 * 4 + 16;
+}
+
+hipError_t launch_p3_hist(int W, const uint64_t* kin, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
+                          uint64_t* hist, uint64_t* tmp, int grid, hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    const int g = (int)hmin(ntiles, (u64)grid);
+    const int gu = (int)hmin(ntiles, (u64)grid * 4);
+#define KC_P3U(WW) hipLaunchKernelGGL(p3_upsweep_k<WW>, dim3(gu), dim3(kBlock), 0, s, kin, rstart, tpre, ntiles, hist)
+    switch (W) {
+    case 1: KC_P3U(1); break;
+    case 2: KC_P3U(2); break;
+    case 3: KC_P3U(3); break;
+    case 4: KC_P3U(4); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef KC_P3U
+    return scan_impl<u64>(hist, hist, (u64)256 * ntiles, tmp, s);
+}
+
+hipError_t launch_p3_scatter(int W, const uint64_t* kin, uint64_t* kout, uint64_t stride, const uint64_t* rstart,
+                             const uint64_t* tpre, uint64_t ntiles, const uint64_t* hist, int grid, hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    const int g = (int)hmin(ntiles, (u64)grid);
+    const size_t lds = (p3_scatter_lds(W) + 15) & ~(size_t)15;
+#define KC_P3S(WW)                                                                                              \
+    hipLaunchKernelGGL(p3_scatter_k<WW>, dim3(g), dim3(kP3Block), lds, s, kin, kout, stride, rstart, tpre, ntiles, \
+                       (const u64*)hist)
+    switch (W) {
+    case 1: KC_P3S(1); break;
+    case 2: KC_P3S(2); break;
+    case 3: KC_P3S(3); break;
+    case 4: KC_P3S(4); break;
+    }
+#undef KC_P3S
     return hipGetLastError();
 }
 

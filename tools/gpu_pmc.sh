@@ -16,4 +16,4 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_AC
   rc=$?; echo "group $i rc=$rc: $grp"
   [ $rc -eq 0 ] || exit $rc
 done
-python3 tools/pmc_summary.py $OUT $READS
+python3 tools/pmc_summary.py $OUT $READS ${K:-31}

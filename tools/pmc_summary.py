@@ -42,14 +42,22 @@ for name, n, per in rows:
                                  ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
                                   "SQ_INSTS_VMEM_WR", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
                                   "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE")))
-p2 = [r for r in rows if "count_front<1, 2>" in r[0]]
-if p2:
-    name, n, per = p2[0]
-    rec = {"kernel": "count_front<1,SINK_SCATTER> (P2)", "reads_per_gpu": reads,
-           "bytes_per_launch": 2 * per.get("FETCH_SIZE", 0) * 1024 + per.get("WRITE_SIZE", 0) * 1024,
-           "read_bytes": 2 * per.get("FETCH_SIZE", 0) * 1024, "write_bytes": per.get("WRITE_SIZE", 0) * 1024,
-           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/gpu_pmc.sh); "
-                     "2 x FETCH_SIZE + WRITE_SIZE per the gfx950 correction in MI355X_MICROARCH.md"}
-    os.makedirs("profiles", exist_ok=True)
-    json.dump(rec, open("profiles/pmc_count_kmers.json", "w"), indent=1)
-    print("wrote profiles/pmc_count_kmers.json", rec["bytes_per_launch"] / 1e9, "GB")
+k = int(sys.argv[3]) if len(sys.argv) > 3 else 31
+W = (k + 31) // 32
+want = {"P2": f"count_front<{W}, 2, true>", "P3": f"p3_scatter_k<{W}>", "P5": f"count_buckets<{W}>"}
+rec = {"reads_per_gpu": reads, "k": k, "kernels": {},
+       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, --kernel-trace only "
+                 "(tools/gpu_pmc.sh); HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), "
+                 "per the gfx950 FETCH_SIZE correction in MI355X_MICROARCH.md"}
+for tag, pat in want.items():
+    hit = [r for r in rows if pat in r[0]]
+    if not hit:
+        continue
+    name, n, per = hit[0]
+    rd = 2 * per.get("FETCH_SIZE", 0) * 1024
+    wr = per.get("WRITE_SIZE", 0) * 1024
+    rec["kernels"][tag] = {"kernel": name, "bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr}
+os.makedirs("profiles", exist_ok=True)
+json.dump(rec, open("profiles/pmc_count_kmers.json", "w"), indent=1)
+json.dump(rec, open(os.path.join(out, "pmc_count_kmers.json"), "w"), indent=1)  # travels back from the box
+print("wrote profiles/pmc_count_kmers.json", {t: round(v["bytes_per_launch"] / 1e9, 2) for t, v in rec["kernels"].items()})
