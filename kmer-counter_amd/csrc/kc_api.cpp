@@ -50,6 +50,7 @@ struct kc_ctx {
     uint64_t* table = nullptr;
     uint64_t cap = 0;
     size_t table_bytes = 0;
+    bool table_dirty = true;  // a slot may be non-zero (cleared by kc_reset)
     uint64_t* spill = nullptr;
     uint64_t spill_cap = 0;
     uint64_t* stats = nullptr;      // device ST_N
@@ -63,7 +64,7 @@ struct kc_ctx {
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
     // P5 segment descriptors (see finish_part_sorted) and their sort scratch
-    DevBuf desc_key, desc_start, desc_len, desc_k2, desc_v, desc_v2, desc_lens, desc_offs;
+    DevBuf desc_key, desc_start, desc_len, desc_k2, desc_v, desc_v2, desc_lens, desc_offs, desc_fb;
     uint64_t* rec_keys = nullptr;  // W x rec_cap
     uint32_t* rec_cnts = nullptr;
     uint64_t rec_cap = 0;
@@ -698,7 +699,7 @@ void kc_destroy(kc_ctx* c) {
     release(c->part_codes);
     release(c->part_inval);
     DevBuf* dbufs[] = {&c->desc_key, &c->desc_start, &c->desc_len, &c->desc_k2, &c->desc_v, &c->desc_v2,
-                       &c->desc_lens, &c->desc_offs};
+                       &c->desc_lens, &c->desc_offs, &c->desc_fb};
     for (DevBuf* b : dbufs) release(*b);
     release(c->part_base);
     release(c->part_tmp);
@@ -715,7 +716,15 @@ void kc_destroy(kc_ctx* c) {
 kc_status kc_reset(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
+    // the global table is cleared only when a slot was claimed since the last
+    // clear (the partition engine's table is a rarely used fallback: clearing
+    // 1/16 of gpuMemoryLimit per reset would cost milliseconds per count)
+    kc_status s0 = sync_stats(c);
+    if (s0) return s0;
+    if (c->table_dirty || c->stats_h[ST_CLAIMED] > 0) {
+        HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
+        c->table_dirty = false;
+    }
     HIPCHK(c, hipMemsetAsync(c->stats, 0, ST_N * 8, c->stream));
     if (c->rec_cursor) HIPCHK(c, hipMemsetAsync(c->rec_cursor, 0, 8, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -831,9 +840,14 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
                                    c->stream));
         HIPCHK(c, launch_scan_u64((const uint64_t*)c->desc_lens.p, (uint64_t*)c->desc_offs.p, ndesc,
                                   (uint64_t*)c->rle_tmp.p, c->stream));
+        // LSD fallback list (u32 per descriptor + count) in the free sort scratch
+        uint32_t* fb = (uint32_t*)c->desc_k2.p;
+        uint64_t* fb_n = (uint64_t*)c->desc_lens.p;  // desc_lens is consumed by the scan above
+        if ((s = ensure(c, c->desc_fb, ndesc * 4 + 16))) return s;
+        fb = (uint32_t*)c->desc_fb.p;
         HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, order, (const uint64_t*)c->desc_start.p,
                                   (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, k0 + off0,
-                                  c0 + off0, out_cap, c->stats, c->n_cu, c->stream));
+                                  c0 + off0, out_cap, c->stats, fb, fb_n, c->n_cu, c->stream));
     }
     if (key0) {
         for (int j = 0; j < W; j++) HIPCHK(c, hipMemsetAsync(k0 + (size_t)j * out_cap, 0, 8, c->stream));

@@ -686,10 +686,24 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                     for (u32 q = tid; q < n; q += kBlock) {
                         const u32 i = s_perm[q];
                         const u32 d = s_dig[i];
-                        const u64 g = s_cur[d] + (q - s_start[d]);
+                        const u64 c0 = s_cur[d];
+                        const u64 g = c0 + (q - s_start[d]);
                         if (pa.skip & 1) continue;
+                        // a 64-byte sector this run covers whole is streamed out
+                        // (non-temporal); the partial sectors at the run's ends
+                        // stay in L2 so the next flush of this digit completes
+                        // them before they are written back
+                        const u64 sec = g & ~7ull;
+                        const bool whole = sec >= c0 && sec + 8 <= c0 + s_cnt[d];
 #pragma unroll
-                        for (int j = 0; j < W; j++) pa.out[(u64)j * pa.out_stride + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
+                        for (int j = 0; j < W; j++) {
+                            const u64 v = s_stage[(size_t)j * (pa.scap + 1) + i];
+                            u64* dst = pa.out + (u64)j * pa.out_stride + g;
+                            if (whole)
+                                __builtin_nontemporal_store(v, dst);
+                            else
+                                *dst = v;
+                        }
                     }
                     __syncthreads();
                     s_cur[tid] += s_cnt[tid];
@@ -1915,7 +1929,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                         if (di < a.desc_cap) {
                             a.desc_key[di] = ((u64)b << 48) | ((u64)sub << (48 - __builtin_ctz(m)));
                             a.desc_start[di] = rbase;
-                            a.desc_len[di] = total;
+                            a.desc_len[di] = total | ((u32)__builtin_ctz(m) << 24);  // len | log2(m) << 24
                         }
                     }
                 }
@@ -2107,8 +2121,9 @@ __global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__
     constexpr int TILE = P3Cfg<W>::TILE;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* skey = (u64*)smem;                 // W x TILE
-    u32* cnt = (u32*)(skey + (size_t)W * TILE);  // 256
-    u32* dst = cnt + 256;                   // 256 digit starts in the tile
+    u32* wc = (u32*)(skey + (size_t)W * TILE);   // 16 waves x 128 words: two u16 rank counters each
+    unsigned short* woff = (unsigned short*)(wc + 16 * 128);  // 16 x 256 wave offsets inside a digit
+    u32* dst = (u32*)(woff + 16 * 256);     // 256 digit starts in the tile
     u64* gpos = (u64*)(dst + 256);          // 256 global run starts
     u32* wsum = (u32*)(gpos + 256);         // 16 wave partial sums
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -2133,22 +2148,31 @@ __global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__
         for (int i = 0; i < KPT; i++)
 #pragma unroll
             for (int j = 0; j < W; j++) key[i][j] = nk[i][j];
-        if (tid < 256) {
-            cnt[tid] = 0;
-            gpos[tid] = pos[(u64)tid * ntiles + t];
-        }
+        for (int i = tid; i < 16 * 128; i += kP3Block) wc[i] = 0;
+        if (tid < 256) gpos[tid] = pos[(u64)tid * ntiles + t];
         __syncthreads();
         load(t + gridDim.x);  // next tile's keys fly while this one is ranked
+        // ranks inside the wave's own counters (atomics only collide within
+        // a wave); a (wave, digit) offset table then orders the waves
         u32 rank[KPT];
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
             const u32 q = (u32)i * kP3Block + (u32)tid;
-            if (q < len) rank[i] = atomicAdd(&cnt[(u32)(key[i][0] >> 56)], 1u);
+            if (q < len) {
+                const u32 d = (u32)(key[i][0] >> 56);
+                const u32 sh = 16 * (d & 1);
+                rank[i] = (atomicAdd(&wc[wave * 128 + (d >> 1)], 1u << sh) >> sh) & 0xffffu;
+            }
         }
         __syncthreads();
-        // digit starts inside the tile: 256 counts, wave 0..3 scan
+        // per digit: wave offsets, digit total, then digit starts (waves 0..3)
         if (tid < 256) {
-            const u32 v = cnt[tid];
+            u32 run = 0;
+            for (int w = 0; w < 16; w++) {
+                woff[w * 256 + tid] = (unsigned short)run;
+                run += (wc[w * 128 + (tid >> 1)] >> (16 * (tid & 1))) & 0xffffu;
+            }
+            const u32 v = run;
             u32 inc = v;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -2169,7 +2193,8 @@ __global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__
         for (int i = 0; i < KPT; i++) {
             const u32 q = (u32)i * kP3Block + (u32)tid;
             if (q < len) {
-                const u32 at = dst[(u32)(key[i][0] >> 56)] + rank[i];
+                const u32 d = (u32)(key[i][0] >> 56);
+                const u32 at = dst[d] + woff[wave * 256 + d] + rank[i];
 #pragma unroll
                 for (int j = 0; j < W; j++) skey[(size_t)j * TILE + at] = key[i][j];
             }
@@ -2188,7 +2213,7 @@ __global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__
 }
 
 size_t p3_scatter_lds(int W) {
-    return (size_t)W * p3_tile(W) * 8 + 512 * 4 + 256 * 8 + 16 * 4 + 16;
+    return (size_t)W * p3_tile(W) * 8 + 16 * 128 * 4 + 16 * 256 * 2 + 256 * 4 + 256 * 8 + 16 * 4 + 16;
 }
 
 hipError_t launch_p3_hist(int W, const uint64_t* kin, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
@@ -2241,7 +2266,7 @@ hipError_t launch_p3_scatter(int W, const uint64_t* kin, uint64_t* kout, uint64_
 __global__ __launch_bounds__(kBlock) void desc_prep_k(const u32* __restrict__ order, const u32* __restrict__ len,
                                                       u64 n, u64* __restrict__ lens_sorted) {
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock)
-        lens_sorted[i] = len[order[i]];
+        lens_sorted[i] = len[order[i]] & 0xffffffu;
 }
 
 __global__ __launch_bounds__(kBlock) void iota_k(u32* out, u64 n) {
@@ -2271,18 +2296,147 @@ struct SegCfg {
     static constexpr int ITEMS = CAP / kSegBlock;
 };
 
+size_t seg_sort_msd_lds(int W) {
+    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));
+    return (size_t)cap * (8 * W + 2) + 4096 * 4 + 32 * 4 + 16;
+}
+
 size_t seg_sort_lds(int W) {
     int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));
     return (size_t)cap * (8 * W + 2) + (size_t)2 * kSegWaves * 256 * 4 + 512 * 4 + 2 * 4 * kSegWaves * 8 + 64;
 }
 
+// MSD segment sort: the bits just below the bucket prefix and the pass's
+// sub-range bits (known from the descriptor) give a 12-bit digit; a counting
+// pass and a scatter pass stream the segment from global memory (L2-resident
+// after the first), bins are insertion-sorted by their owner thread. Keys are
+// distinct, so the unstable LDS-atomic placement is fine. A segment whose
+// largest bin exceeds kMaxBin (skewed keys) is left to seg_sort_lsd_k.
 template <int W>
 __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ rkeys, const u32* __restrict__ rcnts,
                                                         u64 rstride, const u32* __restrict__ order,
                                                         const u64* __restrict__ dstart, const u32* __restrict__ dlen,
                                                         const u64* __restrict__ out_off, u64 ndesc,
                                                         u64* __restrict__ okeys, u32* __restrict__ ocnts,
-                                                        u64 ostride, u64* __restrict__ stats) {
+                                                        u64 ostride, u64* __restrict__ stats, u32* __restrict__ fb,
+                                                        u64* __restrict__ fb_n) {
+    constexpr int CAP = SegCfg<W>::CAP;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* skey = (u64*)smem;                                            // W x CAP
+    unsigned short* sidx = (unsigned short*)(skey + (size_t)W * CAP);  // CAP
+    u32* bcnt = (u32*)(sidx + CAP);                                    // 4096 bins
+    u32* misc = bcnt + 4096;                                           // [0] skew flag, [1..16] wave sums
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    for (u64 di = blockIdx.x; di < ndesc; di += gridDim.x) {
+        const u32 o = order[di];
+        const u64 st = dstart[o];
+        const u32 lw = dlen[o];
+        const u32 len = lw & 0xffffffu;
+        const int l2m = (int)(lw >> 24);
+        const u64 obase = out_off[di];
+        const int sh = 36 - l2m;  // digit = word0 bits [sh, sh + 12)
+        for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
+        if (tid == 0) misc[0] = 0;
+        __syncthreads();
+        if (len > (u32)CAP) {
+            if (tid == 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_SEG_TOO_LONG);
+            __syncthreads();
+            continue;
+        }
+        for (u32 p = tid; p < len; p += kSegBlock) atomicAdd(&bcnt[(u32)(rkeys[st + p] >> sh) & 4095u], 1u);
+        __syncthreads();
+        // bin starts: 4 bins per thread, block-wide exclusive scan; skew check
+        const u32 c0 = bcnt[4 * tid], c1 = bcnt[4 * tid + 1], c2 = bcnt[4 * tid + 2], c3 = bcnt[4 * tid + 3];
+        const u32 sum = c0 + c1 + c2 + c3;
+        u32 inc = sum;
+#pragma unroll
+        for (int o2 = 1; o2 < 64; o2 <<= 1) {
+            const u32 y = __shfl_up(inc, o2);
+            if (lane >= o2) inc += y;
+        }
+        if (lane == 63) misc[1 + wave] = inc;
+        if (max(max(c0, c1), max(c2, c3)) > kMaxBin) atomicOr(&misc[0], 1u);
+        __syncthreads();
+        if (misc[0]) {
+            if (tid == 0) {
+                const u64 f = atomicAdd((unsigned long long*)fb_n, 1ull);
+                fb[f] = (u32)di;
+            }
+            __syncthreads();
+            continue;
+        }
+        u32 wpre = 0;
+        for (int w = 0; w < wave; w++) wpre += misc[1 + w];
+        const u32 bs = wpre + inc - sum;  // start of this thread's first bin
+        bcnt[4 * tid] = bs;
+        bcnt[4 * tid + 1] = bs + c0;
+        bcnt[4 * tid + 2] = bs + c0 + c1;
+        bcnt[4 * tid + 3] = bs + c0 + c1 + c2;
+        __syncthreads();
+        // scatter into bins (bcnt becomes each bin's end)
+        for (u32 p = tid; p < len; p += kSegBlock) {
+            u64 k[W];
+#pragma unroll
+            for (int j = 0; j < W; j++) k[j] = rkeys[(u64)j * rstride + st + p];
+            const u32 q = atomicAdd(&bcnt[(u32)(k[0] >> sh) & 4095u], 1u);
+#pragma unroll
+            for (int j = 0; j < W; j++) skey[(size_t)j * CAP + q] = k[j];
+            sidx[q] = (unsigned short)p;
+        }
+        __syncthreads();
+        // insertion sort of this thread's 4 bins [bs, bs + sum)
+        const u32 ends[4] = {bs + c0, bs + c0 + c1, bs + c0 + c1 + c2, bs + sum};
+        u32 s0 = bs;
+        for (int qb = 0; qb < 4; qb++) {
+            const u32 e0 = ends[qb];
+            for (u32 x = s0 + 1; x < e0; x++) {
+                u64 kx[W];
+#pragma unroll
+                for (int jj = 0; jj < W; jj++) kx[jj] = skey[(size_t)jj * CAP + x];
+                const unsigned short ix = sidx[x];
+                u32 y = x;
+                while (y > s0) {
+                    bool less = false, eq = true;
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) {
+                        const u64 ky = skey[(size_t)jj * CAP + y - 1];
+                        if (eq && kx[jj] != ky) {
+                            less = kx[jj] < ky;
+                            eq = false;
+                        }
+                    }
+                    if (!less) break;
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = skey[(size_t)jj * CAP + y - 1];
+                    sidx[y] = sidx[y - 1];
+                    y--;
+                }
+#pragma unroll
+                for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = kx[jj];
+                sidx[y] = ix;
+            }
+            s0 = e0;
+        }
+        __syncthreads();
+        for (u32 p = tid; p < len; p += kSegBlock) {
+#pragma unroll
+            for (int jj = 0; jj < W; jj++) okeys[(u64)jj * ostride + obase + p] = skey[(size_t)jj * CAP + p];
+            ocnts[obase + p] = rcnts[st + sidx[p]];
+        }
+        __syncthreads();
+    }
+}
+
+// LSD fallback for segments with a bin larger than kMaxBin (skewed keys):
+// radix passes over the varying bytes with stable wave-private ranking.
+template <int W>
+__global__ __launch_bounds__(kSegBlock) void seg_sort_lsd_k(const u64* __restrict__ rkeys, const u32* __restrict__ rcnts,
+                                                        u64 rstride, const u32* __restrict__ order,
+                                                        const u64* __restrict__ dstart, const u32* __restrict__ dlen,
+                                                        const u64* __restrict__ out_off, u64 ndesc,
+                                                        u64* __restrict__ okeys, u32* __restrict__ ocnts,
+                                                        u64 ostride, u64* __restrict__ stats,
+                                                        const u32* __restrict__ fb, const u64* __restrict__ fb_n) {
     constexpr int CAP = SegCfg<W>::CAP;
     constexpr int ITEMS = SegCfg<W>::ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2297,15 +2451,13 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
     const u64 lt = lanemask_lt();
     for (int i = tid; i < kSegWaves * 256; i += kSegBlock) wcnt[i] = 0;
     __syncthreads();
-    for (u64 di = blockIdx.x; di < ndesc; di += gridDim.x) {
+    const u64 nfb = *fb_n;
+    for (u64 fi = blockIdx.x; fi < nfb; fi += gridDim.x) {
+        const u64 di = fb[fi];
         const u32 o = order[di];
         const u64 st = dstart[o];
-        const u32 len = dlen[o];
+        const u32 len = dlen[o] & 0xffffffu;
         const u64 obase = out_off[di];
-        if (len > (u32)CAP) {
-            if (tid == 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_SEG_TOO_LONG);
-            continue;
-        }
         // blocked-by-wave, lane-striped items over R = ceil(len / 1024) rounds:
         // position p = wave*64*R + it*64 + lane, so every wave holds a share
         const int R = (int)((len + kSegBlock - 1) / kSegBlock);
@@ -2331,6 +2483,10 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             }
             idx[it] = (unsigned short)p;
         }
+        if (len > (u32)CAP) {
+            if (tid == 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_SEG_TOO_LONG);
+            continue;
+        }
         // bytes that vary inside the segment
 #pragma unroll
         for (int j = 0; j < W; j++) {
@@ -2355,120 +2511,6 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             diff[j] = oo ^ aa;
         }
         __syncthreads();
-        // MSD fast path: one LDS counting pass on the 12 most significant
-        // varying bits (keys are distinct, so an unstable rank is fine), then
-        // every thread insertion-sorts its 4 bins. Bins larger than kMaxBin
-        // (skewed keys) fall back to the LSD passes below.
-        int hw = -1, hb = 0;
-#pragma unroll
-        for (int j = W - 1; j >= 0; j--)
-            if (diff[j]) {
-                hw = j;
-                hb = 63 - __builtin_clzll(diff[j]);
-            }
-        bool fast = hw >= 0;
-        if (fast) {
-            const int lo = hb >= 11 ? hb - 11 : 0;
-            u32* bcnt = wcnt;  // 4096 bins (wcnt/woff area)
-            for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
-            if (tid == 0) dtot[0] = 0;
-            __syncthreads();
-            u32 dig[ITEMS], rank[ITEMS];
-#pragma unroll
-            for (int it = 0; it < ITEMS; it++) {
-                if (it >= R) break;
-                const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
-                u64 kw = key[it][0];
-#pragma unroll
-                for (int jj = 1; jj < W; jj++)
-                    if (jj == hw) kw = key[it][jj];
-                dig[it] = (u32)(kw >> lo) & 4095u;
-                if (p < len) rank[it] = atomicAdd(&bcnt[dig[it]], 1u);
-            }
-            __syncthreads();
-            // bin starts: 4 bins per thread, block-wide exclusive scan
-            const u32 c0 = bcnt[4 * tid], c1 = bcnt[4 * tid + 1], c2 = bcnt[4 * tid + 2], c3 = bcnt[4 * tid + 3];
-            const u32 mx = max(max(c0, c1), max(c2, c3));
-            const u32 sum = c0 + c1 + c2 + c3;
-            u32 inc = sum;
-#pragma unroll
-            for (int o2 = 1; o2 < 64; o2 <<= 1) {
-                const u32 y = __shfl_up(inc, o2);
-                if (lane >= o2) inc += y;
-            }
-            if (lane == 63) dst0[wave] = inc;
-            if (mx > kMaxBin) atomicOr(&dtot[0], 1u);
-            __syncthreads();
-            u32 wpre = 0;
-            for (int w = 0; w < wave; w++) wpre += dst0[w];
-            const u32 ex = wpre + inc - sum;
-            bcnt[4 * tid] = ex;
-            bcnt[4 * tid + 1] = ex + c0;
-            bcnt[4 * tid + 2] = ex + c0 + c1;
-            bcnt[4 * tid + 3] = ex + c0 + c1 + c2;
-            fast = dtot[0] == 0;
-            __syncthreads();
-            if (fast) {
-#pragma unroll
-                for (int it = 0; it < ITEMS; it++) {
-                    if (it >= R) break;
-                    const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
-                    if (p < len) {
-                        const u32 q = bcnt[dig[it]] + rank[it];
-#pragma unroll
-                        for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + q] = key[it][jj];
-                        sidx[q] = idx[it];
-                    }
-                }
-                __syncthreads();
-                // insertion sort of this thread's 4 bins [4t, 4t+4)
-                const u32 bs = bcnt[4 * tid];
-                const u32 be = bs + sum;
-                const u32 b1 = bs + c0, b2 = b1 + c1, b3 = b2 + c2;
-                for (int q = 0; q < 4; q++) {
-                    const u32 s0 = q == 0 ? bs : (q == 1 ? b1 : (q == 2 ? b2 : b3));
-                    const u32 e0 = q == 0 ? b1 : (q == 1 ? b2 : (q == 2 ? b3 : be));
-                    for (u32 x = s0 + 1; x < e0; x++) {
-                        u64 kx[W];
-#pragma unroll
-                        for (int jj = 0; jj < W; jj++) kx[jj] = skey[(size_t)jj * CAP + x];
-                        const unsigned short ix = sidx[x];
-                        u32 y = x;
-                        while (y > s0) {
-                            bool less = false, eq = true;
-#pragma unroll
-                            for (int jj = 0; jj < W; jj++) {
-                                const u64 ky = skey[(size_t)jj * CAP + y - 1];
-                                if (eq && kx[jj] != ky) {
-                                    less = kx[jj] < ky;
-                                    eq = false;
-                                }
-                            }
-                            if (!less) break;
-#pragma unroll
-                            for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = skey[(size_t)jj * CAP + y - 1];
-                            sidx[y] = sidx[y - 1];
-                            y--;
-                        }
-#pragma unroll
-                        for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = kx[jj];
-                        sidx[y] = ix;
-                    }
-                }
-                __syncthreads();
-                for (u32 p = tid; p < len; p += kSegBlock) {
-#pragma unroll
-                    for (int jj = 0; jj < W; jj++) okeys[(u64)jj * ostride + obase + p] = skey[(size_t)jj * CAP + p];
-                    ocnts[obase + p] = rcnts[st + sidx[p]];
-                }
-                // bins were counted in wcnt: the LSD path expects it zeroed
-                for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
-                __syncthreads();
-                continue;
-            }
-            for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
-            __syncthreads();
-        }
         for (int j = W - 1; j >= 0; j--) {
             u64 dj = 0;
 #pragma unroll
@@ -2566,13 +2608,18 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
 
 hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, uint64_t rstride, const uint32_t* order,
                            const uint64_t* dstart, const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc,
-                           uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, int grid,
-                           hipStream_t s) {
+                           uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, uint32_t* fb,
+                           uint64_t* fb_n, int grid, hipStream_t s) {
     if (ndesc == 0) return hipSuccess;
-    size_t lds = (seg_sort_lds(W) + 15) & ~(size_t)15;
-#define KC_SEG(WW)                                                                                                 \
-    hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds, s, rkeys, rcnts, rstride, order, dstart, \
-                       dlen, out_off, ndesc, okeys, ocnts, ostride, stats)
+    hipError_t e = hipMemsetAsync(fb_n, 0, 8, s);
+    if (e != hipSuccess) return e;
+    const size_t lds_msd = (seg_sort_msd_lds(W) + 15) & ~(size_t)15;
+    const size_t lds = (seg_sort_lds(W) + 15) & ~(size_t)15;
+#define KC_SEG(WW)                                                                                                  \
+    hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds_msd, s, rkeys, rcnts, rstride, order,       \
+                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, stats, fb, fb_n);                       \
+    hipLaunchKernelGGL(seg_sort_lsd_k<WW>, dim3(grid), dim3(kSegBlock), lds, s, rkeys, rcnts, rstride, order,       \
+                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, stats, (const u32*)fb, (const u64*)fb_n)
     switch (W) {
     case 1: KC_SEG(1); break;
     case 2: KC_SEG(2); break;

@@ -496,3 +496,18 @@ def test_config5_full_size_properties(kca):
                 break
             j += 1
         assert found, key
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_skewed_segment_uses_lsd_fallback(kca, orc, k):
+    """Reads that all start with the same 14 bases put >2000 distinct k-mers
+    into one 12-bit bin of one P5 segment: the segment sort's MSD pass hands
+    that segment to the LSD fallback kernel; output still bit-exact."""
+    rng = random.Random(k)
+    prefix = "ACGTTGCAACGTGA"
+    reads = [prefix + "".join(rng.choice("ACGT") for _ in range(136)) for _ in range(3000)]
+    fq = _fq(reads).encode()
+    with kca.Context(kmer_length=k, line_length=150) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, k)
