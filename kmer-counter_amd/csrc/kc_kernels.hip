@@ -1606,10 +1606,11 @@ __device__ __forceinline__ u32 block_excl_scan_n(u32 v, u32* lds, u32* total) {
 }
 
 int bucket_lds_slots(int W) {
-    // slot: W key words + u32 count (+ u32 state for W >= 2); ~147 KiB per CU
+    // slot: W key words + u32 count (+ u32 state for W >= 2); ~139 KiB per CU
+    // (the rest: per-wave slow-path queues); multiple of 64, <= SegCfg CAP
     int per = 8 * W + 4 + (W >= 2 ? 4 : 0);
-    int slots = (147 * 1024) / per;
-    return slots / kBucketBlock * kBucketBlock;
+    int slots = (139 * 1024) / per;
+    return slots / 64 * 64;
 }
 
 struct BucketArgs {
@@ -1746,6 +1747,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
 // sub-ranges stay valid. Only at m == kMaxSub do keys that miss the table go
 // to the global fallback table and then to the spill buffer.
 constexpr u32 kMaxSub = 1024;
+constexpr u32 kQueue = 128;  // P5 per-wave slow-path queue entries (u32)
 
 template <int W>
 __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
@@ -1759,6 +1761,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
     u32* lnext = misc + 22;
     u32* wtot_l = misc + 24;  // kBucketWaves per-wave record counts
     const int tid = threadIdx.x;
+    const int lane = (int)lane_id();
+    const u64 lane_lt = lanemask_lt();
+    u32* wq = misc + 48 + (tid >> 6) * kQueue;  // this wave's slow-path queue (bucket offsets)
     for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
         for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
@@ -1788,6 +1793,56 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         while (sub < m) {
             const bool last = m >= mmax;
             u64 scanned = 0;
+            u32 qn = 0;  // entries in this wave's queue (wave-uniform)
+            // slow path for the first c queued keys: full probing insert, fill
+            // and abort accounting, last-resort global table and spill
+            auto drain = [&](u32 c) {
+                const bool act = lane < (int)c;
+                u64 qk[W];
+#pragma unroll
+                for (int j = 0; j < W; j++) qk[j] = 0;
+                if (act) {
+                    const u64 gi = lo + wq[lane];
+#pragma unroll
+                    for (int j = 0; j < W; j++) qk[j] = a.keys[(u64)j * a.stride + gi];
+                }
+                bool done = true, claimed = false, lclaim = false, full = false;
+                if (act) {
+                    if (!lds_insert<W>(qk, slot_frac<W>(qk), lkeys, lcnt, lstate, a.lcap,
+                                       last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u), &lclaim)) {
+                        if (!last) {
+                            full = true;
+                        } else if constexpr (W == 1) {
+                            done = insert_w1(qk[0], a.table, a.cap, a.probe_limit, &claimed);
+                        } else {
+                            done = insert_wide<W>(qk, a.table, a.cap, a.probe_limit, &claimed);
+                        }
+                    }
+                }
+                const u64 lm = __ballot(lclaim);
+                const u64 fm = __ballot(full);
+                if (!last && (lm || fm) && lane == 0) {
+                    u32 f = atomicAdd(lfill, (u32)__popcll(lm)) + (u32)__popcll(lm);
+                    if (fm || f > limit) atomicOr(labort, 1u);
+                }
+                if (last) {
+                    u64 cm = __ballot(claimed);
+                    if (cm && lane == __ffsll((long long)cm) - 1)
+                        atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+                    bool spill = !done;
+                    if (__ballot(spill)) {
+                        u64 idx = wave_reserve(a.spill_ctr, spill);
+                        if (spill) {
+                            if (idx < a.spill_cap) {
+#pragma unroll
+                                for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = qk[j];
+                            } else {
+                                atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                            }
+                        }
+                    }
+                }
+            };
             constexpr int U = 4;  // independent key loads in flight per thread
             // software pipeline: the next iteration's keys are loaded before
             // this iteration's inserts, so HBM latency overlaps LDS work
@@ -1817,53 +1872,61 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
 #pragma unroll
                     for (int j = 0; j < W; j++) nkey[u][j] = i < hi ? a.keys[(u64)j * a.stride + i] : 0ull;
                 }
+                // fast path, branch-light: a key already in its home group (W=1)
+                // or home slot (W>=2) is counted in place; every other wanted
+                // key goes to the wave's queue (its offset in the bucket), and
+                // the queue is drained 64 keys at a time with all lanes active
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    bool done = true, claimed = false, lclaim = false, full = false;
-                    if (live[u]) {
-                        // sub-range by the key bits below the bucket prefix (key
-                        // order), slot by a multiply-shift hash; outside the
-                        // last resort a long probe means "table full" (abort)
-                        if ((u32)(((key[u][0] & M48) * (u64)m) >> 48) == sub && !a.skip) {
-                            if (!lds_insert<W>(key[u], slot_frac<W>(key[u]), lkeys, lcnt, lstate, a.lcap,
-                                               last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u), &lclaim)) {
-                                if (!last) {
-                                    full = true;
-                                } else if constexpr (W == 1) {
-                                    done = insert_w1(key[u][0], a.table, a.cap, a.probe_limit, &claimed);
-                                } else {
-                                    done = insert_wide<W>(key[u], a.table, a.cap, a.probe_limit, &claimed);
-                                }
+                    const u64 gi = base + (u64)u * kBucketBlock + tid;
+                    const bool want =
+                        live[u] && !a.skip && (u32)(((key[u][0] & M48) * (u64)m) >> 48) == sub;
+                    bool found = false;
+                    const u64 fr = slot_frac<W>(key[u]);
+                    if constexpr (W == 1) {
+                        if ((a.lcap & 3u) == 0) {
+                            const u32 g = (u32)((fr * (u64)(a.lcap >> 2)) >> 48);
+                            typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+                            const volatile v2u64* gp = (const volatile v2u64*)(lkeys + 4 * g);
+                            const v2u64 a0 = gp[0], a1 = gp[1];
+                            const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
+                            int hit = -1, emp = -1;
+#pragma unroll
+                            for (int i = 3; i >= 0; i--) {
+                                if (v[i] == key[u][0]) hit = i;
+                                if (v[i] == 0ull) emp = i;
                             }
+                            found = want && hit >= 0 && (emp < 0 || hit < emp);
+                            if (found) atomicAdd(&lcnt[4 * g + hit], 1u);
+                        }
+                    } else {
+                        const u32 sl = (u32)((fr * (u64)a.lcap) >> 48);
+                        if (__hip_atomic_load(&lstate[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
+                            bool eq = true;
+#pragma unroll
+                            for (int j = 0; j < W; j++) eq = eq && lkeys[(size_t)j * a.lcap + sl] == key[u][j];
+                            found = want && eq;
+                            if (found) atomicAdd(&lcnt[sl], 1u);
                         }
                     }
-                    const u64 lm = __ballot(lclaim);
-                    const u64 fm = __ballot(full);
-                    const int leader = (int)lane_id() == 0;
-                    if (!last && (lm || fm) && leader) {
-                        u32 f = atomicAdd(lfill, (u32)__popcll(lm)) + (u32)__popcll(lm);
-                        if (fm || f > limit) atomicOr(labort, 1u);
-                    }
-                    if (last) {
-                        u64 cm = __ballot(claimed);
-                        if (cm && (int)lane_id() == __ffsll((long long)cm) - 1)
-                            atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-                        bool spill = !done;
-                        if (__ballot(spill)) {
-                            u64 idx = wave_reserve(a.spill_ctr, spill);
-                            if (spill) {
-                                if (idx < a.spill_cap) {
-#pragma unroll
-                                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = key[u][j];
-                                } else {
-                                    atomicOr((unsigned long long*)&a.stats[ST_ERR],
-                                             (unsigned long long)ERR_SPILL_OVERFLOW);
-                                }
-                            }
+                    const bool pend = want && !found;
+                    const u64 pb = __ballot(pend);
+                    if (pb) {
+                        if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = (u32)(gi - lo);
+                        qn += (u32)__popcll(pb);
+                        if (qn >= 64) {
+                            drain(64);
+                            // keep the overflow (< 64 entries) at the queue front
+                            const u32 rest = qn - 64;
+                            const u32 keep = lane < (int)rest ? wq[64 + lane] : 0u;
+                            if (lane < (int)rest) wq[lane] = keep;
+                            qn = rest;
                         }
                     }
                 }
             }
+            // leftovers (an aborted pass is restarted from scratch instead)
+            if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) drain(qn);
             __syncthreads();
             const bool aborted = *labort != 0u;  // every thread reads before tid 0 resets it
             __syncthreads();
@@ -1897,7 +1960,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             // output offset, and it writes its records in slot order (no
             // block-wide scans, two barriers per pass)
             {
-                const int wave = tid >> 6, lane = (int)lane_id();
+                const int wave = tid >> 6;
                 const u32 spw = (a.lcap + kBucketWaves - 1) / kBucketWaves;
                 const u32 s0 = (u32)wave * spw;
                 const u32 s1 = min(a.lcap, s0 + spw);
@@ -1965,7 +2028,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
 
 size_t bucket_lds_bytes(int W) {
     size_t lcap = (size_t)bucket_lds_slots(W);
-    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + 48 * 4 + 16;
+    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + (48 + (size_t)kBucketWaves * kQueue) * 4 + 16;
 }
 
 hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, const uint64_t* starts,
@@ -2292,17 +2355,17 @@ constexpr int kSegWaves = kSegBlock / 64;
 
 template <int W>
 struct SegCfg {
-    static constexpr int CAP = (W == 1) ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));  // >= bucket_lds_slots
-    static constexpr int ITEMS = CAP / kSegBlock;
+    static constexpr int CAP = (W == 1) ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));  // >= bucket_lds_slots
+    static constexpr int ITEMS = (CAP + kSegBlock - 1) / kSegBlock;
 };
 
 size_t seg_sort_msd_lds(int W) {
-    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));
+    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));
     return (size_t)cap * (8 * W + 2) + 4096 * 4 + 32 * 4 + 16;
 }
 
 size_t seg_sort_lds(int W) {
-    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4096 : 3072));
+    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));
     return (size_t)cap * (8 * W + 2) + (size_t)2 * kSegWaves * 256 * 4 + 512 * 4 + 2 * 4 * kSegWaves * 8 + 64;
 }
 
