@@ -109,7 +109,7 @@ def main():
                     help="N>1: key-space all-to-all (cfg4) or read-shard only (cfg3); ignored at N=1")
     args = ap.parse_args()
     preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
-              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=64 << 30)}[args.config]
+              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=72 << 30)}[args.config]
     for key, v in preset.items():
         if getattr(args, key) is None:
             setattr(args, key, v)

@@ -60,6 +60,7 @@ struct kc_ctx {
     bool part = true;
     uint64_t key_cap = 0;          // keys per batch
     uint64_t* keys_a = nullptr;    // W x key_cap
+    uint8_t* digs = nullptr;       // key_cap: P3 digit (word0 >> 56) of keys_a[i], written by P2
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
@@ -407,7 +408,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         if (n > c->key_cap) return fail(c, KC_ERR_INTERNAL, "batch keys %llu exceed capacity", (unsigned long long)n);
 
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48, c->stream));
+        HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48, c->digs,
+                                      c->stream));
         HIPCHK(c, hipEventRecord(c->ev1, c->stream));
         HIPCHK(c, hipEventSynchronize(c->ev1));
         HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -437,7 +439,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             uint64_t* p3t = p3h + 256 * ntiles + scan_tmp_elems(256 * ntiles);
             HIPCHK(c, hipMemcpyAsync(p3t, rt.data(), 2 * 257 * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_p3_hist(W, c->keys_a, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
+            HIPCHK(c, launch_p3_hist(W, c->digs, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
                                      c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
@@ -649,7 +651,7 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
         spill_bytes = M / 64;
         tbytes = cfg->table_bytes ? cfg->table_bytes : M / 16;
         uint64_t rest = M - M / 64 - M / 16;
-        c->key_cap = rest / (16 * (uint64_t)c->W);
+        c->key_cap = rest / (16 * (uint64_t)c->W + 1);  // two key buffers + the P3 digit byte
         if (c->key_cap < 65536) c->key_cap = 65536;
     } else {
         spill_bytes = M / 16;
@@ -667,6 +669,7 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     if (c->part) {
         if (hipMalloc((void**)&c->keys_a, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->keys_b, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
+        if (hipMalloc((void**)&c->digs, (size_t)c->key_cap + 16) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->rec_cursor, 8) != hipSuccess) return bail(KC_ERR_NOMEM);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -692,6 +695,7 @@ void kc_destroy(kc_ctx* c) {
     if (c->spill) (void)hipFree(c->spill);
     if (c->keys_a) (void)hipFree(c->keys_a);
     if (c->keys_b) (void)hipFree(c->keys_b);
+    if (c->digs) (void)hipFree(c->digs);
     if (c->rec_keys) (void)hipFree(c->rec_keys);
     if (c->rec_cnts) (void)hipFree(c->rec_cnts);
     if (c->rec_cursor) (void)hipFree(c->rec_cursor);

@@ -88,12 +88,13 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
 // P2: scatter keys to out (SoA, out_stride) at base = exclusive scan of hist;
 // also counts key 0 / holes / valid windows into l.stats
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
-                               uint64_t out_stride, int shift, hipStream_t s);
+                               uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s);
 // P3 (regional scatter, see kc_kernels.hip): rstart[257] region bounds,
 // tpre[257] tile prefix per region (tiles of p3_tile(W) keys); hist holds
 // 256 * ntiles u64, tmp scan_tmp_elems(256 * ntiles) u64.
 int p3_tile(int W);
-hipError_t launch_p3_hist(int W, const uint64_t* kin, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
+// digs: the P3 digit of every key (written by P2), one byte per key
+hipError_t launch_p3_hist(int W, const uint8_t* digs, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
                           uint64_t* hist, uint64_t* tmp, int grid, hipStream_t s);
 hipError_t launch_p3_scatter(int W, const uint64_t* kin, uint64_t* kout, uint64_t stride, const uint64_t* rstart,
                              const uint64_t* tpre, uint64_t ntiles, const uint64_t* hist, int grid, hipStream_t s);

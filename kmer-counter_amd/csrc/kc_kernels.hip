@@ -275,6 +275,7 @@ struct PartArgs {
     int max_win;      // windows per tile (R * windows per read)
     int scap;         // SCATTER staging capacity (keys, >= max_win)
     int skip;         // timing experiments only (KC_P2_SKIP): 1 flush writes, 2 staging, 4 whole sink
+    unsigned char* digs;  // SCATTER: the P3 digit (word0 >> 56) of each written key
     const u32* codes; // CODES front end: encoded reads (kernel E), G u32 per read
     const unsigned short* inval;  //      not-ACGT masks, G u16 per read
     int G;            //                  16-base groups per read
@@ -703,6 +704,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                                 __builtin_nontemporal_store(v, dst);
                             else
                                 *dst = v;
+                            if (j == 0) pa.digs[g] = (unsigned char)(v >> 56);
                         }
                     }
                     __syncthreads();
@@ -877,7 +879,7 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
 }
 
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
-                               uint64_t out_stride, int shift, hipStream_t s) {
+                               uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s) {
     if (l.n_reads == 0) return hipSuccess;
     const CountGeom& g = pg.geom;
     CountArgs a = make_args(l, g);
@@ -887,6 +889,7 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa = zero_pa;
     pa.base = base;
     pa.out = out;
+    pa.digs = (unsigned char*)digs;
     pa.out_stride = out_stride;
     pa.codes = l.codes;
     pa.inval = (const unsigned short*)l.inval;
@@ -2143,12 +2146,13 @@ __device__ __forceinline__ void p3_tile_range(const u64* __restrict__ rstart, co
     *hi = min(st + (u64)TILE, rstart[a + 1]);
 }
 
-// 256-thread blocks, one private histogram per wave (LDS atomics of a wave
-// only collide with its own lanes), summed at the end of the tile
+// P3 tile histograms from the digit bytes P2 wrote (1 B per key instead of
+// re-reading 8W B keys): 256-thread blocks, one private histogram per wave,
+// 16 digits per thread per load (uint4 of bytes, tile-aligned)
 template <int W>
-__global__ __launch_bounds__(kBlock) void p3_upsweep_k(const u64* __restrict__ keys, const u64* __restrict__ rstart,
-                                                       const u64* __restrict__ tpre, u64 ntiles,
-                                                       u64* __restrict__ hist) {
+__global__ __launch_bounds__(kBlock) void p3_upsweep_k(const unsigned char* __restrict__ digs,
+                                                       const u64* __restrict__ rstart, const u64* __restrict__ tpre,
+                                                       u64 ntiles, u64* __restrict__ hist) {
     constexpr int TILE = P3Cfg<W>::TILE;
     __shared__ u32 h[4 * 256];
     const int tid = threadIdx.x, wave = tid >> 6;
@@ -2158,17 +2162,22 @@ __global__ __launch_bounds__(kBlock) void p3_upsweep_k(const u64* __restrict__ k
         u64 lo, hi;
         p3_tile_range(rstart, tpre, t, TILE, &lo, &hi);
         u32* hw = h + wave * 256;
-        u64 i = lo + tid;
-        for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
-            const u64 k0 = __builtin_nontemporal_load(keys + i), k1 = __builtin_nontemporal_load(keys + i + kBlock),
-                      k2 = __builtin_nontemporal_load(keys + i + 2 * kBlock),
-                      k3 = __builtin_nontemporal_load(keys + i + 3 * kBlock);
-            atomicAdd(&hw[(u32)(k0 >> 56)], 1u);
-            atomicAdd(&hw[(u32)(k1 >> 56)], 1u);
-            atomicAdd(&hw[(u32)(k2 >> 56)], 1u);
-            atomicAdd(&hw[(u32)(k3 >> 56)], 1u);
+        // head up to 16-byte alignment, aligned body, tail
+        const u64 alo = min(hi, (lo + 15) & ~15ull);
+        for (u64 i = lo + tid; i < alo; i += kBlock) atomicAdd(&hw[digs[i]], 1u);
+        const u64 ahi = alo + ((hi - alo) & ~15ull);
+        for (u64 i = alo + 16 * (u64)tid; i < ahi; i += 16 * (u64)kBlock) {
+            const v4u v = __builtin_nontemporal_load((const v4u*)(digs + i));
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const u32 w = c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+                atomicAdd(&hw[w & 255u], 1u);
+                atomicAdd(&hw[(w >> 8) & 255u], 1u);
+                atomicAdd(&hw[(w >> 16) & 255u], 1u);
+                atomicAdd(&hw[w >> 24], 1u);
+            }
         }
-        for (; i < hi; i += kBlock) atomicAdd(&hw[(u32)(keys[i] >> 56)], 1u);
+        for (u64 i = ahi + tid; i < hi; i += kBlock) atomicAdd(&hw[digs[i]], 1u);
         __syncthreads();
         hist[(u64)tid * ntiles + t] = h[tid] + h[256 + tid] + h[512 + tid] + h[768 + tid];
         __syncthreads();
@@ -2279,12 +2288,12 @@ size_t p3_scatter_lds(int W) {
     return (size_t)W * p3_tile(W) * 8 + 16 * 128 * 4 + 16 * 256 * 2 + 256 * 4 + 256 * 8 + 16 * 4 + 16;
 }
 
-hipError_t launch_p3_hist(int W, const uint64_t* kin, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
+hipError_t launch_p3_hist(int W, const uint8_t* digs, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
                           uint64_t* hist, uint64_t* tmp, int grid, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    const int g = (int)hmin(ntiles, (u64)grid);
     const int gu = (int)hmin(ntiles, (u64)grid * 4);
-#define KC_P3U(WW) hipLaunchKernelGGL(p3_upsweep_k<WW>, dim3(gu), dim3(kBlock), 0, s, kin, rstart, tpre, ntiles, hist)
+#define KC_P3U(WW) \
+    hipLaunchKernelGGL(p3_upsweep_k<WW>, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)digs, rstart, tpre, ntiles, hist)
     switch (W) {
     case 1: KC_P3U(1); break;
     case 2: KC_P3U(2); break;

@@ -448,7 +448,7 @@ def test_config5_full_size_properties(kca):
 
     n, L, k = 20_000_000, 150, 55
     dev = torch.device("cuda", 0)
-    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=64 << 30) as ctx:
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=72 << 30) as ctx:
         ptr, nb = ctx.synth_device(n, L, 5, 0, 0.0, 0)
         assert ctx.count_fastq_device(ptr, nb) == n
         ctx.free_device(ptr)
