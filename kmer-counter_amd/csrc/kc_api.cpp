@@ -433,10 +433,9 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             rt[257] = 0;
             for (int r = 0; r < 256; r++) rt[257 + r + 1] = rt[257 + r] + (rt[r + 1] - rt[r] + tile - 1) / tile;
             const uint64_t ntiles = rt[257 + 256];
-            if ((s = ensure(c, c->part_sort_hist, (256 * ntiles + scan_tmp_elems(256 * ntiles) + 2 * 257) * 8)))
-                return s;
+            if ((s = ensure(c, c->part_sort_hist, (256 * ntiles + p3_tmp_elems(ntiles) + 2 * 257) * 8))) return s;
             uint64_t* p3h = (uint64_t*)c->part_sort_hist.p;
-            uint64_t* p3t = p3h + 256 * ntiles + scan_tmp_elems(256 * ntiles);
+            uint64_t* p3t = p3h + 256 * ntiles + p3_tmp_elems(ntiles);
             HIPCHK(c, hipMemcpyAsync(p3t, rt.data(), 2 * 257 * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
             HIPCHK(c, launch_p3_hist(W, c->digs, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,

@@ -93,9 +93,11 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
 // tpre[257] tile prefix per region (tiles of p3_tile(W) keys); hist holds
 // 256 * ntiles u64, tmp scan_tmp_elems(256 * ntiles) u64.
 int p3_tile(int W);
-// digs: the P3 digit of every key (written by P2), one byte per key
+// digs: the P3 digit of every key (written by P2), one byte per key; pos:
+// 256 * ntiles u64 (tile-major run starts); tmp: p3_tmp_elems(ntiles) u64
 hipError_t launch_p3_hist(int W, const uint8_t* digs, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
-                          uint64_t* hist, uint64_t* tmp, int grid, hipStream_t s);
+                          uint64_t* pos, uint64_t* tmp, int grid, hipStream_t s);
+uint64_t p3_tmp_elems(uint64_t ntiles);
 hipError_t launch_p3_scatter(int W, const uint64_t* kin, uint64_t* kout, uint64_t stride, const uint64_t* rstart,
                              const uint64_t* tpre, uint64_t ntiles, const uint64_t* hist, int grid, hipStream_t s);
 // P4: starts[b] for b in [0, 2^bits]: first key index of bucket b (= hash >> (64 - bits))

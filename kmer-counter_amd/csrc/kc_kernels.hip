@@ -2152,7 +2152,7 @@ __device__ __forceinline__ void p3_tile_range(const u64* __restrict__ rstart, co
 template <int W>
 __global__ __launch_bounds__(kBlock) void p3_upsweep_k(const unsigned char* __restrict__ digs,
                                                        const u64* __restrict__ rstart, const u64* __restrict__ tpre,
-                                                       u64 ntiles, u64* __restrict__ hist) {
+                                                       u64 ntiles, u32* __restrict__ cnt_t) {
     constexpr int TILE = P3Cfg<W>::TILE;
     __shared__ u32 h[4 * 256];
     const int tid = threadIdx.x, wave = tid >> 6;
@@ -2179,8 +2179,72 @@ __global__ __launch_bounds__(kBlock) void p3_upsweep_k(const unsigned char* __re
         }
         for (u64 i = ahi + tid; i < hi; i += kBlock) atomicAdd(&hw[digs[i]], 1u);
         __syncthreads();
-        hist[(u64)tid * ntiles + t] = h[tid] + h[256 + tid] + h[512 + tid] + h[768 + tid];
+        cnt_t[t * 256 + tid] = h[tid] + h[256 + tid] + h[512 + tid] + h[768 + tid];  // tile-major, coalesced
         __syncthreads();
+    }
+}
+
+// Positions from the tile-major counts, digit-major order: pos[t][d] =
+// sum_{d' < d} total(d') + sum_{t' < t} cnt[t'][d], in three streaming kernels
+// over chunks of kP3Chunk tiles (rows of 256 counts are read coalesced).
+constexpr int kP3Chunk = 64;
+
+__global__ __launch_bounds__(256) void p3_chunk_sum_k(const u32* __restrict__ cnt_t, u64 ntiles, u64* __restrict__ csum) {
+    const u64 c = blockIdx.x;
+    const u64 t0 = c * kP3Chunk, t1 = min(ntiles, t0 + kP3Chunk);
+    u64 sum = 0;
+    for (u64 t = t0; t < t1; t++) sum += cnt_t[t * 256 + threadIdx.x];
+    csum[c * 256 + threadIdx.x] = sum;
+}
+
+// one block per digit: exclusive scan of that digit's chunk sums (each thread
+// a run of consecutive chunks); the digit total goes to dtot[d]
+__global__ __launch_bounds__(256) void p3_chunk_scan_k(u64* __restrict__ csum, u64 nchunks, u64* __restrict__ dtot) {
+    __shared__ u64 part[256];
+    const int d = blockIdx.x, t = threadIdx.x;
+    const u64 per = (nchunks + 255) / 256;
+    const u64 c0 = min(nchunks, (u64)t * per), c1 = min(nchunks, c0 + per);
+    u64 sum = 0;
+    for (u64 c = c0; c < c1; c++) sum += csum[c * 256 + d];
+    part[t] = sum;
+    __syncthreads();
+    if (t == 0) {
+        u64 acc = 0;
+        for (int i = 0; i < 256; i++) {
+            const u64 v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+        dtot[d] = acc;
+    }
+    __syncthreads();
+    u64 run = part[t];
+    for (u64 c = c0; c < c1; c++) {
+        const u64 v = csum[c * 256 + d];
+        csum[c * 256 + d] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(256) void p3_digit_base_k(u64* __restrict__ dtot) {
+    if (threadIdx.x == 0) {
+        u64 acc = 0;
+        for (int i = 0; i < 256; i++) {
+            const u64 v = dtot[i];
+            dtot[i] = acc;
+            acc += v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void p3_chunk_pos_k(const u32* __restrict__ cnt_t, const u64* __restrict__ csum,
+                                                      const u64* __restrict__ dbase, u64 ntiles, u64* __restrict__ pos) {
+    const u64 c = blockIdx.x;
+    const u64 t0 = c * kP3Chunk, t1 = min(ntiles, t0 + kP3Chunk);
+    u64 run = dbase[threadIdx.x] + csum[c * 256 + threadIdx.x];
+    for (u64 t = t0; t < t1; t++) {
+        pos[t * 256 + threadIdx.x] = run;
+        run += cnt_t[t * 256 + threadIdx.x];
     }
 }
 
@@ -2221,7 +2285,7 @@ __global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__
 #pragma unroll
             for (int j = 0; j < W; j++) key[i][j] = nk[i][j];
         for (int i = tid; i < 16 * 128; i += kP3Block) wc[i] = 0;
-        if (tid < 256) gpos[tid] = pos[(u64)tid * ntiles + t];
+        if (tid < 256) gpos[tid] = pos[t * 256 + tid];
         __syncthreads();
         load(t + gridDim.x);  // next tile's keys fly while this one is ranked
         // ranks inside the wave's own counters (atomics only collide within
@@ -2289,11 +2353,15 @@ size_t p3_scatter_lds(int W) {
 }
 
 hipError_t launch_p3_hist(int W, const uint8_t* digs, const uint64_t* rstart, const uint64_t* tpre, uint64_t ntiles,
-                          uint64_t* hist, uint64_t* tmp, int grid, hipStream_t s) {
+                          uint64_t* pos, uint64_t* tmp, int grid, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
+    // tmp: ntiles x 256 u32 tile counts + p3_chunks(ntiles) x 256 u64 chunk sums
+    u32* cnt_t = (u32*)tmp;
+    u64* csum = tmp + (ntiles * 256 + 1) / 2;
+    const u64 nchunks = (ntiles + kP3Chunk - 1) / kP3Chunk;
     const int gu = (int)hmin(ntiles, (u64)grid * 4);
 #define KC_P3U(WW) \
-    hipLaunchKernelGGL(p3_upsweep_k<WW>, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)digs, rstart, tpre, ntiles, hist)
+    hipLaunchKernelGGL(p3_upsweep_k<WW>, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)digs, rstart, tpre, ntiles, cnt_t)
     switch (W) {
     case 1: KC_P3U(1); break;
     case 2: KC_P3U(2); break;
@@ -2302,7 +2370,17 @@ hipError_t launch_p3_hist(int W, const uint8_t* digs, const uint64_t* rstart, co
     default: return hipErrorInvalidValue;
     }
 #undef KC_P3U
-    return scan_impl<u64>(hist, hist, (u64)256 * ntiles, tmp, s);
+    u64* dtot = csum + nchunks * 256;
+    hipLaunchKernelGGL(p3_chunk_sum_k, dim3(nchunks), dim3(256), 0, s, (const u32*)cnt_t, ntiles, csum);
+    hipLaunchKernelGGL(p3_chunk_scan_k, dim3(256), dim3(256), 0, s, csum, nchunks, dtot);
+    hipLaunchKernelGGL(p3_digit_base_k, dim3(1), dim3(256), 0, s, dtot);
+    hipLaunchKernelGGL(p3_chunk_pos_k, dim3(nchunks), dim3(256), 0, s, (const u32*)cnt_t, (const u64*)csum,
+                       (const u64*)dtot, ntiles, pos);
+    return hipGetLastError();
+}
+
+uint64_t p3_tmp_elems(uint64_t ntiles) {
+    return (ntiles * 256 + 1) / 2 + ((ntiles + kP3Chunk - 1) / kP3Chunk) * 256 + 256 + 8;
 }
 
 hipError_t launch_p3_scatter(int W, const uint64_t* kin, uint64_t* kout, uint64_t stride, const uint64_t* rstart,
