@@ -126,14 +126,14 @@ struct CountArgs {
 
 // Reads per tile that keep the kRoll-window chunks of a tile close to a whole
 // number of 256-lane rounds (R_max bounds R).
-static int balance_reads(int R_max, int nw) {
+static int balance_reads(int R_max, int nw, int nt = kBlock) {
     const int nchr = (nw + 7) / 8;
     int best = R_max;
     double best_eff = 0;
     for (int R = R_max; R >= 1 && R >= R_max / 2; R--) {
         int ch = R * nchr;
-        int rounds = (ch + kBlock - 1) / kBlock;
-        double eff = (double)ch / (rounds * kBlock);
+        int rounds = (ch + nt - 1) / nt;
+        double eff = (double)ch / (rounds * nt);
         if (eff > best_eff + 1e-9) {
             best_eff = eff;
             best = R;
@@ -284,8 +284,7 @@ struct PartArgs {
 static size_t sink_lds_host(int W, int sink, int scap) {
     if (sink == SINK_HIST) return 256 * 4;
     if (sink == SINK_SCATTER)
-        return 256 * 8 + 3 * 256 * 4 + 16 + 32 + (size_t)W * 8 * (scap + 1) + (((size_t)scap + 1 + 15) & ~(size_t)15) +
-               2 * (size_t)scap;
+        return 2 * 256 * 8 + 260 * 4 + 256 * 4 + 32 + (size_t)W * 8 * (scap + 1) + 2 * (size_t)scap + 16;
     return 0;
 }
 
@@ -299,10 +298,34 @@ __device__ __forceinline__ u64 code_word(const u32* cr, int b) {
     return o ? ((hi << (2 * o)) | (u64)(cr[g + 2] >> (32 - 2 * o))) : hi;
 }
 
+// Exclusive scan of 256 per-digit values held by threads 0..255 of a block of
+// any size (waves 0..3 scan, one barrier that every thread executes).
+// scratch: >= 4 u32. Threads >= 256 get 0.
+__device__ __forceinline__ u32 digit_scan256(u32 v, u32* scratch, int tid) {
+    const int lane = lane_id(), wave = tid >> 6;
+    u32 inc = v;
+    if (tid < 256) {
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) scratch[wave] = inc;
+    }
+    __syncthreads();
+    u32 pre = 0;
+    if (tid < 256)
+        for (int w = 0; w < wave; w++) pre += scratch[w];
+    return tid < 256 ? pre + inc - v : 0u;
+}
+
 constexpr int kPrefetch = 4;  // code words prefetched per thread (CODES front end)
 
-template <int W, int SINK, bool CODES>
-__global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) {
+// NT threads per workgroup (256, or 1024 for the P2 scatter: 16 waves per CU
+// with twice the staging capacity); per-digit arrays are handled by the first
+// 256 threads.
+template <int W, int SINK, bool CODES, int NT>
+__global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* raw = smem;
     u32* codes = (u32*)(smem + (size_t)a.R * a.raw_stride);
@@ -316,13 +339,13 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
     unsigned char* sk = smem + sk_off;
     u32* s_hist = (u32*)sk;                      // HIST
     u64* s_cur = (u64*)sk;                       // SCATTER: global cursor of each digit's run
-    u32* s_cnt = (u32*)(s_cur + 256);            //          staged keys per digit (+ trash counter 256)
-    u32* s_start = s_cnt + 256 + 4;              //          digit start in the flush order
-    u32* s_fill = s_start + 256;                 //          rank cursor
+    u64* s_gb = s_cur + 256;                     //          flush: s_cur[d] - start of d in flush order
+    u32* s_cnt = (u32*)(s_gb + 256);             //          staged keys per digit (+ trash counter 256)
+    u32* s_fill = s_cnt + 256 + 4;               //          rank cursor
     u32* s_misc = s_fill + 256;                  //          [0] staged count, [4..7] scan scratch
-    u64* s_stage = (u64*)(s_misc + 8);           //          W x (scap + 1) staged keys (slot scap: trash)
-    unsigned char* s_dig = (unsigned char*)(s_stage + (size_t)W * (pa.scap + 1));  // scap + 1 digits
-    unsigned short* s_perm = (unsigned short*)(s_dig + ((pa.scap + 1 + 15) & ~15)); // scap flush order
+    u64* s_stage = (u64*)(s_misc + 8);           //          W x (scap + 1) staged keys (slot scap: trash);
+                                                 //          the digit is recomputed from word 0
+    unsigned short* s_perm = (unsigned short*)(s_stage + (size_t)W * (pa.scap + 1));  // scap flush order
     u32* scan_tmp = s_misc + 4;
 
     const int tid = threadIdx.x;
@@ -347,7 +370,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
         const int nr = (tile < ntiles) ? (int)min((u64)a.R, a.n_reads - r0) : 0;
 #pragma unroll
         for (int j = 0; j < kPrefetch; j++) {
-            const int it = tid + j * kBlock;
+            const int it = tid + j * NT;
             const int r = it / NG, g = it - r * NG;
             u32 cw = 0, iv = 0;
             if (r < nr && g < pa.G) {
@@ -363,10 +386,12 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
 
     for (u64 unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
         if constexpr (SINK == SINK_HIST) {
-            s_hist[tid] = 0;
+            if (tid < 256) s_hist[tid] = 0;
         } else if constexpr (SINK == SINK_SCATTER) {
-            s_cnt[tid] = 0;
-            s_cur[tid] = pa.base[(u64)tid * pa.nseg + unit];
+            if (tid < 256) {
+                s_cnt[tid] = 0;
+                s_cur[tid] = pa.base[(u64)tid * pa.nseg + unit];
+            }
             if (tid == 0) s_misc[0] = 0;
         }
         const u64 t_end = min(ntiles, (unit + 1) * per_unit);
@@ -379,13 +404,13 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                 //      the read end are zero (A, valid), as the encoder leaves them
 #pragma unroll
                 for (int j = 0; j < kPrefetch; j++) {
-                    const int it = tid + j * kBlock;
+                    const int it = tid + j * NT;
                     if (it < nr * NG) {
                         codes[it] = pf_code[j];
                         inval[it] = pf_inv[j];
                     }
                 }
-                for (int it = tid + kPrefetch * kBlock; it < nr * NG; it += kBlock) {
+                for (int it = tid + kPrefetch * NT; it < nr * NG; it += NT) {
                     const int r = it / NG, g = it - r * NG;
                     u32 cw = 0, iv = 0;
                     if (g < pa.G) {
@@ -400,12 +425,12 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                 __syncthreads();
                 // issue the next tile's loads now; they land during this tile
                 prefetch(tile + 1 < t_end ? tile + 1 : (unit + gridDim.x) * per_unit);
-                for (int it = tid; it < nr * NG; it += kBlock)
+                for (int it = tid; it < nr * NG; it += NT)
                     if (inval[it]) atomicOr(&rflag[it / NG], 1u);
                 __syncthreads();
             } else {
             // 1. stage the raw text of the tile's reads into LDS
-            for (int it = tid; it < nr * nch; it += kBlock) {
+            for (int it = tid; it < nr * nch; it += NT) {
                 int r = it / nch, c = it - r * nch;
                 u64 gr = a.read0 + r0 + (u64)r;
                 u64 off = a.seq_off ? a.seq_off[gr] : gr * (u64)L;
@@ -423,7 +448,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
             __syncthreads();
 
             // 2. encode 16-base groups
-            for (int it = tid; it < nr * NG; it += kBlock) {
+            for (int it = tid; it < nr * NG; it += NT) {
                 int r = it / NG, g = it - r * NG;
                 int i0 = 16 * g;
                 u32 cw = 0, iv = 0;
@@ -467,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                 // slot in it is its rank among the step's live lanes, so
                 // consecutive lanes write consecutive slots. B: roll again and
                 // stage. No LDS round trip inside a step.
-                for (int c = tid; c - (tid & 63) < total; c += kBlock) {
+                for (int c = tid; c - (tid & 63) < total; c += NT) {
                     const bool cact = c < total;
                     int r = 0, p0 = 0;
                     u64 raw[W];
@@ -551,7 +576,6 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                         const u32 d = (u32)(key[0] >> pa.shift) & 255u;
 #pragma unroll
                         for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
-                        s_dig[idx] = (unsigned char)d;
                         atomicAdd(&s_cnt[lv ? d : 256u], 1u);
 #pragma unroll
                         for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
@@ -560,7 +584,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                     }
                 }
             } else {
-                for (int c = tid; c - (tid & 63) < total; c += kBlock) {
+                for (int c = tid; c - (tid & 63) < total; c += NT) {
                     // the loop bound is wave-uniform so every lane reaches the ballots
                     const bool cact = c < total;
                     int r = 0, p0 = 0;
@@ -615,24 +639,6 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                             }
                             if (valid) my_valid++;
                         }
-                        if constexpr (SINK == SINK_SCATTER) {
-                            // stage the key (wave-aggregated LDS reservation)
-                            u64 m = __ballot(live);
-                            u32 base = 0;
-                            if (m) {
-                                int leader = __ffsll((long long)m) - 1;
-                                if ((int)lane_id() == leader) base = atomicAdd(&s_misc[0], (u32)__popcll(m));
-                                base = __shfl(base, leader);
-                            }
-                            if (live) {
-                                u32 idx = base + (u32)__popcll(m & lanemask_lt());
-                                const u32 d = (u32)(key[0] >> pa.shift) & 255u;
-        #pragma unroll
-                                for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
-                                s_dig[idx] = (unsigned char)d;
-                                atomicAdd(&s_cnt[d], 1u);
-                            }
-                        }
                         if constexpr (SINK == SINK_TABLE) {
                             bool done = true, claimed = false;
                             if (live) {
@@ -674,42 +680,33 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
                 // each digit's run with consecutive lanes
                 const u32 n = s_misc[0];
                 if (tile + 1 == t_end || n + (u32)pa.max_win > (u32)pa.scap) {
-                    u32 tot;
-                    u32 st = block_excl_scan(s_cnt[tid], scan_tmp, &tot);
-                    s_start[tid] = st;
-                    s_fill[tid] = st;
+                    const u32 st = digit_scan256(tid < 256 ? s_cnt[tid] : 0u, scan_tmp, tid);
+                    if (tid < 256) {
+                        s_fill[tid] = st;
+                        s_gb[tid] = s_cur[tid] - st;
+                    }
                     __syncthreads();
-                    for (u32 i = tid; i < n; i += kBlock) {
-                        u32 q = atomicAdd(&s_fill[s_dig[i]], 1u);
+                    for (u32 i = tid; i < n; i += NT) {
+                        u32 q = atomicAdd(&s_fill[(u32)(s_stage[i] >> pa.shift) & 255u], 1u);
                         s_perm[q] = (unsigned short)i;
                     }
                     __syncthreads();
-                    for (u32 q = tid; q < n; q += kBlock) {
+                    for (u32 q = tid; q < n; q += NT) {
                         const u32 i = s_perm[q];
-                        const u32 d = s_dig[i];
-                        const u64 c0 = s_cur[d];
-                        const u64 g = c0 + (q - s_start[d]);
+                        const u64 k0 = s_stage[i];
+                        const u64 g = s_gb[(u32)(k0 >> pa.shift) & 255u] + q;
                         if (pa.skip & 1) continue;
-                        // a 64-byte sector this run covers whole is streamed out
-                        // (non-temporal); the partial sectors at the run's ends
-                        // stay in L2 so the next flush of this digit completes
-                        // them before they are written back
-                        const u64 sec = g & ~7ull;
-                        const bool whole = sec >= c0 && sec + 8 <= c0 + s_cnt[d];
+                        pa.out[g] = k0;
 #pragma unroll
-                        for (int j = 0; j < W; j++) {
-                            const u64 v = s_stage[(size_t)j * (pa.scap + 1) + i];
-                            u64* dst = pa.out + (u64)j * pa.out_stride + g;
-                            if (whole)
-                                __builtin_nontemporal_store(v, dst);
-                            else
-                                *dst = v;
-                            if (j == 0) pa.digs[g] = (unsigned char)(v >> 56);
-                        }
+                        for (int j = 1; j < W; j++)
+                            pa.out[(u64)j * pa.out_stride + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
+                        pa.digs[g] = (unsigned char)(k0 >> 56);
                     }
                     __syncthreads();
-                    s_cur[tid] += s_cnt[tid];
-                    s_cnt[tid] = 0;
+                    if (tid < 256) {
+                        s_cur[tid] += s_cnt[tid];
+                        s_cnt[tid] = 0;
+                    }
                     if (tid == 0) s_misc[0] = 0;
                     __syncthreads();
                 }
@@ -717,7 +714,7 @@ __global__ __launch_bounds__(kBlock) void count_front(CountArgs a, PartArgs pa) 
         }
         if constexpr (SINK == SINK_HIST) {
             __syncthreads();
-            pa.hist[(u64)tid * pa.nseg + unit] = s_hist[tid];
+            if (tid < 256) pa.hist[(u64)tid * pa.nseg + unit] = s_hist[tid];
             __syncthreads();
         }
     }
@@ -747,12 +744,12 @@ static CountArgs make_args(const CountLaunch& l, const CountGeom& g) {
     return a;
 }
 
-#define KC_FRONT_SWITCH(SINKV, CODESV, GRID, LDS, S, A, PA)                                                          \
+#define KC_FRONT_SWITCH(SINKV, CODESV, NTV, GRID, LDS, S, A, PA)                                                     \
     switch (W) {                                                                                                     \
-    case 1: hipLaunchKernelGGL((count_front<1, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
-    case 2: hipLaunchKernelGGL((count_front<2, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
-    case 3: hipLaunchKernelGGL((count_front<3, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
-    case 4: hipLaunchKernelGGL((count_front<4, SINKV, CODESV>), dim3(GRID), dim3(kBlock), LDS, S, A, PA); break;     \
+    case 1: hipLaunchKernelGGL((count_front<1, SINKV, CODESV, NTV>), dim3(GRID), dim3(NTV), LDS, S, A, PA); break;   \
+    case 2: hipLaunchKernelGGL((count_front<2, SINKV, CODESV, NTV>), dim3(GRID), dim3(NTV), LDS, S, A, PA); break;   \
+    case 3: hipLaunchKernelGGL((count_front<3, SINKV, CODESV, NTV>), dim3(GRID), dim3(NTV), LDS, S, A, PA); break;   \
+    case 4: hipLaunchKernelGGL((count_front<4, SINKV, CODESV, NTV>), dim3(GRID), dim3(NTV), LDS, S, A, PA); break;   \
     default: return hipErrorInvalidValue;                                                                            \
     }
 
@@ -766,7 +763,7 @@ hipError_t launch_count_kmers(const CountLaunch& l, int grid_cap, hipStream_t s)
     u64 tiles = (l.n_reads + g.R - 1) / g.R;
     int grid = (int)hmin(tiles, (u64)grid_cap);
     int W = (l.k + 31) / 32;
-    KC_FRONT_SWITCH(SINK_TABLE, false, grid, g.lds, s, a, pa)
+    KC_FRONT_SWITCH(SINK_TABLE, false, kBlock, grid, g.lds, s, a, pa)
     return hipGetLastError();
 }
 
@@ -816,14 +813,20 @@ hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* 
     return hipGetLastError();
 }
 
-// LDS of one P2 workgroup; two workgroups per CU
-constexpr size_t kPartLds = 76 * 1024;
+// P2 workgroup: kP2Block threads, one per CU, most of the CU's LDS for staging
+constexpr int kP2Block = 1024;
+constexpr size_t kPartLds = 150 * 1024;
 
 PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     PartGeom p;
     CountGeom g = count_geometry(L, k);
     g.raw_stride = 0;  // CODES front end: no raw text in LDS
-    g.R = 64;
+    // aim for two rounds of 8-window runs per P2 thread; the P1 workgroup
+    // (256 threads) walks the same tiles in more rounds
+    const int nw0 = L - k + 1;
+    g.R = (2 * kP2Block * 8 + nw0 - 1) / (nw0 > 0 ? nw0 : 1);
+    if (g.R > 256) g.R = 256;
+    if (g.R < 1) g.R = 1;
     while (g.R > 1 && g.R * g.NG > kPrefetch * kBlock) g.R--;
     // P1 and P2 share this tile geometry. P2 stages keys over several tiles
     // (scap >= 2 tiles where possible) before writing them in digit order, so
@@ -834,9 +837,9 @@ PartGeom part_geometry(int L, int k, uint64_t n_reads) {
         size_t f = (size_t)r * g.raw_stride + (size_t)r * g.NG * 8 + (size_t)r * 8 + 16;
         return ((f + 15) & ~(size_t)15) + 16;
     };
-    const size_t per_key = (size_t)W * 8 + 1 + 2 + 1;
+    const size_t per_key = (size_t)W * 8 + 2;  // staged key words + u16 permutation entry
     while (g.R > 1 && front(g.R) + sink_lds_host(W, SINK_SCATTER, 2 * g.R * nw) > kPartLds) g.R--;
-    g.R = balance_reads(g.R, nw);
+    g.R = balance_reads(g.R, nw, kP2Block);
     size_t room = kPartLds > front(g.R) + 4096 ? kPartLds - front(g.R) - 4096 : 0;
     int scap = (int)(room / per_key);
     if (scap > 65535) scap = 65535;  // u16 permutation indices
@@ -874,7 +877,7 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
     pa.scap = pg.scap;
     size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_HIST, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
-    KC_FRONT_SWITCH(SINK_HIST, true, grid, lds, s, a, pa)
+    KC_FRONT_SWITCH(SINK_HIST, true, kBlock, grid, lds, s, a, pa)
     return hipGetLastError();
 }
 
@@ -906,7 +909,7 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     }
     size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
-    KC_FRONT_SWITCH(SINK_SCATTER, true, grid, lds, s, a, pa)
+    KC_FRONT_SWITCH(SINK_SCATTER, true, kP2Block, grid, lds, s, a, pa)
     return hipGetLastError();
 }
 
@@ -1846,7 +1849,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     }
                 }
             };
-            constexpr int U = 4;  // independent key loads in flight per thread
+            constexpr int U = (W == 1) ? 8 : 4;  // independent key loads in flight per thread
             // software pipeline: the next iteration's keys are loaded before
             // this iteration's inserts, so HBM latency overlaps LDS work
             u64 nkey[U][W];
