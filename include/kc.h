@@ -203,6 +203,11 @@ kc_status kc_owner_counts(kc_ctx* ctx, uint32_t world, uint64_t* counts);
  * stays finished; kc_reset starts a new count. KC_ERR_STATE before kc_finish
  * or when spill runs exist. */
 kc_status kc_merge_records_device(kc_ctx* ctx, const void* d_packed, uint64_t n_records);
+/* As kc_merge_records_device when the records are nruns runs laid out one
+ * after another, each sorted by key (what an all-to-all of sorted runs
+ * delivers): merged pairwise by merge path instead of re-sorted.
+ * run_counts: host array of nruns record counts. */
+kc_status kc_merge_runs_device(kc_ctx* ctx, const void* d_packed, const uint64_t* run_counts, uint32_t nruns);
 /* The same exchange between n contexts of one process (the CLI's gpus=N
  * exchange=alltoall): context o ends up owning owner_of == o, so writing the
  * contexts' runs one after another in order is the whole SortedKMerFile.

@@ -141,6 +141,7 @@ def lib() -> ctypes.CDLL:
         "kc_merge_records_device": ([vp, vp, u64], ctypes.c_int),
         "kc_copy_device": ([vp, vp, vp, u64], ctypes.c_int),
         "kc_exchange_contexts": ([P(vp), u32], ctypes.c_int),
+        "kc_merge_runs_device": ([vp, vp, P(u64), u32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -311,6 +312,20 @@ class Context:
         self._chk(self._L.kc_merge_records_device(self._h, ctypes.c_void_p(src.data_ptr()), n_records))
         return self.finish()
 
+    def merge_runs(self, src, run_counts) -> int:
+        """Like merge_records when `src` holds len(run_counts) sorted runs one
+        after another (kc_merge_runs_device: pairwise merge path)."""
+        n = int(sum(run_counts))
+        if n * self.rs > src.numel():
+            raise ValueError("source too small")
+        if not src.is_cuda:
+            import torch
+
+            src = src.to(torch.device("cuda", self._device))
+        arr = (ctypes.c_uint64 * max(1, len(run_counts)))(*[int(x) for x in run_counts])
+        self._chk(self._L.kc_merge_runs_device(self._h, ctypes.c_void_p(src.data_ptr()), arr, len(run_counts)))
+        return self.finish()
+
     def write_output(self, path: str, fan_in: int = 2, threads: int = 2):
         self.finish()
         self._chk(self._L.kc_write_output(self._h, path.encode(), fan_in, threads))
@@ -384,6 +399,9 @@ def keyspace_exchange(run, dist, device) -> int:
     if recv.is_cuda:
         torch.cuda.current_stream(recv.device).synchronize()  # RCCL ran on torch's stream
     del send
+    # what arrived is one sorted slice per source rank, in rank order
+    if hasattr(run, "merge_runs"):
+        return run.merge_runs(recv, rcounts)
     return run.merge_records(recv, m)
 
 

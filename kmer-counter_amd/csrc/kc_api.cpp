@@ -348,6 +348,7 @@ static kc_status grow_records(kc_ctx* c, uint64_t need) {
 }
 
 static const int kBucketBits = 16;
+static const size_t kMaxLds = 160 * 1024;  // LDS of one CU (gfx950): the P2 workgroup's ceiling
 static const uint64_t kDescCap = 1u << 20;  // P5 segment descriptors kept for the sorted finish
 
 // Engine "partition": per batch of reads
@@ -533,7 +534,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
 static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
-    if (c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= 150 * 1024)
+    if (c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= kMaxLds)
         return count_reads_part(c, base, seq_off, n_reads, L);
     return count_reads_table(c, base, seq_off, n_reads, L);
 }
@@ -906,16 +907,25 @@ static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
     return sort_reduce_pack(c, out_cap, n, c->batches > 1 || t > 0, n_out);
 }
 
+static kc_status reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, int which, bool dups, uint64_t* n_out);
+
 // fin_keys[0]/fin_cnts[0] hold n records at stride out_cap: radix sort, sum
 // equal keys when `dups` may exist, pack into fin_packed.
 static kc_status sort_reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, bool dups, uint64_t* n_out) {
     kc_status s;
-    const int W = c->W;
     uint64_t* k0 = (uint64_t*)c->fin_keys[0].p;
     uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
     int which = 0;
     if ((s = sort_records(c, k0, (uint64_t*)c->fin_keys[1].p, c0, (uint32_t*)c->fin_cnts[1].p, out_cap, n, &which)))
         return s;
+    return reduce_pack(c, out_cap, n, which, dups, n_out);
+}
+
+// fin_keys[which]/fin_cnts[which] hold n sorted records (equal keys adjacent):
+// sum equal keys (segmented reduce) when `dups`, pack into fin_packed.
+static kc_status reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, int which, bool dups, uint64_t* n_out) {
+    kc_status s;
+    const int W = c->W;
     if (dups && n > 1) {
         uint64_t* ks = (uint64_t*)c->fin_keys[which].p;
         uint32_t* cs = (uint32_t*)c->fin_cnts[which].p;
@@ -1236,6 +1246,69 @@ kc_status kc_merge_records_device(kc_ctx* c, const void* d_packed, uint64_t n_re
     return KC_OK;
 }
 
+kc_status kc_merge_runs_device(kc_ctx* c, const void* d_packed, const uint64_t* run_counts, uint32_t nruns) {
+    if (!c || (nruns && !run_counts)) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist");
+    std::vector<uint64_t> off(nruns + 1, 0);
+    for (uint32_t r = 0; r < nruns; r++) off[r + 1] = off[r] + run_counts[r];
+    const uint64_t n = off[nruns];
+    if (n && !d_packed) return KC_ERR_ARG;
+    kc_status s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    const uint64_t out_cap = n + 1;
+    const int W = c->W;
+    for (int i = 0; i < 2; i++) {
+        if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
+            return s;
+    }
+    if ((s = ensure(c, c->fin_misc, merge_split_elems(n) * 8 + 64))) return s;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_unpack(W, d_packed, n, (uint64_t*)c->fin_keys[0].p, out_cap, (uint32_t*)c->fin_cnts[0].p,
+                            c->stream));
+    // pairwise merge levels: runs 2i and 2i+1 are adjacent, so their merge
+    // occupies the same range of the other buffer
+    int which = 0;
+    std::vector<uint64_t> ro = off;
+    while (ro.size() > 2) {
+        std::vector<uint64_t> nro;
+        const uint64_t* ks = (const uint64_t*)c->fin_keys[which].p;
+        const uint32_t* cs = (const uint32_t*)c->fin_cnts[which].p;
+        uint64_t* kd = (uint64_t*)c->fin_keys[which ^ 1].p;
+        uint32_t* cd = (uint32_t*)c->fin_cnts[which ^ 1].p;
+        const size_t nr = ro.size() - 1;
+        for (size_t r = 0; r < nr; r += 2) {
+            nro.push_back(ro[r]);
+            if (r + 1 < nr) {
+                const uint64_t a0 = ro[r], na = ro[r + 1] - ro[r], nb = ro[r + 2] - ro[r + 1];
+                // the merge kernels take base pointers: offset the SoA columns
+                HIPCHK(c, launch_merge(W, ks + a0, cs + a0, out_cap, na, ks + a0 + na, cs + a0 + na, out_cap, nb,
+                                       kd + a0, cd + a0, out_cap, (uint64_t*)c->fin_misc.p, c->stream));
+            } else {
+                const uint64_t a0 = ro[r], na = ro[r + 1] - ro[r];
+                for (int j = 0; j < W; j++)
+                    HIPCHK(c, hipMemcpyAsync(kd + (size_t)j * out_cap + a0, ks + (size_t)j * out_cap + a0, na * 8,
+                                             hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(cd + a0, cs + a0, na * 4, hipMemcpyDeviceToDevice, c->stream));
+            }
+        }
+        nro.push_back(ro.back());
+        ro.swap(nro);
+        which ^= 1;
+    }
+    uint64_t nout = 0;
+    if ((s = reduce_pack(c, out_cap, n, which, true, &nout))) return s;
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    c->st.finish_ms += t;
+    c->n_records = nout;
+    c->st.output_records = nout;
+    c->finished = true;
+    return KC_OK;
+}
+
 kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n) {
     if (!ctxs || n == 0) return KC_ERR_ARG;
     for (uint32_t r = 0; r < n; r++) {
@@ -1289,7 +1362,10 @@ kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n) {
         }
     }
     for (uint32_t o = 0; o < n; o++) {
-        if ((s = kc_merge_records_device(ctxs[o], recv[o], m[o]))) {
+        // owner o received one sorted slice from every context, in order
+        std::vector<uint64_t> rc(n);
+        for (uint32_t r = 0; r < n; r++) rc[r] = cnt[r][o];
+        if ((s = kc_merge_runs_device(ctxs[o], recv[o], rc.data(), n))) {
             release();
             return s;
         }

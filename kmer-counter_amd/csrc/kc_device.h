@@ -172,6 +172,12 @@ hipError_t launch_pack(int W, const uint64_t* keys, uint64_t stride, const uint3
 // (o in [0, world]); unpack packed records into SoA.
 hipError_t launch_owner_bounds(const void* packed, int rs, uint64_t n, uint32_t world, uint64_t* bounds,
                                hipStream_t s);
+// Merge path of two sorted SoA runs (A first on equal keys) into ko/co
+// (stride so); split: merge_split_elems(na + nb) u64 scratch.
+hipError_t launch_merge(int W, const uint64_t* ka, const uint32_t* ca, uint64_t sa, uint64_t na, const uint64_t* kb,
+                        const uint32_t* cb, uint64_t sb, uint64_t nb, uint64_t* ko, uint32_t* co, uint64_t so,
+                        uint64_t* split, hipStream_t s);
+uint64_t merge_split_elems(uint64_t n);
 hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, uint64_t stride, uint32_t* cnts,
                          hipStream_t s);
 

@@ -815,7 +815,7 @@ hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* 
 
 // P2 workgroup: kP2Block threads, one per CU, most of the CU's LDS for staging
 constexpr int kP2Block = 1024;
-constexpr size_t kPartLds = 150 * 1024;
+constexpr size_t kPartLds = 152 * 1024;  // + alignment and the sink's fixed arrays stays under 160 KiB
 
 PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     PartGeom p;
@@ -853,7 +853,7 @@ PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     p.nseg = (tiles + seg_tiles - 1) / seg_tiles;
     p.max_win = g.R * nw;
     p.scap = scap;
-    p.lds_scatter = front(g.R) + sink_lds_host(W, SINK_SCATTER, scap);
+    p.lds_scatter = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, scap);  // as launched
     return p;
 }
 
@@ -2825,6 +2825,131 @@ __global__ __launch_bounds__(kBlock) void unpack_records_k(const u32* __restrict
         cnts[i] = r[2 * W];
     }
 }
+
+// ---------------------------------------------------------------------------
+// Merge path: two sorted SoA record runs A, B -> one sorted run (A first on
+// equal keys; equal keys stay adjacent for the segmented reduce). Tiles of
+// kMergeTile outputs: merge_split_k finds each tile's split (i from A) by a
+// binary search on the cross diagonal; merge_tile_k loads the tile's A and B
+// slices into LDS and every thread merges kMergeItems consecutive outputs.
+// ---------------------------------------------------------------------------
+
+template <int W>
+struct MergeCfg {
+    static constexpr int ITEMS = W <= 2 ? 8 : 4;  // outputs per thread
+    static constexpr int TILE = kBlock * ITEMS;   // LDS: TILE x (8W + 4) B <= 40 KB
+};
+int merge_tile(int W) { return kBlock * (W <= 2 ? 8 : 4); }
+
+template <int W>
+__device__ __forceinline__ bool key_le(const u64* __restrict__ ka, u64 sa, u64 ia, const u64* __restrict__ kb, u64 sb,
+                                       u64 ib) {
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        const u64 x = ka[(u64)j * sa + ia], y = kb[(u64)j * sb + ib];
+        if (x != y) return x < y;
+    }
+    return true;
+}
+
+template <int W>
+__device__ __forceinline__ u64 merge_search(const u64* __restrict__ ka, u64 sa, u64 na, const u64* __restrict__ kb,
+                                            u64 sb, u64 nb, u64 diag) {
+    u64 lo = diag > nb ? diag - nb : 0, hi = diag < na ? diag : na;
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (key_le<W>(ka, sa, mid, kb, sb, diag - 1 - mid))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void merge_split_k(const u64* __restrict__ ka, u64 sa, u64 na,
+                                                        const u64* __restrict__ kb, u64 sb, u64 nb, u64 ntiles,
+                                                        u64* __restrict__ split) {
+    constexpr int TILE = MergeCfg<W>::TILE;
+    for (u64 t = (u64)blockIdx.x * kBlock + threadIdx.x; t <= ntiles; t += (u64)gridDim.x * kBlock)
+        split[t] = merge_search<W>(ka, sa, na, kb, sb, nb, min(t * (u64)TILE, na + nb));
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void merge_tile_k(const u64* __restrict__ ka, const u32* __restrict__ ca, u64 sa,
+                                                       u64 na, const u64* __restrict__ kb, const u32* __restrict__ cb,
+                                                       u64 sb, u64 nb, const u64* __restrict__ split, u64 ntiles,
+                                                       u64* __restrict__ ko, u32* __restrict__ co, u64 so) {
+    constexpr int kMergeTile = MergeCfg<W>::TILE;
+    constexpr int kMergeItems = MergeCfg<W>::ITEMS;
+    __shared__ u64 sk[W * kMergeTile];
+    __shared__ u32 sc[kMergeTile];
+    const int tid = threadIdx.x;
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const u64 d0 = t * (u64)kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
+        const u64 i0 = split[t], i1 = split[t + 1];
+        const u64 j0 = d0 - i0, j1 = d1 - i1;
+        const u32 la = (u32)(i1 - i0), lb = (u32)(j1 - j0);
+        // LDS: A slice at [0, la), B slice at [la, la + lb)
+        for (u32 x = tid; x < la + lb; x += kBlock) {
+            const bool fa = x < la;
+            const u64 src = fa ? i0 + x : j0 + (x - la);
+#pragma unroll
+            for (int j = 0; j < W; j++) sk[j * kMergeTile + x] = fa ? ka[(u64)j * sa + src] : kb[(u64)j * sb + src];
+            sc[x] = fa ? ca[src] : cb[src];
+        }
+        __syncthreads();
+        // this thread's outputs [dl, dl + kMergeItems) of the tile
+        const u32 dl = min((u32)tid * kMergeItems, la + lb);
+        u32 lo = dl > lb ? dl - lb : 0, hi = dl < la ? dl : la;
+        while (lo < hi) {
+            const u32 mid = (lo + hi) >> 1;
+            if (key_le<W>(sk, kMergeTile, mid, sk, kMergeTile, la + dl - 1 - mid))
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        u32 ia = lo, ib = dl - lo;
+        const u32 de = min(dl + kMergeItems, la + lb);
+        for (u32 d = dl; d < de; d++) {
+            const bool takea = ib >= lb || (ia < la && key_le<W>(sk, kMergeTile, ia, sk, kMergeTile, la + ib));
+            const u32 x = takea ? ia : la + ib;
+            if (takea)
+                ia++;
+            else
+                ib++;
+#pragma unroll
+            for (int j = 0; j < W; j++) ko[(u64)j * so + d0 + d] = sk[j * kMergeTile + x];
+            co[d0 + d] = sc[x];
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_merge(int W, const uint64_t* ka, const uint32_t* ca, uint64_t sa, uint64_t na, const uint64_t* kb,
+                        const uint32_t* cb, uint64_t sb, uint64_t nb, uint64_t* ko, uint32_t* co, uint64_t so,
+                        uint64_t* split, hipStream_t s) {
+    const u64 n = na + nb;
+    if (n == 0) return hipSuccess;
+    const u64 ntiles = (n + merge_tile(W) - 1) / merge_tile(W);
+    const int gs = (int)hmin((ntiles + 1 + kBlock - 1) / kBlock, 4096);
+    const int gt = (int)hmin(ntiles, 8192);
+#define KC_MG(WW)                                                                                                    \
+    hipLaunchKernelGGL(merge_split_k<WW>, dim3(gs), dim3(kBlock), 0, s, ka, sa, na, kb, sb, nb, ntiles, split);     \
+    hipLaunchKernelGGL(merge_tile_k<WW>, dim3(gt), dim3(kBlock), 0, s, ka, ca, sa, na, kb, cb, sb, nb,             \
+                       (const u64*)split, ntiles, ko, co, so)
+    switch (W) {
+    case 1: KC_MG(1); break;
+    case 2: KC_MG(2); break;
+    case 3: KC_MG(3); break;
+    case 4: KC_MG(4); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef KC_MG
+    return hipGetLastError();
+}
+
+uint64_t merge_split_elems(uint64_t n) { return n / 1024 + 2; }
 
 hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, uint64_t stride, uint32_t* cnts,
                          hipStream_t s) {

@@ -511,3 +511,24 @@ def test_skewed_segment_uses_lsd_fallback(kca, orc, k):
         ctx.count_fastq(fq)
         got = ctx.records()
     assert got == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("k,nruns", [(31, 1), (31, 2), (31, 5), (55, 8), (100, 3)])
+def test_merge_runs_device(kca, orc, k, nruns):
+    """kc_merge_runs_device: nruns sorted runs (overlapping key ranges, shared
+    keys summed, empty runs allowed) merged by merge path == one count of all."""
+    import torch
+
+    L = 120
+    shards = [kca.synth_fastq(700 * (r % 3), L, 40 + r, n_rate=0.002, genome_length=30_000) for r in range(nruns)]
+    runs = [orc.count_fastq(fq, k) if fq else b"" for fq in shards]
+    rs = orc.rs_of(k)
+    with kca.Context(kmer_length=k, line_length=L) as ctx:
+        ctx.finish()
+        buf = b"".join(runs)
+        src = torch.frombuffer(bytearray(buf), dtype=torch.uint8).cuda() if buf else \
+            torch.empty(0, dtype=torch.uint8).cuda()
+        n = ctx.merge_runs(src, [len(r) // rs for r in runs])
+        got = ctx.records()
+    want = orc.count_fastq(b"".join(shards), k)
+    assert got == want and n * rs == len(want)
