@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--genome", type=int, default=None, help="0 = iid uniform reads")
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--mem", type=int, default=None, help="gpuMemoryLimit per GPU (bytes)")
-    ap.add_argument("--engine", default="partition", choices=["partition", "table"])
+    ap.add_argument("--engine", default="partition", choices=["partition", "table", "skm"])
     ap.add_argument("--cpu-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],

@@ -98,6 +98,11 @@ typedef struct kc_config {
                                    (default engine: hash-partition the k-mers into
                                    65536 buckets and count each in an LDS table;
                                    the global table catches LDS overflow) */
+#define KC_FLAG_ENGINE_SKM 4u   /* super-k-mer engine: runs of consecutive windows
+                                   sharing a minimizer bucket move through HBM as
+                                   one record of bases (~1.5 B per k-mer at k=31
+                                   instead of an 8-byte key); for 18 <= k <= 96,
+                                   other (L, k) fall back to the default engine */
 
 typedef struct kc_stats {
     uint64_t reads;            /* reads counted so far */

@@ -188,9 +188,9 @@ class Context:
         self.rs = 8 * self.W + 4
         self._device = device
         self._tmp = temp_dir.encode() if temp_dir else None
-        if engine not in ("partition", "table"):
-            raise ValueError("engine must be 'partition' or 'table'")
-        flags = (1 if quiet else 0) | (2 if engine == "table" else 0)
+        if engine not in ("partition", "table", "skm"):
+            raise ValueError("engine must be 'partition', 'table' or 'skm'")
+        flags = (1 if quiet else 0) | (2 if engine == "table" else 0) | (4 if engine == "skm" else 0)
         cfg = _Config(device, 0, kmer_length, line_length or kmer_length, int(gpu_memory_limit), int(table_bytes),
                       self._tmp, flags, int(lds_slots))
         h = ctypes.c_void_p()

@@ -58,6 +58,9 @@ struct kc_ctx {
 
     // partition engine (default): key buffers for one batch, records
     bool part = true;
+    bool skm = false;              // KC_FLAG_ENGINE_SKM: super-k-mer records instead of keys
+    bool skm_used = false;         // a batch went through the skm engine since the last reset
+    uint64_t* pool_cursor = nullptr;  // device u64: skm pool allocator
     uint64_t key_cap = 0;          // keys per batch
     uint64_t* keys_a = nullptr;    // W x key_cap
     uint8_t* digs = nullptr;       // key_cap: P3 digit (word0 >> 56) of keys_a[i], written by P2
@@ -531,9 +534,225 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
     return KC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Engine "skm" (super-k-mer records; kernels and record layout in kc_skm.inl)
+// ---------------------------------------------------------------------------
+
+// Groups n SoA items (NW words at stride sa in `a`, optional u32 payload pa)
+// by the 16 bits word0 >> 48: level 1 by bits 48..55 into `b` (writing the
+// level-2 digit, bits 56..63, of every item to `digs`), level 2 by bits 56..63
+// stable over level 1's regions, back into `a`. ms[0] += histogram + scan
+// time, ms[1] += scatter time (HIP events).
+static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, uint32_t* pa, uint64_t* b,
+                         uint64_t sb, uint32_t* pb, uint8_t* digs, uint64_t n, double* ms) {
+    if (n == 0) return KC_OK;
+    kc_status s;
+    const uint64_t tile = (uint64_t)rp_tile(NW, pay);
+    const uint64_t nt1 = (n + tile - 1) / tile;
+    const uint64_t ntmax = nt1 + 256;
+    const uint64_t tmpn = p3_tmp_elems(ntmax);
+    if ((s = ensure(c, c->part_sort_hist, (256 * ntmax + tmpn + 4 + 2 * 257) * 8))) return s;
+    uint64_t* pos = (uint64_t*)c->part_sort_hist.p;
+    uint64_t* tmp = pos + 256 * ntmax;
+    uint64_t* rt = tmp + tmpn;
+    const int grid = 2 * c->n_cu;
+    float t = 0.f;
+    std::vector<uint64_t> h(4 + 2 * 257);
+    h[0] = 0;
+    h[1] = n;
+    h[2] = 0;
+    h[3] = nt1;
+    HIPCHK(c, hipMemcpyAsync(rt, h.data(), 4 * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_rp_hist(nullptr, a, 48, rt, rt + 2, 1, nt1, (uint32_t)tile, pos, tmp, grid, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    ms[0] += t;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_rp_scatter(NW, pay, a, sa, b, sb, pa, pb, rt, rt + 2, 1, nt1, pos, 48, digs, 56, grid,
+                                c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    std::vector<uint64_t> dbase(256);
+    HIPCHK(c, hipMemcpyAsync(dbase.data(), rp_digit_base(tmp, nt1), 256 * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    ms[1] += t;
+    uint64_t* rs = h.data() + 4;
+    uint64_t* tp = rs + 257;
+    for (int d = 0; d < 256; d++) rs[d] = dbase[d];
+    rs[256] = n;
+    tp[0] = 0;
+    for (int d = 0; d < 256; d++) tp[d + 1] = tp[d] + (rs[d + 1] - rs[d] + tile - 1) / tile;
+    const uint64_t nt2 = tp[256];
+    HIPCHK(c, hipMemcpyAsync(rt + 4, rs, 2 * 257 * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_rp_hist(digs, nullptr, 0, rt + 4, rt + 4 + 257, 256, nt2, (uint32_t)tile, pos, tmp, grid,
+                             c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    ms[0] += t;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_rp_scatter(NW, pay, b, sb, a, sa, pb, pa, rt + 4, rt + 4 + 257, 256, nt2, pos, 56, nullptr, 0,
+                                grid, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    ms[1] += t;
+    return KC_OK;
+}
+
+// part_ms slots for this engine: [0] E + F, [1] F, [2] S1/S2 scatters,
+// [3] S1/S2 histograms + scans + P4, [4] P5.
+static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
+                                 int64_t L, const SkmGeom& g) {
+    if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
+    const int W = c->W;
+    const int RW = W + 1;
+    const uint64_t nw = (uint64_t)(L - c->k + 1);
+    // keys_a / keys_b hold RW x pool_cap record words each; digs holds a byte per record
+    uint64_t pool_cap = (uint64_t)W * c->key_cap / RW;
+    if (const char* e = getenv("KC_SKM_POOL_CAP")) {  // tests: force the pool-overflow retry
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v > 0 && v < pool_cap) pool_cap = v;
+    }
+    uint64_t max_reads = c->key_cap / nw;
+    if (max_reads == 0) return fail(c, KC_ERR_ARG, "gpu_memory_limit too small for one read's windows");
+    kc_status s;
+    uint64_t done = 0;
+    float t = 0.f;
+    while (done < n_reads) {
+        uint64_t nr = n_reads - done;
+        if (nr > max_reads) nr = max_reads;
+        CountLaunch l;
+        l.base = base;
+        l.seq_off = seq_off;
+        l.read0 = done;
+        l.n_reads = nr;
+        l.L = (int)L;
+        l.k = (int)c->k;
+        l.table = c->table;
+        l.cap = c->cap;
+        l.spill = c->spill;
+        l.spill_cap = c->spill_cap;
+        l.stats = c->stats;
+        l.probe_limit = probe_limit(c);
+        const uint64_t ng = nr * (uint64_t)groups_per_read((int)L);
+        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
+        l.codes = (const uint32_t*)c->part_codes.p;
+        l.inval = (const uint16_t*)c->part_inval.p;
+        if ((s = sync_stats(c))) return s;
+        std::vector<uint64_t> saved(c->stats_h, c->stats_h + ST_N);
+        HIPCHK(c, hipMemsetAsync(c->pool_cursor, 0, 8, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        HIPCHK(c, hipEventSynchronize(c->ev1));
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+        c->part_ms[0] += t;
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_skm_front(l, g, c->keys_a, pool_cap, c->pool_cursor, 8 * c->n_cu, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        uint64_t np = 0;
+        HIPCHK(c, hipMemcpyAsync(&np, c->pool_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+        c->part_ms[0] += t;
+        c->part_ms[1] += t;
+        c->st.insert_launches++;
+        c->st.insert_ms += t;
+        if (np > pool_cap) {
+            // more records than the pool holds (runs far shorter than usual):
+            // undo the batch's statistics and retry with half the reads
+            HIPCHK(c, hipMemcpyAsync(c->stats, saved.data(), ST_N * 8, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            memcpy(c->stats_h, saved.data(), ST_N * 8);
+            if (nr <= 1) return fail(c, KC_ERR_INTERNAL, "skm pool overflow on one read");
+            max_reads = nr / 2;
+            continue;
+        }
+        c->skm_used = true;
+        if (np > 0) {
+            double gm[2] = {0, 0};
+            if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, c->keys_b, pool_cap, nullptr, c->digs, np,
+                             gm)))
+                return s;
+            c->part_ms[3] += gm[0];
+            c->part_ms[2] += gm[1];
+            c->part_keys += np;
+            const uint32_t nb = 1u << kBucketBits;
+            if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8))) return s;
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            HIPCHK(c, launch_bucket_bounds(1, c->keys_a, pool_cap, np, kBucketBits, (uint64_t*)c->part_starts.p,
+                                           c->stream));
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipEventSynchronize(c->ev1));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[3] += t;
+            uint64_t bound = (uint64_t)nb * (uint64_t)skm_lds_slots(W);
+            const uint64_t kbound = nr * nw;
+            if (bound > kbound) bound = kbound;
+            const uint64_t rec0 = c->rec_n;
+            const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
+            for (;;) {
+                if ((s = grow_records(c, rec0 + bound))) return s;
+                // keys_b is free after S2: it takes P5's spills (W x key_cap words)
+                HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                HIPCHK(c, launch_count_skm(W, (int)c->k, c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, nb,
+                                           c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
+                                           c->keys_b, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots, c->n_cu,
+                                           c->stream));
+                HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+                if ((s = sync_stats(c))) return s;
+                HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                c->part_ms[4] += t;
+                c->p5_launches++;
+                if (getenv("KC_DEBUG"))
+                    fprintf(stderr, "kc: skm F records=%llu P5 passes=%llu aborts=%llu max_m=%llu records=%llu %.3f ms\n",
+                            (unsigned long long)np, (unsigned long long)c->stats_h[ST_P5_PASSES],
+                            (unsigned long long)c->stats_h[ST_P5_ABORTS], (unsigned long long)c->stats_h[ST_P5_MAXM],
+                            (unsigned long long)c->rec_n, t);
+                if (!(c->stats_h[ST_ERR] & ERR_REC_OVERFLOW)) break;
+                if (bound >= kbound || c->stats_h[ST_CLAIMED] != claimed0 || c->stats_h[ST_SPILL2_FILL])
+                    return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
+                bound = kbound;
+                uint64_t err = c->stats_h[ST_ERR] & ~(uint64_t)ERR_REC_OVERFLOW;
+                HIPCHK(c, hipMemcpyAsync(c->stats + ST_ERR, &err, 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec0, 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                c->stats_h[ST_ERR] = err;
+                c->rec_n = rec0;
+            }
+            if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
+            uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
+            if (n2) {
+                if ((s = flush_keys(c, c->keys_b, c->key_cap, n2, c->keys_a))) return s;
+                HIPCHK(c, hipMemsetAsync(c->stats + ST_SPILL2_FILL, 0, 8, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                c->stats_h[ST_SPILL2_FILL] = 0;
+            }
+        } else if ((s = sync_stats(c))) {
+            return s;
+        }
+        c->batches++;
+        done += nr;
+    }
+    c->st.reads += n_reads;
+    c->st.windows += n_reads * nw;
+    c->st.valid_kmers = c->stats_h[ST_VALID];
+    c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
+    return KC_OK;
+}
+
 static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
+    if (c->skm) {
+        const SkmGeom g = skm_geometry((int)L, (int)c->k);
+        if (g.ok) return count_reads_skm(c, base, seq_off, n_reads, L, g);
+    }
     if (c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= kMaxLds)
         return count_reads_part(c, base, seq_off, n_reads, L);
     return count_reads_table(c, base, seq_off, n_reads, L);
@@ -643,6 +862,7 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
     if (M < (1u << 20)) M = 1u << 20;
     c->part = (cfg->flags & KC_FLAG_ENGINE_TABLE) == 0;
+    c->skm = c->part && (cfg->flags & KC_FLAG_ENGINE_SKM) != 0;
     size_t slot_bytes = 8 * (size_t)slot_words(c->W);
     size_t spill_bytes, tbytes;
     if (c->part) {
@@ -671,6 +891,7 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
         if (hipMalloc((void**)&c->keys_b, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->digs, (size_t)c->key_cap + 16) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->rec_cursor, 8) != hipSuccess) return bail(KC_ERR_NOMEM);
+        if (hipMalloc((void**)&c->pool_cursor, 8) != hipSuccess) return bail(KC_ERR_NOMEM);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
             c->n_cu = prop.multiProcessorCount;
@@ -699,6 +920,7 @@ void kc_destroy(kc_ctx* c) {
     if (c->rec_keys) (void)hipFree(c->rec_keys);
     if (c->rec_cnts) (void)hipFree(c->rec_cnts);
     if (c->rec_cursor) (void)hipFree(c->rec_cursor);
+    if (c->pool_cursor) (void)hipFree(c->pool_cursor);
     release(c->part_hist);
     release(c->part_codes);
     release(c->part_inval);
@@ -738,6 +960,7 @@ kc_status kc_reset(kc_ctx* c) {
     for (double& x : c->part_ms) x = 0;
     c->part_keys = 0;
     c->p5_launches = 0;
+    c->skm_used = false;
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
@@ -811,6 +1034,7 @@ kc_status kc_check_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, ui
 }
 
 static kc_status sort_reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, bool dups, uint64_t* n_out);
+static kc_status reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, int which, bool dups, uint64_t* n_out);
 
 // Sorted finish of the partition engine (one batch, every key counted in LDS):
 // the records of each P5 pass form one key-ordered segment; the descriptors
@@ -866,10 +1090,90 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
     return KC_OK;
 }
 
+// Finish whenever an skm batch contributed: the P5 records (+ global-table
+// records + key 0) are grouped by their first 8 bases (word0 >> 48) with the
+// rp_* passes (counts as payload), every group is sorted in LDS by seg_sort_k,
+// equal keys (several batches, the global table) are summed, then packed. A
+// group longer than seg_sort's capacity (skewed keys) or a small record set
+// takes the global radix sort instead.
+static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
+    kc_status s;
+    const int W = c->W;
+    const uint64_t nrec = c->rec_n;
+    const uint64_t claimed = c->stats_h[ST_CLAIMED];
+    if ((s = grow_records(c, nrec + claimed + 1))) return s;
+    if ((s = ensure(c, c->fin_misc, (2 * W + 1 + compact_tmp_elems()) * 8))) return s;
+    uint64_t* cursor = (uint64_t*)c->fin_misc.p + 2 * W;
+    uint64_t t = 0;
+    if (claimed) {
+        HIPCHK(c, launch_compact(W, c->table, c->cap, c->rec_keys + nrec, c->rec_cnts + nrec, c->rec_cap, cursor,
+                                 cursor + 1, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&t, cursor, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    uint64_t cur = nrec + t;
+    HIPCHK(c, hipMemcpyAsync(cursor, &cur, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_append_key0(W, c->rec_keys, c->rec_cnts, c->rec_cap, cursor, c->stats, c->stream));
+    uint64_t n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, cursor, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const bool dups = c->batches > 1 || t > 0;
+    const uint64_t out_cap = n + 1;
+    for (int i = 0; i < 2; i++) {
+        if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
+            return s;
+    }
+    uint64_t* k0 = (uint64_t*)c->fin_keys[0].p;
+    uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
+    const uint32_t nb = 1u << kBucketBits;
+    bool grouped = n >= nb && n <= c->key_cap && !getenv("KC_NO_SEGSORT");
+    std::vector<uint64_t> st;
+    if (grouped) {
+        double gm[2] = {0, 0};
+        if ((s = group16(c, W, true, c->rec_keys, c->rec_cap, c->rec_cnts, (uint64_t*)c->fin_keys[1].p, out_cap,
+                         (uint32_t*)c->fin_cnts[1].p, c->digs, n, gm)))
+            return s;
+        if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8))) return s;
+        HIPCHK(c, launch_bucket_bounds(W, c->rec_keys, c->rec_cap, n, kBucketBits, (uint64_t*)c->part_starts.p,
+                                       c->stream));
+        st.resize((size_t)nb + 1);
+        HIPCHK(c, hipMemcpyAsync(st.data(), c->part_starts.p, st.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        uint64_t mx = 0;
+        for (uint32_t b = 0; b < nb; b++) mx = std::max(mx, st[b + 1] - st[b]);
+        if (mx > (uint64_t)seg_sort_cap(W)) grouped = false;
+    }
+    if (grouped) {
+        if ((s = ensure(c, c->desc_v, (size_t)nb * 4)) || (s = ensure(c, c->desc_len, (size_t)nb * 4)) ||
+            (s = ensure(c, c->desc_fb, (size_t)nb * 4 + 16)))
+            return s;
+        std::vector<uint32_t> lens(nb);
+        for (uint32_t b = 0; b < nb; b++) lens[b] = (uint32_t)(st[b + 1] - st[b]);  // log2(m) = 0: 16-bit prefix
+        HIPCHK(c, hipMemcpyAsync(c->desc_len.p, lens.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, nb, c->stream));
+        uint64_t* fb_n = (uint64_t*)((char*)c->desc_fb.p + (size_t)nb * 4);
+        HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, (const uint32_t*)c->desc_v.p,
+                                  (const uint64_t*)c->part_starts.p, (const uint32_t*)c->desc_len.p,
+                                  (const uint64_t*)c->part_starts.p, nb, k0, c0, out_cap, c->stats,
+                                  (uint32_t*)c->desc_fb.p, fb_n, c->n_cu, c->stream));
+        if ((s = sync_stats(c))) return s;
+        if (c->stats_h[ST_ERR] & ERR_SEG_TOO_LONG) return fail(c, KC_ERR_INTERNAL, "segment longer than its LDS sort");
+        return reduce_pack(c, out_cap, n, 0, dups, n_out);
+    }
+    if (n) {
+        for (int j = 0; j < W; j++)
+            HIPCHK(c, hipMemcpyAsync(k0 + (size_t)j * out_cap, c->rec_keys + (size_t)j * c->rec_cap, n * 8,
+                                     hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c0, c->rec_cnts, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
+    return sort_reduce_pack(c, out_cap, n, dups, n_out);
+}
+
 // Finish of the partition engine: LDS records + fallback-table records + key 0
 // -> radix sort -> (sum duplicates when several batches or the fallback table
 // contributed) -> pack.
 static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
+    if (c->skm_used) return finish_skm(c, n_out);
     kc_status s;
     const int W = c->W;
     const uint64_t nrec = c->rec_n;

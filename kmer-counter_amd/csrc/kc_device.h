@@ -189,6 +189,39 @@ hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_
 hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, uint64_t n_rec, int L,
                               uint64_t* stats, hipStream_t s);
 
+// ---- super-k-mer engine (kc_skm.inl) ----
+struct SkmGeom {
+    bool ok;        // (L, k) supported: W <= 3, k >= 18, L - k + 1 <= 4096
+    int m;          // minimizer length
+    int Kp;         // key span in bases (k, or 32W when the last word is not masked)
+    int nmax;       // keys per record at most
+    int R, NG, HS;  // F tile: reads, code groups per read, m-mer hash slots per read
+    size_t lds;     // F dynamic LDS bytes
+};
+SkmGeom skm_geometry(int L, int k);
+// F: records (RW = W + 1 words, SoA at pool_cap) of the launch's reads; *pool_cursor
+// (zeroed by the caller) ends as the number of records handed out (padding
+// included); > pool_cap means the pool overflowed and nothing may be used.
+hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* pool, uint64_t pool_cap,
+                            uint64_t* pool_cursor, int grid_cap, hipStream_t s);
+// rp_*: radix grouping passes over NW-word SoA items (+ optional u32 payload)
+int rp_tile(int NW, bool pay);
+uint64_t* rp_digit_base(uint64_t* tmp, uint64_t ntiles);  // exclusive digit bases after launch_rp_hist
+// digit = digs[i] (digs != nullptr) or (w0[i] >> shift) & 255; tmp: p3_tmp_elems(ntiles); pos: 256 * ntiles
+hipError_t launch_rp_hist(const uint8_t* digs, const uint64_t* w0, int shift, const uint64_t* rstart,
+                          const uint64_t* tpre, int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos,
+                          uint64_t* tmp, int grid, hipStream_t s);
+hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t istride, uint64_t* kout,
+                             uint64_t ostride, const uint32_t* pin, uint32_t* pout, const uint64_t* rstart,
+                             const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,
+                             uint8_t* emit, int eshift, int grid, hipStream_t s);
+int skm_lds_slots(int W);
+int seg_sort_cap(int W);  // longest segment seg_sort_k takes
+hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride, const uint64_t* starts,
+                            uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                            uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
+                            uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s);
+
 // Synthetic FASTQ generator (bench/test input).
 struct SynthArgs {
     uint64_t first, n, seed, genome, n_threshold;

@@ -18,6 +18,10 @@ namespace kc {
 typedef uint64_t u64;
 typedef unsigned int u32;
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+// a volatile 16-byte LDS load (ds_read_b128): the cast pins the LDS address
+// space, which a generic volatile pointer loses (it would become a FLAT load)
+typedef __attribute__((address_space(3))) volatile v2u64 lds_v2u64;
 
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWave = 64;
@@ -1668,8 +1672,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
             const u32 ng = lcap >> 2;
             u32 g = (u32)((frac * (u64)ng) >> 48);
             for (u32 pr = 0; pr < max_probe; pr += 4) {
-                typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
-                const volatile v2u64* gp = (const volatile v2u64*)(lkeys + 4 * g);
+                const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
                 const v2u64 a0 = gp[0], a1 = gp[1];
                 const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
                 int hit = -1, emp = -1;
@@ -1892,8 +1895,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     if constexpr (W == 1) {
                         if ((a.lcap & 3u) == 0) {
                             const u32 g = (u32)((fr * (u64)(a.lcap >> 2)) >> 48);
-                            typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
-                            const volatile v2u64* gp = (const volatile v2u64*)(lkeys + 4 * g);
+                            const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
                             const v2u64 a0 = gp[0], a1 = gp[1];
                             const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
                             int hit = -1, emp = -1;
@@ -3147,5 +3149,8 @@ void synth_host(const SynthArgs& a, char* out) {
 }
 
 uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L) { return kc_synth_offset(first, first + n, L); }
+
+// super-k-mer engine (F, rp_*, count_skm): see kc_skm.inl
+#include "kc_skm.inl"
 
 }  // namespace kc

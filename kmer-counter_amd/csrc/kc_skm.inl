@@ -1,0 +1,1199 @@
+// kc_skm.inl — kernels of the super-k-mer engine ("skm"). Included by
+// kc_kernels.hip inside namespace kc: it shares that file's wave helpers, the
+// LDS hash insert, the global-table fallback and the P3 scan kernels.
+//
+// The partition engine moves every k-mer through HBM as an 8W-byte key three
+// times (P2 write, P3 read + write, P5 read). Consecutive windows of a read
+// share most of their bases, so the skm engine moves runs of them instead:
+// a super-k-mer is a maximal run of consecutive live windows of one read whose
+// minimizer bucket is equal, stored once as its bases (~1.5 B per k-mer at
+// k=31 instead of 8). Per batch of reads:
+//   E   encode_reads_k (shared)   reads -> 2-bit codes + not-ACGT masks
+//   F   skm_front_k<W>            windows -> minimizer bucket -> records
+//   S1  rp_upsweep_k/rp_scatter_k records by bucket bits 0..7  (+ digit bytes)
+//   S2  rp_upsweep_k/rp_scatter_k records by bucket bits 8..15, stable over
+//                                 S1's regions -> grouped by bucket
+//   P4  bucket_bounds_k (shared)  bucket ranges
+//   P5  count_skm_k<W>            per bucket: expand records into keys, count
+//                                 in the LDS table (sub-range passes, global
+//                                 table and spill exactly as count_buckets)
+// Finish: the (key, count) records are grouped by their first 8 bases with
+// the same rp_* passes (counts as payload) and every group is sorted in LDS
+// by seg_sort_k, so the output needs no global sort.
+//
+// Bucket of a window: the minimum over the window's m-mers (its first k bases,
+// all ACGT for a live window) of mmer_hash, low 16 bits. It is a function of
+// the key, so equal keys always meet in one bucket; counts stay exact for any
+// input (the bucket only decides where a key is counted).
+//
+// Record (RW = W + 1 u64 words, SoA): the words concatenated MSB-first hold
+//   bits [0, 16)          bucket (so word0 >> 48 is the bucket: the rp_*
+//                         passes and bucket_bounds_k read it like a key prefix)
+//   bits [16, 16 + 2 nb)  nb = K' + n - 1 bases, 2 bits each (A0 C1 G2 T3,
+//                         other bytes 3, bases past the read end 0), where K'
+//                         is the key span (k when the last key word is masked,
+//                         32W otherwise: GPUHandler.cu:181-186)
+//   low 6 bits            n, the number of keys (0 = padding record)
+// Key i of the record = K' bases from base i (the window i positions after
+// the run start) = exactly the key extractKMers builds for that window.
+// nb <= 32 RW - 11, so n <= nmax = 32 RW - 10 - K'; longer runs are split.
+
+constexpr int kSkmBlock = 256;
+constexpr u32 kSkmChunk = 4096;  // pool records per allocation (>= records of one tile)
+constexpr u32 kDead = 0xffffffffu;
+constexpr int kSkmPf = 2;  // F: code words prefetched per thread
+
+__device__ __forceinline__ u32 fmix32(u32 x) {
+    x ^= x >> 16;
+    x *= 0x85ebca6bu;
+    x ^= x >> 13;
+    x *= 0xc2b2ae35u;
+    x ^= x >> 16;
+    return x;
+}
+
+// m-mer order: m <= 16 (one u32) uses a multiplicative hash of the m-mer,
+// whose low 16 bits (the bucket) are a bijection of its last 8 bases; longer
+// m-mers are folded to 32 bits first
+__device__ __forceinline__ u32 mmer_hash(u64 mm) {
+    const u32 x = (u32)mm ^ ((u32)(mm >> 32) * 0x9e3779b1u);
+    return (x ^ 0x5bd1e995u) * 0x9e3779b1u;
+}
+
+// n / d for n, d < 2^16 with one mul_hi (m = ceil(2^32 / d) is exact there)
+struct FastDiv {
+    u32 d, m;
+    __device__ __forceinline__ explicit FastDiv(u32 dd) : d(dd), m((u32)((0x100000000ull + dd - 1) / dd)) {}
+    __device__ __forceinline__ u32 div(u32 n) const { return d == 1 ? n : __umulhi(n, m); }
+};
+
+__device__ __forceinline__ u64 readlane64(u64 v, int l) {
+    const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, l);
+    const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l);
+    return ((u64)hi << 32) | lo;
+}
+
+struct SkmArgs {
+    const u32* codes;             // kernel E output, G u32 per read
+    const unsigned short* inval;  //   not-ACGT masks, G u16 per read
+    int G;
+    u64 n_reads;
+    int L, k, m, Kp, nmax, R, NG, HS;
+    u64* pool;         // RW x pool_cap u64 (SoA)
+    u64 pool_cap;
+    u64* pool_cursor;  // chunk allocator (records handed out)
+    u64* stats;
+};
+
+struct SkmLds {
+    size_t codes, inval, hm, winfo, rflag, sa, ea, misc, total;
+};
+
+// LDS skew: a lane works on 8 consecutive windows, so lanes read hm / winfo
+// at a stride of 8 words; one pad word per 8 makes the stride 9 (no bank
+// conflicts)
+__host__ __device__ inline int skm_sk(int j) { return j + (j >> 3); }
+__host__ __device__ inline int skm_hsk(int HS) { return skm_sk(HS) + 1; }
+
+__host__ __device__ inline SkmLds skm_lds_layout(int R, int NG, int HS, int nw) {
+    SkmLds o;
+    size_t p = 0;
+    o.codes = p;
+    p += (size_t)R * NG * 4;
+    o.inval = p;
+    p += (size_t)R * NG * 4;
+    o.hm = p;
+    p += (size_t)R * skm_hsk(HS) * 4;
+    o.winfo = p;
+    p += ((size_t)R * nw + ((size_t)R * nw >> 3) + 8) * 4;
+    o.rflag = p;
+    p += (size_t)R * 4;
+    o.sa = p;
+    p += (size_t)R * nw * 2;
+    o.ea = p;
+    p += (size_t)R * nw * 2;
+    p = (p + 15) & ~(size_t)15;
+    o.misc = p;
+    p += 128;
+    o.total = p;
+    return o;
+}
+
+// F: one 256-thread workgroup per tile of R reads.
+//   1. code words and masks of the tile into LDS (groups past the read: 0)
+//   2. hm[r][j] = mmer_hash of the m bases from j (8 positions per thread)
+//   3. per 8-window chunk: window minimum over its k-m+1 m-mers as
+//      min(left suffix, shared core, right prefix); live = valid and key != 0
+//      (the rolling key of count_front); winfo = bucket or kDead
+//   4. run starts (live, bucket differs from the previous window) and ends,
+//      compacted in tile order by one block scan: the i-th start pairs with
+//      the i-th end (runs never cross reads)
+//   5. runs -> pieces of <= nmax windows -> records, written at consecutive
+//      positions of the workgroup's current pool chunk (one global atomic per
+//      kSkmChunk records); the chunk tail is padded with n = 0 records at exit
+template <int W>
+__global__ __launch_bounds__(kSkmBlock) void skm_front_k(SkmArgs a) {
+    constexpr int RW = W + 1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int L = a.L, k = a.k, m = a.m, NG = a.NG, HS = a.HS, R = a.R, Kp = a.Kp;
+    const u32 nmax = (u32)a.nmax;
+    const int nw = L - k + 1;
+    const int wm = k - m + 1;  // m-mers per window (>= 8)
+    const int nchr = (nw + 7) >> 3;
+    const int HSK = skm_hsk(HS);
+    const FastDiv div_nchr((u32)nchr), div_hch((u32)((HS + 7) >> 3)), div_nw((u32)nw), div_g((u32)a.G);
+    const SkmLds lay = skm_lds_layout(R, NG, HS, nw);
+    u32* codes = (u32*)(smem + lay.codes);
+    u32* inval = (u32*)(smem + lay.inval);
+    u32* hm = (u32*)(smem + lay.hm);
+    u32* winfo = (u32*)(smem + lay.winfo);
+    u32* rflag = (u32*)(smem + lay.rflag);
+    unsigned short* sa = (unsigned short*)(smem + lay.sa);
+    unsigned short* ea = (unsigned short*)(smem + lay.ea);
+    u64* ms = (u64*)(smem + lay.misc);  // [0] chunk cursor [1] chunk end [2] old cursor [3] room [4] new chunk
+    u32* scan_tmp = (u32*)(ms + 8);
+    const int tid = threadIdx.x;
+    const bool mask_last = ((k + 3) / 4) < 8 * W;
+    const u64 last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
+    const u64 ntiles = (a.n_reads + R - 1) / R;
+    u64 my_valid = 0;
+    bool my_hole = false;
+    if (tid == 0) {
+        ms[0] = 0;
+        ms[1] = 0;
+    }
+    // code groups past the read (g >= G) stay zero in LDS for the whole launch
+    for (int it = tid; it < R * NG; it += kSkmBlock) {
+        codes[it] = 0;
+        inval[it] = 0;
+    }
+    // the next tile's code words are loaded into registers while the current
+    // tile is processed; a thread's (read, group) slots are the same in every tile
+    const int G = a.G;
+    int pr[kSkmPf], pg[kSkmPf];
+#pragma unroll
+    for (int j = 0; j < kSkmPf; j++) {
+        const int it = tid + j * kSkmBlock;
+        pr[j] = it / G;
+        pg[j] = it - pr[j] * G;
+    }
+    u32 pfc[kSkmPf], pfi[kSkmPf];
+    auto prefetch = [&](u64 tile) {
+        const u64 r0 = tile * (u64)R;
+        const int nr = tile < ntiles ? (int)min((u64)R, a.n_reads - r0) : 0;
+#pragma unroll
+        for (int j = 0; j < kSkmPf; j++) {
+            u32 cw = 0, iv = 0;
+            if (pr[j] < nr) {
+                const u64 idx = (r0 + (u64)pr[j]) * (u64)G + (u64)pg[j];
+                cw = __builtin_nontemporal_load(a.codes + idx);
+                iv = __builtin_nontemporal_load(a.inval + idx);
+            }
+            pfc[j] = cw;
+            pfi[j] = iv;
+        }
+    };
+    prefetch(blockIdx.x);
+    __syncthreads();
+    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const u64 r0 = tile * (u64)R;
+        const int nr = (int)min((u64)R, a.n_reads - r0);
+        // 1. codes (prefetched; a tile with more groups than kSkmPf per thread
+        //    loads the rest directly)
+#pragma unroll
+        for (int j = 0; j < kSkmPf; j++)
+            if (pr[j] < nr) {
+                codes[pr[j] * NG + pg[j]] = pfc[j];
+                inval[pr[j] * NG + pg[j]] = pfi[j];
+            }
+        for (int it = tid + kSkmPf * kSkmBlock; it < nr * G; it += kSkmBlock) {
+            const int r = (int)div_g.div((u32)it), g = it - r * G;
+            const u64 idx = (r0 + (u64)r) * (u64)G + (u64)g;
+            codes[r * NG + g] = a.codes[idx];
+            inval[r * NG + g] = a.inval[idx];
+        }
+        for (int r = tid; r < nr; r += kSkmBlock) rflag[r] = 0;
+        __syncthreads();
+        prefetch(tile + gridDim.x);
+        // 2. m-mer hashes (positions past L - m are never used by a window)
+        const int hch = (HS + 7) >> 3;
+        for (int it = tid; it < nr * hch; it += kSkmBlock) {
+            const int r = (int)div_hch.div((u32)it), j0 = (it - r * hch) * 8;
+            const u64 x = code_word(codes + r * NG, j0);
+            u32* hr = hm + r * HSK;
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (j0 + i < HS) hr[skm_sk(j0 + i)] = mmer_hash((x << (2 * i)) >> (64 - 2 * m));
+        }
+        for (int it = tid; it < nr * G; it += kSkmBlock) {
+            const int r = (int)div_g.div((u32)it);
+            if (inval[r * NG + (it - r * G)]) atomicOr(&rflag[r], 1u);
+        }
+        __syncthreads();
+        // 3. windows
+        for (int c = tid; c < nr * nchr; c += kSkmBlock) {
+            const int r = (int)div_nchr.div((u32)c), p0 = (c - r * nchr) * 8;
+            const u32* cr = codes + r * NG;
+            const u32* hr = hm + r * HSK;
+            u32 core = ~0u;
+            for (int j = p0 + 7; j < p0 + wm; j++) core = min(core, hr[skm_sk(j)]);
+            u32 lft[8], rgt[8];
+            lft[7] = ~0u;
+#pragma unroll
+            for (int i = 6; i >= 0; i--) lft[i] = min(lft[i + 1], hr[skm_sk(p0 + i)]);
+            rgt[0] = ~0u;
+#pragma unroll
+            for (int i = 1; i < 8; i++) rgt[i] = min(rgt[i - 1], hr[skm_sk(p0 + wm + i - 1)]);
+            u64 kr[W];
+#pragma unroll
+            for (int j = 0; j < W; j++) kr[j] = code_word(cr, p0 + 32 * j);
+            u64 tl = code_word(cr, p0 + 32 * W);
+            const bool clean = rflag[r] == 0;
+            u32 zeros = 0, valids = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int p = p0 + i;
+                const bool active = p < nw;
+                bool valid = active;
+                if (active && !clean) {
+                    const u32* ir = inval + r * NG;
+                    const int last = p + k - 1;
+                    for (int gg = p >> 4; gg <= (last >> 4); gg++) {
+                        const int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
+                        const u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
+                        if (ir[gg] & rm) valid = false;
+                    }
+                }
+                bool is_zero = (kr[W - 1] & last_mask) == 0ull;
+#pragma unroll
+                for (int j = 0; j < W - 1; j++) is_zero = is_zero && (kr[j] == 0ull);
+                my_hole |= active && !valid;
+                valids += valid ? 1u : 0u;
+                zeros += (valid && is_zero) ? 1u : 0u;
+                if (active)
+                    winfo[skm_sk(r * nw + p)] = (valid && !is_zero) ? (min(core, min(lft[i], rgt[i])) & 0xffffu) : kDead;
+#pragma unroll
+                for (int j = 0; j < W - 1; j++) kr[j] = (kr[j] << 2) | (kr[j + 1] >> 62);
+                kr[W - 1] = (kr[W - 1] << 2) | (tl >> 62);
+                tl <<= 2;
+            }
+            my_valid += valids;
+            if (zeros) {
+                atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)zeros);
+                atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+            }
+        }
+        __syncthreads();
+        // 4. run starts / ends, compacted in tile order
+        u32 sbase = 0, ebase = 0;
+        for (int c0 = 0; c0 < nr * nchr; c0 += kSkmBlock) {
+            const int c = c0 + tid;
+            u32 smask = 0, emask = 0;
+            int q0 = 0;
+            if (c < nr * nchr) {
+                const int r = (int)div_nchr.div((u32)c), p0 = (c - r * nchr) * 8;
+                q0 = r * nw + p0;
+                u32 prev = p0 > 0 ? winfo[skm_sk(q0 - 1)] : kDead;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int p = p0 + i;
+                    if (p < nw) {
+                        const u32 v = winfo[skm_sk(q0 + i)];
+                        const u32 nx = p + 1 < nw ? winfo[skm_sk(q0 + i + 1)] : kDead;
+                        if (v != kDead) {
+                            if (v != prev) smask |= 1u << i;
+                            if (v != nx) emask |= 1u << i;
+                        }
+                        prev = v;
+                    }
+                }
+            }
+            u32 tot;
+            const u32 ex = block_excl_scan((u32)__popc(smask) | ((u32)__popc(emask) << 16), scan_tmp, &tot);
+            u32 sp = sbase + (ex & 0xffffu), ep = ebase + (ex >> 16);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if ((smask >> i) & 1u) sa[sp++] = (unsigned short)(q0 + i);
+                if ((emask >> i) & 1u) ea[ep++] = (unsigned short)(q0 + i);
+            }
+            sbase += tot & 0xffffu;
+            ebase += tot >> 16;
+        }
+        __syncthreads();
+        // 5. runs -> records
+        const u32 T = sbase;
+        const u32 per = (T + kSkmBlock - 1) / kSkmBlock;
+        const u32 i0 = min(T, (u32)tid * per), i1 = min(T, i0 + per);
+        u32 mine = 0;
+        for (u32 i = i0; i < i1; i++) {
+            const u32 n = (u32)ea[i] - (u32)sa[i] + 1u;
+            mine += (n + nmax - 1) / nmax;
+        }
+        u32 ptot;
+        const u32 pb = block_excl_scan(mine, scan_tmp, &ptot);
+        if (tid == 0) {
+            const u64 cur = ms[0], end = ms[1];
+            const u64 room = end - cur;
+            ms[2] = cur;
+            ms[3] = room;
+            if ((u64)ptot > room) {
+                const u64 nb = atomicAdd((unsigned long long*)a.pool_cursor, (unsigned long long)kSkmChunk);
+                ms[4] = nb;
+                ms[0] = nb + ((u64)ptot - room);
+                ms[1] = nb + kSkmChunk;
+            } else {
+                ms[0] = cur + ptot;
+            }
+        }
+        __syncthreads();
+        const u64 oc = ms[2], room = ms[3], nbase = ms[4];
+        u32 g = pb;
+        for (u32 i = i0; i < i1; i++) {
+            const u32 qs = sa[i];
+            const u32 n = (u32)ea[i] - qs + 1u;
+            const int r = (int)div_nw.div(qs);
+            const int ps0 = (int)qs - r * nw;
+            const u64 bk = winfo[skm_sk((int)qs)] & 0xffffu;
+            const u32* cr = codes + r * NG;
+            for (u32 off = 0; off < n; off += nmax, g++) {
+                const u32 nn = min(nmax, n - off);
+                const int ps = ps0 + (int)off;
+                u64 rec[RW];
+                rec[0] = (bk << 48) | (code_word(cr, ps) >> 16);
+#pragma unroll
+                for (int j = 1; j < RW; j++) rec[j] = code_word(cr, ps + 32 * j - 8);
+                const int vb = 16 + 2 * (Kp + (int)nn - 1);
+#pragma unroll
+                for (int j = 0; j < RW; j++) {
+                    const int bits = vb - 64 * j;
+                    const u64 msk = bits >= 64 ? ~0ull : (bits <= 0 ? 0ull : (~0ull << (64 - bits)));
+                    rec[j] &= msk;
+                }
+                rec[RW - 1] |= (u64)nn;
+                const u64 dst = (u64)g < room ? oc + g : nbase + ((u64)g - room);
+                if (dst < a.pool_cap) {
+#pragma unroll
+                    for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + dst] = rec[j];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // pad the rest of the current chunk with n = 0 records (bucket 0)
+    {
+        const u64 cur = ms[0], end = ms[1];
+        for (u64 i = cur + (u64)tid; i < end; i += kSkmBlock)
+            if (i < a.pool_cap) {
+#pragma unroll
+                for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + i] = 0ull;
+            }
+    }
+    wave_add(&a.stats[ST_VALID], my_valid);
+    if (__ballot(my_hole) && lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+}
+
+SkmGeom skm_geometry(int L, int k) {
+    SkmGeom g;
+    g.ok = false;
+    const int W = (k + 31) / 32;
+    const int RW = W + 1;
+    if (W > 3 || k < 18 || L < k) return g;
+    const bool mask_last = ((k + 3) / 4) < 8 * W;
+    g.Kp = mask_last ? k : 32 * W;
+    g.nmax = 32 * RW - 10 - g.Kp;
+    if (g.nmax > 63) g.nmax = 63;
+    // m-mers: a window's minimizer lives ~(k - m + 1) windows; runs longer
+    // than nmax are split, so aim k - m + 1 <= nmax (m in [11, 24])
+    int m = k - g.nmax + 1;
+    if (m < 11) m = 11;
+    if (m > 24) m = 24;
+    if (k - m + 1 < 8) m = k - 7;
+    g.m = m;
+    const int nw = L - k + 1;
+    const int nchr = (nw + 7) / 8;
+    if (nw > 4096) return g;  // a tile's records must fit one pool chunk
+    g.NG = (L + 32 * RW + 64) / 16 + 3;
+    g.HS = L - m + 8;
+    int R = kSkmBlock / nchr;
+    if (R < 1) R = 1;
+    while (R > 1 && skm_lds_layout(R, g.NG, g.HS, nw).total > 48 * 1024) R--;
+    g.R = R;
+    g.lds = skm_lds_layout(R, g.NG, g.HS, nw).total;
+    if (g.lds > 64 * 1024) return g;
+    g.ok = true;
+    return g;
+}
+
+hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* pool, uint64_t pool_cap,
+                            uint64_t* pool_cursor, int grid_cap, hipStream_t s) {
+    if (l.n_reads == 0) return hipSuccess;
+    if (!g.ok || !l.codes || !l.inval) return hipErrorInvalidValue;
+    SkmArgs a;
+    a.codes = l.codes;
+    a.inval = (const unsigned short*)l.inval;
+    a.G = groups_per_read(l.L);
+    a.n_reads = l.n_reads;
+    a.L = l.L;
+    a.k = l.k;
+    a.m = g.m;
+    a.Kp = g.Kp;
+    a.nmax = g.nmax;
+    a.R = g.R;
+    a.NG = g.NG;
+    a.HS = g.HS;
+    a.pool = pool;
+    a.pool_cap = pool_cap;
+    a.pool_cursor = pool_cursor;
+    a.stats = l.stats;
+    const u64 tiles = (l.n_reads + g.R - 1) / g.R;
+    const int W = (l.k + 31) / 32;
+    // one wave of workgroups: every workgroup walks the same number of tiles
+    int per_cu = 0, n_cu = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (W == 1) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, skm_front_k<1>, kSkmBlock, g.lds);
+    else if (W == 2) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, skm_front_k<2>, kSkmBlock, g.lds);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, skm_front_k<3>, kSkmBlock, g.lds);
+    u64 cap = (per_cu > 0 && n_cu > 0) ? (u64)per_cu * (u64)n_cu : (u64)grid_cap;
+    if (cap > (u64)grid_cap) cap = (u64)grid_cap;
+    const int grid = (int)hmin(tiles, cap);
+    switch (W) {
+    case 1: hipLaunchKernelGGL(skm_front_k<1>, dim3(grid), dim3(kSkmBlock), g.lds, s, a); break;
+    case 2: hipLaunchKernelGGL(skm_front_k<2>, dim3(grid), dim3(kSkmBlock), g.lds, s, a); break;
+    case 3: hipLaunchKernelGGL(skm_front_k<3>, dim3(grid), dim3(kSkmBlock), g.lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// rp_*: two-level radix grouping of SoA items by the 16 bits word0 >> 48
+// (generalizes P3 to any word count, an optional u32 payload, a digit taken
+// from word0 at any shift, and a digit byte emitted for the next level).
+// Regions: region r holds tiles [tpre[r], tpre[r+1]); tile i of r starts at
+// rstart[r] + i * TILE. Level 1 is one region; level 2 takes level 1's 256
+// digit regions, so its digit-major positions give (high byte, low byte)
+// order. Ranks inside a tile are unstable (LDS atomics): only grouping is
+// needed (records, and the keys of one group are distinct or summed later).
+// ---------------------------------------------------------------------------
+
+template <int NW, bool PAY>
+struct RpCfg {
+    static constexpr int BYTES = 8 * NW + (PAY ? 4 : 0);
+    static constexpr int K0 = 143808 / (BYTES * kP3Block);
+    static constexpr int KPT = K0 > 16 ? 16 : K0;
+    static constexpr int TILE = kP3Block * KPT;
+};
+
+int rp_tile(int NW, bool pay) {
+    const int bytes = 8 * NW + (pay ? 4 : 0);
+    int kpt = 143808 / (bytes * kP3Block);
+    if (kpt > 16) kpt = 16;
+    return kP3Block * kpt;
+}
+
+__device__ __forceinline__ void rp_tile_range(const u64* __restrict__ rstart, const u64* __restrict__ tpre, int nreg,
+                                              u64 t, u64 TILE, u64* lo, u64* hi) {
+    int a = 0, b = nreg;  // region r with tpre[r] <= t < tpre[r+1]
+    while (b - a > 1) {
+        const int mid = (a + b) >> 1;
+        if (tpre[mid] <= t)
+            a = mid;
+        else
+            b = mid;
+    }
+    const u64 st = rstart[a] + (t - tpre[a]) * TILE;
+    *lo = st;
+    *hi = min(st + TILE, rstart[a + 1]);
+}
+
+// Tile histograms (tile-major u32 counts): digit = digs[i] when digs is given,
+// else (w0[i] >> shift) & 255.
+__global__ __launch_bounds__(kBlock) void rp_upsweep_k(const unsigned char* __restrict__ digs,
+                                                       const u64* __restrict__ w0, int shift,
+                                                       const u64* __restrict__ rstart, const u64* __restrict__ tpre,
+                                                       int nreg, u64 ntiles, u32 TILE, u32* __restrict__ cnt_t) {
+    __shared__ u32 h[4 * 256];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        for (int i = tid; i < 4 * 256; i += kBlock) h[i] = 0;
+        __syncthreads();
+        u64 lo, hi;
+        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+        u32* hw = h + wave * 256;
+        if (digs) {
+            const u64 alo = min(hi, (lo + 15) & ~15ull);
+            for (u64 i = lo + tid; i < alo; i += kBlock) atomicAdd(&hw[digs[i]], 1u);
+            const u64 ahi = alo + ((hi - alo) & ~15ull);
+            for (u64 i = alo + 16 * (u64)tid; i < ahi; i += 16 * (u64)kBlock) {
+                const v4u v = __builtin_nontemporal_load((const v4u*)(digs + i));
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const u32 x = c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+                    atomicAdd(&hw[x & 255u], 1u);
+                    atomicAdd(&hw[(x >> 8) & 255u], 1u);
+                    atomicAdd(&hw[(x >> 16) & 255u], 1u);
+                    atomicAdd(&hw[x >> 24], 1u);
+                }
+            }
+            for (u64 i = ahi + tid; i < hi; i += kBlock) atomicAdd(&hw[digs[i]], 1u);
+        } else {
+            for (u64 i = lo + tid; i < hi; i += kBlock)
+                atomicAdd(&hw[(u32)(__builtin_nontemporal_load(w0 + i) >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        cnt_t[t * 256 + tid] = h[tid] + h[256 + tid] + h[512 + tid] + h[768 + tid];
+        __syncthreads();
+    }
+}
+
+template <int NW, bool PAY>
+__global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__ kin, u64 istride,
+                                                         u64* __restrict__ kout, u64 ostride,
+                                                         const u32* __restrict__ pin, u32* __restrict__ pout,
+                                                         const u64* __restrict__ rstart, const u64* __restrict__ tpre,
+                                                         int nreg, u64 ntiles, const u64* __restrict__ pos,
+                                                         int dshift, unsigned char* __restrict__ emit, int eshift) {
+    constexpr int KPT = RpCfg<NW, PAY>::KPT;
+    constexpr int TILE = RpCfg<NW, PAY>::TILE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* skey = (u64*)smem;                                    // NW x TILE
+    u32* spay = (u32*)(skey + (size_t)NW * TILE);              // TILE (PAY)
+    u32* wc = spay + (PAY ? TILE : 0);                         // 16 waves x 128 words: two u16 counters each
+    unsigned short* woff = (unsigned short*)(wc + 16 * 128);   // 16 x 256
+    u32* dst = (u32*)(woff + 16 * 256);                        // 256 digit starts in the tile
+    u64* gpos = (u64*)(dst + 256);                             // 256 global run starts
+    u32* wsum = (u32*)(gpos + 256);                            // 16
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    u64 nk[KPT][NW];
+    u32 np[KPT];
+    auto load = [&](u64 t) {
+        u64 lo = 0, hi = 0;
+        if (t < ntiles) rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u64 q = lo + (u64)i * kP3Block + tid;
+#pragma unroll
+            for (int j = 0; j < NW; j++)
+                nk[i][j] = q < hi ? __builtin_nontemporal_load(kin + (u64)j * istride + q) : 0ull;
+            if constexpr (PAY) np[i] = q < hi ? __builtin_nontemporal_load(pin + q) : 0u;
+        }
+    };
+    load(blockIdx.x);
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        u64 lo, hi;
+        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+        const u32 len = (u32)(hi - lo);
+        u64 key[KPT][NW];
+        u32 pv[KPT];
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+#pragma unroll
+            for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
+            pv[i] = PAY ? np[i] : 0u;
+        }
+        for (int i = tid; i < 16 * 128; i += kP3Block) wc[i] = 0;
+        if (tid < 256) gpos[tid] = pos[t * 256 + tid];
+        __syncthreads();
+        load(t + gridDim.x);
+        u32 rank[KPT];
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u32 q = (u32)i * kP3Block + (u32)tid;
+            rank[i] = 0;
+            if (q < len) {
+                const u32 d = (u32)(key[i][0] >> dshift) & 255u;
+                const u32 sh = 16 * (d & 1);
+                rank[i] = (atomicAdd(&wc[wave * 128 + (d >> 1)], 1u << sh) >> sh) & 0xffffu;
+            }
+        }
+        __syncthreads();
+        if (tid < 256) {
+            u32 run = 0;
+            for (int w = 0; w < 16; w++) {
+                woff[w * 256 + tid] = (unsigned short)run;
+                run += (wc[w * 128 + (tid >> 1)] >> (16 * (tid & 1))) & 0xffffu;
+            }
+            const u32 v = run;
+            u32 inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            if (lane == 63) wsum[wave] = inc;
+            dst[tid] = inc - v;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            u32 add = 0;
+            for (int w = 0; w < wave; w++) add += wsum[w];
+            dst[tid] += add;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u32 q = (u32)i * kP3Block + (u32)tid;
+            if (q < len) {
+                const u32 d = (u32)(key[i][0] >> dshift) & 255u;
+                const u32 at = dst[d] + woff[wave * 256 + d] + rank[i];
+#pragma unroll
+                for (int j = 0; j < NW; j++) skey[(size_t)j * TILE + at] = key[i][j];
+                if constexpr (PAY) spay[at] = pv[i];
+            }
+        }
+        __syncthreads();
+        for (u32 q = tid; q < len; q += kP3Block) {
+            const u64 k0 = skey[q];
+            const u32 d = (u32)(k0 >> dshift) & 255u;
+            const u64 g = gpos[d] + (q - dst[d]);
+            kout[g] = k0;
+#pragma unroll
+            for (int j = 1; j < NW; j++) kout[(u64)j * ostride + g] = skey[(size_t)j * TILE + q];
+            if constexpr (PAY) pout[g] = spay[q];
+            if (emit) emit[g] = (unsigned char)(k0 >> eshift);
+        }
+        __syncthreads();
+    }
+}
+
+static size_t rp_scatter_lds(int NW, bool pay) {
+    const size_t tile = (size_t)rp_tile(NW, pay);
+    return (size_t)NW * tile * 8 + (pay ? tile * 4 : 0) + 16 * 128 * 4 + 16 * 256 * 2 + 256 * 4 + 256 * 8 + 16 * 4 +
+           16;
+}
+
+u64* rp_digit_base(u64* tmp, uint64_t ntiles) {
+    const u64 nchunks = (ntiles + kP3Chunk - 1) / kP3Chunk;
+    return tmp + (ntiles * 256 + 1) / 2 + nchunks * 256;
+}
+
+hipError_t launch_rp_hist(const uint8_t* digs, const uint64_t* w0, int shift, const uint64_t* rstart,
+                          const uint64_t* tpre, int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos,
+                          uint64_t* tmp, int grid, hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    u32* cnt_t = (u32*)tmp;
+    u64* csum = tmp + (ntiles * 256 + 1) / 2;
+    const u64 nchunks = (ntiles + kP3Chunk - 1) / kP3Chunk;
+    u64* dtot = csum + nchunks * 256;
+    const int gu = (int)hmin(ntiles, (u64)grid * 4);
+    hipLaunchKernelGGL(rp_upsweep_k, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)digs, w0, shift, rstart,
+                       tpre, nreg, ntiles, tile, cnt_t);
+    hipLaunchKernelGGL(p3_chunk_sum_k, dim3(nchunks), dim3(256), 0, s, (const u32*)cnt_t, ntiles, csum);
+    hipLaunchKernelGGL(p3_chunk_scan_k, dim3(256), dim3(256), 0, s, csum, nchunks, dtot);
+    hipLaunchKernelGGL(p3_digit_base_k, dim3(1), dim3(256), 0, s, dtot);
+    hipLaunchKernelGGL(p3_chunk_pos_k, dim3(nchunks), dim3(256), 0, s, (const u32*)cnt_t, (const u64*)csum,
+                       (const u64*)dtot, ntiles, pos);
+    return hipGetLastError();
+}
+
+hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t istride, uint64_t* kout,
+                             uint64_t ostride, const uint32_t* pin, uint32_t* pout, const uint64_t* rstart,
+                             const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,
+                             uint8_t* emit, int eshift, int grid, hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    const int g = (int)hmin(ntiles, (u64)grid);
+    const size_t lds = (rp_scatter_lds(NW, pay) + 15) & ~(size_t)15;
+#define KC_RPS(NWV, PAYV)                                                                                          \
+    hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kP3Block), lds, s, kin, istride, kout, ostride, pin, \
+                       pout, rstart, tpre, nreg, ntiles, pos, dshift, (unsigned char*)emit, eshift)
+    if (pay) {
+        switch (NW) {
+        case 1: KC_RPS(1, true); break;
+        case 2: KC_RPS(2, true); break;
+        case 3: KC_RPS(3, true); break;
+        case 4: KC_RPS(4, true); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (NW) {
+        case 1: KC_RPS(1, false); break;
+        case 2: KC_RPS(2, false); break;
+        case 3: KC_RPS(3, false); break;
+        case 4: KC_RPS(4, false); break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+#undef KC_RPS
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// P5 of the skm engine: count_buckets over records. Each wave expands its 64
+// records (one per lane) into a flat key sequence: an exclusive scan of the
+// key counts, then rounds of 64 keys in which a scalar loop walks the owner
+// records of the round (v_readlane broadcasts) and every lane picks the key
+// at its position. Keys then take the LDS table exactly as in count_buckets
+// (home-group fast path, per-wave slow-path queue of (record, key index),
+// sub-range passes, global table and spill at the last level).
+// ---------------------------------------------------------------------------
+
+struct SkmBucketArgs {
+    const u64* recs;  // RW x stride (SoA), grouped by bucket
+    u64 stride;
+    const u64* starts;
+    u32 nbuckets;
+    u32 lcap;
+    u64 last_mask;
+    u64* rec_keys;
+    u32* rec_cnts;
+    u64 rec_cap;
+    u64* rec_cursor;
+    u64* table;
+    u64 cap;
+    u64* spill;
+    u64 spill_cap;
+    u64* spill_ctr;
+    u64* stats;
+    u32 probe_limit;
+    int skip;
+};
+
+// key i of a record (see the record layout above)
+template <int W>
+__device__ __forceinline__ void skm_key(const u64 (&rw)[W + 1], u32 i, u64 last_mask, u64 (&key)[W]) {
+    const u32 o = 16u + 2u * i;
+    const bool hiw = o >= 64u;
+    const u32 sh = o & 63u;
+    u64 ext[W + 2];
+#pragma unroll
+    for (int j = 0; j <= W; j++) ext[j] = rw[j];
+    ext[W + 1] = 0ull;
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        const u64 a0 = hiw ? ext[j + 1] : ext[j];
+        const u64 a1 = hiw ? ext[j + 2] : ext[j + 1];
+        key[j] = sh ? ((a0 << sh) | (a1 >> (64u - sh))) : a0;
+    }
+    key[W - 1] &= last_mask;
+}
+
+constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: record << 6 | key index)
+
+// P5 LDS: table (lcap slots) + misc (48 u32) + per-wave slow-path queues +
+// per-wave record stage (64 records of W + 1 words)
+static size_t skm_fixed_lds(int W) {
+    return 48 * 4 + (size_t)kBucketWaves * kSkmQueue * 8 + (size_t)kBucketWaves * 64 * (W + 1) * 8 + 16;
+}
+
+int skm_lds_slots(int W) {
+    const int per = 8 * W + 4 + (W >= 2 ? 4 : 0);
+    const int slots = (int)((160 * 1024 - 64 - skm_fixed_lds(W)) / per);
+    return slots / 64 * 64;
+}
+
+static size_t skm_bucket_lds_bytes(int W) {
+    const size_t lcap = (size_t)skm_lds_slots(W);
+    return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + skm_fixed_lds(W);
+}
+
+// bases of a record from bit offset o (16 + 2 * key index) as RW words, base
+// o at the top, zeros past the record
+template <int RW>
+__device__ __forceinline__ void skm_window(const u64 (&rec)[RW], u32 o, u64 (&win)[RW]) {
+    const bool hiw = o >= 64u;
+    const u32 sh = o & 63u;
+    u64 ext[RW + 2];
+#pragma unroll
+    for (int j = 0; j < RW; j++) ext[j] = rec[j];
+    ext[RW] = 0ull;
+    ext[RW + 1] = 0ull;
+#pragma unroll
+    for (int j = 0; j < RW; j++) {
+        const u64 a0 = hiw ? ext[j + 1] : ext[j];
+        const u64 a1 = hiw ? ext[j + 2] : ext[j + 1];
+        win[j] = sh ? ((a0 << sh) | (a1 >> (64u - sh))) : a0;
+    }
+}
+
+// 32-bit slot hash of a key (P5 of the skm engine): the LDS group of a key is
+// umulhi(h, groups); lds_insert takes the same position as the 48-bit
+// fraction h << 16
+template <int W>
+__device__ __forceinline__ u32 skm_hash32(const u64 (&key)[W]) {
+    u64 x = key[0];
+#pragma unroll
+    for (int j = 1; j < W; j++) x = (x ^ (x >> 29)) * 0xc2b2ae3d27d4eb4full + key[j];
+    x ^= x >> 31;
+    return ((u32)x ^ (u32)(x >> 32)) * 0x9e3779b1u;
+}
+
+struct SkmLdsTable {
+    u64* lkeys;
+    u32* lcnt;
+    u32* lstate;
+    u32* lfill;
+    u32* labort;
+};
+
+// Slow path for the first c entries of a wave's queue (record << 6 | key):
+// full probing insert into the LDS table, fill/abort accounting, and at the
+// last sub-range level the global table and the spill buffer. Out of line:
+// it runs once per 64 queued keys and keeps the hot loop small.
+template <int W>
+__device__ __noinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t, const u64* wq, u32 c, u64 lo,
+                                       bool last, u32 limit) {
+    constexpr int RW = W + 1;
+    const int lane = (int)lane_id();
+    const bool act = lane < (int)c;
+    u64 qk[W];
+#pragma unroll
+    for (int j = 0; j < W; j++) qk[j] = 0;
+    if (act) {
+        const u64 e = wq[lane];
+        const u64 ri = lo + (e >> 6);
+        u64 rw[RW];
+#pragma unroll
+        for (int j = 0; j < RW; j++) rw[j] = a.recs[(u64)j * a.stride + ri];
+        skm_key<W>(rw, (u32)(e & 63u), a.last_mask, qk);
+    }
+    bool done = true, claimed = false, lclaim = false, full = false;
+    if (act) {
+        const u64 frac = (u64)skm_hash32<W>(qk) << 16;
+        if (!lds_insert<W>(qk, frac, t.lkeys, t.lcnt, t.lstate, a.lcap, last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u),
+                           &lclaim)) {
+            if (!last) {
+                full = true;
+            } else if constexpr (W == 1) {
+                done = insert_w1(qk[0], a.table, a.cap, a.probe_limit, &claimed);
+            } else {
+                done = insert_wide<W>(qk, a.table, a.cap, a.probe_limit, &claimed);
+            }
+        }
+    }
+    const u64 lm = __ballot(lclaim);
+    const u64 fm = __ballot(full);
+    if (!last && (lm || fm) && lane == 0) {
+        u32 f = atomicAdd(t.lfill, (u32)__popcll(lm)) + (u32)__popcll(lm);
+        if (fm || f > limit) atomicOr(t.labort, 1u);
+    }
+    if (last) {
+        u64 cm = __ballot(claimed);
+        if (cm && lane == __ffsll((long long)cm) - 1)
+            atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
+        bool spill = !done;
+        if (__ballot(spill)) {
+            u64 idx = wave_reserve(a.spill_ctr, spill);
+            if (spill) {
+                if (idx < a.spill_cap) {
+#pragma unroll
+                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = qk[j];
+                } else {
+                    atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
+                }
+            }
+        }
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
+    constexpr int RW = W + 1;
+    constexpr int PD = 4;  // record batches in flight
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* lkeys = (u64*)smem;                         // W x lcap
+    u32* lcnt = (u32*)(lkeys + (size_t)W * a.lcap);  // lcap
+    u32* lstate = lcnt + a.lcap;                     // lcap (W >= 2)
+    u32* misc = lstate + (W >= 2 ? a.lcap : 0);      // base (2 @16), fill, abort, next, kscan, wave totals (16 @24)
+    u32* lfill = misc + 20;
+    u32* labort = misc + 21;
+    u32* lnext = misc + 22;
+    u32* lkscan = misc + 23;  // keys of an aborted pass scanned (abort estimate)
+    u32* wtot_l = misc + 24;
+    const int tid = threadIdx.x;
+    const int lane = (int)lane_id();
+    const u64 lane_lt = lanemask_lt();
+    u64* wq = (u64*)(misc + 48) + (tid >> 6) * kSkmQueue;
+    u64* wst = (u64*)(misc + 48) + kBucketWaves * kSkmQueue + (tid >> 6) * 64 * RW;  // this wave's record stage
+    const SkmLdsTable tab = {lkeys, lcnt, lstate, lfill, labort};
+    for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+#pragma unroll
+        for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+        lcnt[i] = 0;
+        if constexpr (W >= 2) lstate[i] = 0;
+    }
+    if (tid == 0) {
+        *lfill = 0;
+        *labort = 0;
+        *lkscan = 0;
+    }
+    __syncthreads();
+    const u32 limit = (a.lcap * 13u) >> 4;
+    const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;
+    const u32 ng = a.lcap >> 2;
+    const bool grouped = W == 1 && (a.lcap & 3u) == 0;
+    constexpr u64 M48 = 0xffffffffffffull;
+    for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        if (tid == 0)
+            *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) &
+                           ERR_REC_OVERFLOW);
+        __syncthreads();
+        const bool stop = *lnext != 0u;
+        __syncthreads();
+        if (stop) return;
+        const u64 lo = a.starts[b], hi = a.starts[b + 1];
+        u32 m = 1, sub = 0;
+        while (sub < m) {
+            const bool last = m >= mmax;
+            u64 scanned = 0;
+            u32 my_keys = 0;
+            u32 qn = 0;
+            // records of the next PD batches (one per thread per batch) in flight
+            u64 pf[PD][RW];
+#pragma unroll
+            for (int d = 0; d < PD; d++) {
+                const u64 i = lo + (u64)d * kBucketBlock + tid;
+#pragma unroll
+                for (int j = 0; j < RW; j++) pf[d][j] = i < hi ? a.recs[(u64)j * a.stride + i] : 0ull;
+            }
+            for (u64 base = lo; base < hi; base += (u64)kBucketBlock) {
+                if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                scanned += (u64)kBucketBlock;
+                // this batch's record -> the wave's LDS stage; next loads issued
+#pragma unroll
+                for (int j = 0; j < RW; j++) wst[(size_t)lane * RW + j] = pf[0][j];
+                const u32 n = (u32)(pf[0][RW - 1] & 63u);
+#pragma unroll
+                for (int d = 0; d + 1 < PD; d++)
+#pragma unroll
+                    for (int j = 0; j < RW; j++) pf[d][j] = pf[d + 1][j];
+                {
+                    const u64 i = base + (u64)PD * kBucketBlock + tid;
+#pragma unroll
+                    for (int j = 0; j < RW; j++) pf[PD - 1][j] = i < hi ? a.recs[(u64)j * a.stride + i] : 0ull;
+                }
+                // the wave's keys as one flat sequence: exclusive scan of the
+                // records' key counts; lane l takes keys [l*per, l*per + per)
+                u32 inc = n;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const u32 y = __shfl_up(inc, o);
+                    if (lane >= o) inc += y;
+                }
+                const u32 excl = inc - n;
+                const u32 T = (u32)__builtin_amdgcn_readlane((int)inc, 63);
+                if (T == 0) continue;
+                const u32 per = (T + 63) >> 6;
+                const u32 s0 = min(T, (u32)lane * per), s1 = min(T, s0 + per);
+                // owner of key s0: the last record whose first key is <= s0
+                int o = 0;
+#pragma unroll
+                for (int st = 32; st >= 1; st >>= 1) {
+                    const u32 e = (u32)__shfl((int)excl, o + st);
+                    if (e <= s0) o += st;
+                }
+                u32 ki = s0 - (u32)__shfl((int)excl, o);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                u64 cur[RW];
+#pragma unroll
+                for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
+                u32 nn = (u32)(cur[RW - 1] & 63u);
+                u64 win[RW];
+                skm_window<RW>(cur, 16u + 2u * ki, win);
+                const u64 wrec0 = base + (u64)(tid - lane) - lo;  // lane 0's record of this batch
+                for (u32 t = 0; t < per; t++) {
+                    const bool act = s0 + t < s1;
+                    u64 key[W];
+#pragma unroll
+                    for (int j = 0; j < W; j++) key[j] = win[j];
+                    key[W - 1] &= a.last_mask;
+                    bool want = act && !a.skip;
+                    if (m > 1) want = want && (u32)(((key[0] & M48) * (u64)m) >> 48) == sub;
+                    my_keys += want ? 1u : 0u;
+                    bool found = false;
+                    const u32 h = skm_hash32<W>(key);
+                    if (grouped) {
+                        const u32 g = __umulhi(h, ng);
+                        const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
+                        const v2u64 a0 = gp[0], a1 = gp[1];
+                        const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
+                        int hit = -1, emp = -1;
+#pragma unroll
+                        for (int i = 3; i >= 0; i--) {
+                            if (v[i] == key[0]) hit = i;
+                            if (v[i] == 0ull) emp = i;
+                        }
+                        found = want && hit >= 0 && (emp < 0 || hit < emp);
+                        if (found) atomicAdd(&lcnt[4 * g + hit], 1u);
+                    } else if constexpr (W >= 2) {
+                        const u32 sl = __umulhi(h, a.lcap);
+                        if (__hip_atomic_load(&lstate[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
+                            bool eq = true;
+#pragma unroll
+                            for (int j = 0; j < W; j++) eq = eq && lkeys[(size_t)j * a.lcap + sl] == key[j];
+                            found = want && eq;
+                            if (found) atomicAdd(&lcnt[sl], 1u);
+                        }
+                    }
+                    const bool pend = want && !found;
+                    const u64 pb = __ballot(pend);
+                    if (pb) {
+                        if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = ((wrec0 + (u64)o) << 6) | ki;
+                        qn += (u32)__popcll(pb);
+                        if (qn >= 64) {
+                            skm_drain<W>(a, tab, wq, 64, lo, last, limit);
+                            const u32 rest = qn - 64;
+                            const u64 keep = lane < (int)rest ? wq[64 + lane] : 0ull;
+                            if (lane < (int)rest) wq[lane] = keep;
+                            qn = rest;
+                        }
+                    }
+                    // next key: roll one base in; past the record's last key
+                    // move to the next record with keys (the stage of this wave)
+#pragma unroll
+                    for (int j = 0; j < RW - 1; j++) win[j] = (win[j] << 2) | (win[j + 1] >> 62);
+                    win[RW - 1] <<= 2;
+                    ++ki;
+                    if (ki == nn && s0 + t + 1 < s1) {
+                        do {
+                            ++o;
+#pragma unroll
+                            for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
+                            nn = (u32)(cur[RW - 1] & 63u);
+                        } while (nn == 0u);
+                        skm_window<RW>(cur, 16u, win);
+                        ki = 0;
+                    }
+                }
+            }
+            if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                skm_drain<W>(a, tab, wq, qn, lo, last, limit);
+            __syncthreads();
+            const bool aborted = *labort != 0u;
+            if (aborted && my_keys) atomicAdd(lkscan, my_keys);
+            __syncthreads();
+            if (aborted) {
+                if (tid == 0) {
+                    // distinct keys of the bucket, extrapolated from the scanned
+                    // fraction f of its records: linear when keys repeat rarely
+                    // in the scanned part, ~all seen already when they repeat
+                    // often (genome coverage)
+                    const u64 nrec_b = hi - lo;
+                    const float f = (float)min(scanned, nrec_b) / (float)(nrec_b ? nrec_b : 1);
+                    const float rep = (float)(*lkscan) / (float)(*lfill ? *lfill : 1u);
+                    const float seen = rep >= 4.f ? 1.f : (rep >= 2.f ? fmaxf(f, 0.5f) : fmaxf(f, 1e-6f));
+                    const u64 est = (u64)((float)(*lfill) * (float)m / seen);
+                    *lkscan = 0;
+                    u32 nm = m * 2;
+                    while (nm < mmax && (u64)nm * ((u64)limit * 7 / 8) < est) nm *= 2;
+                    *lnext = nm < mmax ? nm : mmax;
+                    *lfill = 0;
+                    *labort = 0;
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_ABORTS], 1ull);
+                    atomicMax((unsigned long long*)&a.stats[ST_P5_MAXM], (unsigned long long)*lnext);
+                }
+                for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
+#pragma unroll
+                    for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+                    lcnt[i] = 0;
+                    if constexpr (W >= 2) lstate[i] = 0;
+                }
+                __syncthreads();
+                const u32 nm = *lnext;
+                sub *= nm / m;
+                m = nm;
+                __syncthreads();
+                continue;
+            }
+            {
+                const int wave = tid >> 6;
+                const u32 spw = (a.lcap + kBucketWaves - 1) / kBucketWaves;
+                const u32 s0 = (u32)wave * spw;
+                const u32 s1 = min(a.lcap, s0 + spw);
+                u32 wc = 0;
+                for (u32 c0 = s0; c0 < s1; c0 += 64) {
+                    const u32 i = c0 + (u32)lane;
+                    const bool occ = i < s1 && ((W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u));
+                    wc += (u32)__popcll(__ballot(occ));
+                }
+                if (lane == 0) wtot_l[wave] = wc;
+                __syncthreads();
+                u32 total = 0, before = 0;
+                for (int w = 0; w < kBucketWaves; w++) {
+                    const u32 v = wtot_l[w];
+                    before += w < wave ? v : 0u;
+                    total += v;
+                }
+                if (tid == 0) {
+                    u64 rbase = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
+                    *(u64*)(misc + 16) = rbase;
+                    if (rbase + total > a.rec_cap)
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                    *lfill = 0;
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                }
+                __syncthreads();
+                u64 pos = *(u64*)(misc + 16) + before;
+                for (u32 c0 = s0; c0 < s1; c0 += 64) {
+                    const u32 i = c0 + (u32)lane;
+                    const bool occ = i < s1 && ((W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u));
+                    const u64 bm = __ballot(occ);
+                    if (occ) {
+                        const u64 qq = pos + (u64)__popcll(bm & lane_lt);
+                        if (qq < a.rec_cap) {
+#pragma unroll
+                            for (int j = 0; j < W; j++)
+                                a.rec_keys[(u64)j * a.rec_cap + qq] = lkeys[(size_t)j * a.lcap + i];
+                            a.rec_cnts[qq] = lcnt[i];
+                        }
+#pragma unroll
+                        for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
+                        lcnt[i] = 0;
+                        if constexpr (W >= 2) lstate[i] = 0;
+                    }
+                    pos += (u64)__popcll(bm);
+                }
+            }
+            __syncthreads();
+            ++sub;
+        }
+    }
+}
+
+hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride, const uint64_t* starts,
+                            uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                            uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
+                            uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s) {
+    SkmBucketArgs a;
+    {
+        const char* e = getenv("KC_P5_SKIP");
+        a.skip = e ? atoi(e) : 0;
+    }
+    const bool mask_last = ((k + 3) / 4) < 8 * W;
+    a.last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
+    a.recs = recs;
+    a.stride = stride;
+    a.starts = starts;
+    a.nbuckets = nbuckets;
+    a.lcap = (lcap == 0 || lcap > (u32)skm_lds_slots(W)) ? (u32)skm_lds_slots(W) : lcap;
+    a.rec_keys = rec_keys;
+    a.rec_cnts = rec_cnts;
+    a.rec_cap = rec_cap;
+    a.rec_cursor = rec_cursor;
+    a.table = table;
+    a.cap = cap;
+    a.spill = spill;
+    a.spill_cap = spill_cap;
+    a.spill_ctr = stats + ST_SPILL2_FILL;
+    a.stats = stats;
+    a.probe_limit = probe_limit;
+    const size_t lds = (skm_bucket_lds_bytes(W) + 15) & ~(size_t)15;
+    switch (W) {
+    case 1: hipLaunchKernelGGL(count_skm_k<1>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(count_skm_k<2>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    case 3: hipLaunchKernelGGL(count_skm_k<3>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+int seg_sort_cap(int W) {
+    switch (W) {
+    case 1: return SegCfg<1>::CAP;
+    case 2: return SegCfg<2>::CAP;
+    case 3: return SegCfg<3>::CAP;
+    default: return SegCfg<4>::CAP;
+    }
+}

@@ -21,7 +21,7 @@ def _fq(reads):
     return "".join(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n" for i, s in enumerate(reads))
 
 
-@pytest.fixture(params=["partition", "table"])
+@pytest.fixture(params=["partition", "table", "skm"])
 def engine(request):
     return request.param
 

@@ -1,0 +1,107 @@
+"""GPU parity of the super-k-mer engine (engine="skm", kc_skm.inl) against the
+CPU oracle, bit-exact SortedKMerFile bytes, on the shapes that reach its
+special paths: the grouped finish (>= 65536 records), P5 sub-range passes,
+several batches, the pool-overflow retry, runs longer than nmax (tandem
+repeats keep one minimizer), prefix skew beyond the segment sort, and every
+record width (W = 1..3, K' = k or 32W). Needs an MI355X."""
+import os
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _fq(reads):
+    return "".join(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n" for i, s in enumerate(reads)).encode()
+
+
+@pytest.mark.parametrize("k,L", [(18, 60), (19, 100), (21, 100), (28, 150), (29, 150), (31, 150), (32, 150),
+                                 (33, 150), (55, 150), (60, 150), (64, 150), (65, 160), (96, 150)])
+def test_skm_grouped_finish(kca, orc, k, L):
+    n = 4_000_000 // L
+    fq = kca.synth_fastq(n, L, seed=100 + k, n_rate=0.001)
+    with kca.Context(kmer_length=k, line_length=L, engine="skm") as ctx:
+        assert ctx.count_fastq(fq) == n
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["output_records"] >= 65536
+    assert got == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("k,slots", [(31, 64), (31, 256), (55, 64), (96, 128)])
+def test_skm_subrange_passes(kca, orc, k, slots):
+    fq = kca.synth_fastq(30000, 150, seed=k + slots, n_rate=0.0005)
+    with kca.Context(kmer_length=k, line_length=150, lds_slots=slots, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert got == orc.count_fastq(fq, k)
+    assert st["spilled_kmers"] == 0
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_skm_many_batches(kca, orc, k):
+    fq = kca.synth_fastq(60000, 150, seed=21, genome_length=300_000, n_rate=0.0005)
+    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=1 << 21, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["batches"] > 3
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_skm_pool_overflow_retry(kca, orc, monkeypatch):
+    """A pool smaller than one batch's records: the batch is undone and
+    retried with fewer reads until it fits; statistics are not double counted."""
+    monkeypatch.setenv("KC_SKM_POOL_CAP", "20000")
+    fq = kca.synth_fastq(20000, 150, seed=5, n_rate=0.002)
+    with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["batches"] > 1
+    assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
+    assert got == orc.count_fastq(fq, 31)
+
+
+@pytest.mark.parametrize("k", [19, 31, 55])
+def test_skm_tandem_repeats_split_long_runs(kca, orc, k):
+    """Tandem repeats keep one minimizer value across many windows, so runs
+    exceed nmax and are split into several records."""
+    rng = random.Random(k)
+    reads = []
+    for i in range(3000):
+        unit = "".join(rng.choice("ACGT") for _ in range(rng.choice([1, 2, 3, 5, 7])))
+        s = (unit * 200)[:150]
+        if i % 3 == 0:
+            s = s[:70] + "".join(rng.choice("ACGT") for _ in range(80))
+        reads.append(s)
+    fq = _fq(reads)
+    with kca.Context(kmer_length=k, line_length=150, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_skm_prefix_skew_falls_back_to_radix(kca, orc, k):
+    """Every read starts with the same 8 bases: > seg_sort capacity distinct
+    keys share one 16-bit prefix, so the finish takes the radix sort."""
+    rng = random.Random(7 * k)
+    reads = ["ACGTACGA" + "".join(rng.choice("ACGT") for _ in range(142)) for _ in range(30000)]
+    fq = _fq(reads)
+    with kca.Context(kmer_length=k, line_length=150, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_skm_genome_reads_multi_block(kca, orc):
+    blocks = [kca.synth_fastq(40000, 150, seed=2, genome_length=1_000_000, first_read=i * 40000) for i in range(3)]
+    with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
+        for b in blocks:
+            ctx.count_fastq(b)
+        got = ctx.records()
+    want, _ = orc.refcpu(b"".join(blocks), 31, threads=8)
+    assert got == want
