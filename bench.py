@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--genome", type=int, default=None, help="0 = iid uniform reads")
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--mem", type=int, default=None, help="gpuMemoryLimit per GPU (bytes)")
-    ap.add_argument("--engine", default="partition", choices=["partition", "table", "skm"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "skm", "partition", "table"])
     ap.add_argument("--cpu-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
@@ -207,17 +207,34 @@ def main():
     keys_step = st["keys"] or windows_step  # ctx stats are per step (reset at each step)
     recs_step = st["output_records"]
     kernels = {}
-    if args.engine == "partition":
+    used = st.get("engines_used", 0)
+    if used & 1:
+        # super-k-mer engine: F reads the encoded reads (6 B per 16 bases) and
+        # writes the records (8(W+1) B each); each of the two grouping scatters
+        # reads and writes every record; P5 reads the records and writes the
+        # distinct (key, count) records
+        rec_step = st["keys"] or 1  # records handed out by F per step
+        rb = 8 * (W + 1)
         p5_per_step = max(1, st["p5_launches"])
         specs = [
-            ("P2", f"count_front<{W},SINK_SCATTER,CODES>", part_ms[1], launches, windows_step,
+            ("F", f"skm_front_k<{W}>", part_ms[1], launches, windows_step, "k-mers",
+             (G * 6) / max(1, L - k + 1) + rb * rec_step / windows_step),
+            ("S", f"rp_scatter_k<{W + 1},false>", part_ms[2], 2 * steps * st["batches"], rec_step, "records",
+             2 * rb + 1),
+            ("P5", f"count_skm_k<{W}>", part_ms[4], steps * p5_per_step, rec_step, "records",
+             rb + (8 * W + 4) * recs_step / rec_step),
+        ]
+    elif used & 2:
+        p5_per_step = max(1, st["p5_launches"])
+        specs = [
+            ("P2", f"count_front<{W},2,true,1024>", part_ms[1], launches, windows_step,
              "k-mers", (G * 6) / max(1, L - k + 1) + 8 * W),
             ("P3", f"p3_scatter_k<{W}>", part_ms[2], steps * st["batches"], keys_step, "keys", 16 * W),
             ("P5", f"count_buckets<{W}>", part_ms[4], steps * p5_per_step, keys_step, "keys",
              8 * W + (8 * W + 4) * recs_step / max(1, keys_step)),
         ]
     else:
-        specs = [("insert", f"count_front<{W},SINK_TABLE>", insert_ms, launches, windows_step, "k-mers",
+        specs = [("insert", f"count_front<{W},0,false,256>", insert_ms, launches, windows_step, "k-mers",
                   nbytes / windows_per_gpu + 8 * W + 8)]
     for tag, name, ms_total, nl, units_step, unit_name, bpu in specs:
         nl = max(1, nl)
@@ -232,7 +249,7 @@ def main():
     traffic = load_traffic()
     t_bytes = None
     if traffic and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
-        t_bytes = traffic.get("kernels", {}).get(dom, {}).get("bytes_per_launch")
+        t_bytes = traffic.get("kernels", {}).get(d["kernel"].replace(" ", ""), {}).get("bytes_per_launch")
     b_path = nbytes / windows_per_gpu + 8 * W + 8
     step_s = elapsed / args.steps
     path_achieved = b_path * windows_per_gpu / step_s / 1e9
@@ -275,7 +292,8 @@ def main():
                                       "finish": finish_ms / args.steps,
                                       "exchange_rank0": xch_ms[0] / args.steps,
                                       "partition_passes": [round(x / args.steps, 3) for x in part_ms]},
-            "engine": args.engine,
+            "engine": args.engine, "engines_used": {1: "skm", 2: "key-prefix partition", 3: "skm + key-prefix",
+                                                    4: "table"}.get(st.get("engines_used", 0), str(st.get("engines_used"))),
             "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"],
         }
         print(json.dumps(line), flush=True)

@@ -94,15 +94,22 @@ typedef struct kc_config {
 
 #define KC_FLAG_NONE 0u
 #define KC_FLAG_QUIET 1u        /* no progress lines on stderr */
-#define KC_FLAG_ENGINE_TABLE 2u /* count with the global atomic hash table only
-                                   (default engine: hash-partition the k-mers into
-                                   65536 buckets and count each in an LDS table;
-                                   the global table catches LDS overflow) */
-#define KC_FLAG_ENGINE_SKM 4u   /* super-k-mer engine: runs of consecutive windows
-                                   sharing a minimizer bucket move through HBM as
-                                   one record of bases (~1.5 B per k-mer at k=31
-                                   instead of an 8-byte key); for 18 <= k <= 96,
-                                   other (L, k) fall back to the default engine */
+#define KC_FLAG_ENGINE_TABLE 2u  /* count with the global atomic hash table only */
+#define KC_FLAG_ENGINE_SKM 4u    /* super-k-mer engine without the cardinality
+                                    check (see below) */
+#define KC_FLAG_ENGINE_PREFIX 8u /* key-prefix partition engine only: hash-free
+                                    65536 buckets by the first 8 bases, each
+                                    counted in an LDS table; sorted output needs
+                                    no global sort */
+/* Default engine (no ENGINE flag): the super-k-mer engine. Runs of consecutive
+ * windows that share a minimizer bucket move through HBM as one record of
+ * bases (~1.5 B per k-mer at k=31 instead of an 8-byte key), are grouped by
+ * bucket and counted per bucket in an LDS table. Before counting a large
+ * batch it counts a sample of buckets; when most sampled keys are distinct
+ * (no coverage, e.g. iid reads) the key-prefix engine counts the batch and the
+ * rest of the context's input instead. (L, k) outside its range (k < 18,
+ * k > 96, reads > 4096 + k - 1 bases) use the key-prefix engine. Every engine
+ * gives the same bytes. */
 
 typedef struct kc_stats {
     uint64_t reads;            /* reads counted so far */
@@ -127,6 +134,9 @@ typedef struct kc_stats {
     uint64_t keys;             /* partition engine: keys partitioned (valid,
                                   non-zero windows) since the last reset */
     uint64_t p5_launches;      /* P5 launches (reruns on record overflow included) */
+    uint32_t engines_used;     /* bit 0: super-k-mer, bit 1: key-prefix partition,
+                                  bit 2: global table (batches since the last reset) */
+    uint32_t reserved1;
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". */

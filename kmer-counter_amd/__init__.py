@@ -73,6 +73,8 @@ class Stats(ctypes.Structure):
         ("batches", ctypes.c_uint64),
         ("keys", ctypes.c_uint64),
         ("p5_launches", ctypes.c_uint64),
+        ("engines_used", ctypes.c_uint32),
+        ("reserved1", ctypes.c_uint32),
     ]
 
     def as_dict(self):
@@ -181,16 +183,17 @@ class Context:
 
     def __init__(self, kmer_length: int, line_length: int = 0, device: int = 0,
                  gpu_memory_limit: int = 100000000, table_bytes: int = 0, temp_dir: Optional[str] = None,
-                 quiet: bool = True, engine: str = "partition", lds_slots: int = 0):
+                 quiet: bool = True, engine: str = "auto", lds_slots: int = 0):
         self._L = lib()
         self.k = kmer_length
         self.W = (kmer_length + 31) // 32
         self.rs = 8 * self.W + 4
         self._device = device
         self._tmp = temp_dir.encode() if temp_dir else None
-        if engine not in ("partition", "table", "skm"):
-            raise ValueError("engine must be 'partition', 'table' or 'skm'")
-        flags = (1 if quiet else 0) | (2 if engine == "table" else 0) | (4 if engine == "skm" else 0)
+        engine_flags = {"auto": 0, "table": 2, "skm": 4, "partition": 8}
+        if engine not in engine_flags:
+            raise ValueError("engine must be 'auto', 'skm', 'partition' or 'table'")
+        flags = (1 if quiet else 0) | engine_flags[engine]
         cfg = _Config(device, 0, kmer_length, line_length or kmer_length, int(gpu_memory_limit), int(table_bytes),
                       self._tmp, flags, int(lds_slots))
         h = ctypes.c_void_p()

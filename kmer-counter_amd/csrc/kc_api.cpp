@@ -60,6 +60,10 @@ struct kc_ctx {
     bool part = true;
     bool skm = false;              // KC_FLAG_ENGINE_SKM: super-k-mer records instead of keys
     bool skm_used = false;         // a batch went through the skm engine since the last reset
+    bool skm_force = false;        // KC_FLAG_ENGINE_SKM: no cardinality sample
+    bool skm_checked = false;      // the skm cardinality sample has run since the last reset
+    uint32_t engines_used = 0;     // kc_stats.engines_used
+    bool skm_hc = false;           // high cardinality seen: the key-prefix engine counts
     uint64_t* pool_cursor = nullptr;  // device u64: skm pool allocator
     uint64_t key_cap = 0;          // keys per batch
     uint64_t* keys_a = nullptr;    // W x key_cap
@@ -319,6 +323,7 @@ static kc_status count_reads_table(kc_ctx* c, const uint8_t* base, const uint64_
     }
     c->st.insert_ms += ms;
     c->st.last_count_ms = ms;
+    c->engines_used |= 4u;
     c->st.reads += n_reads;
     c->st.windows += n_reads * nw;
     c->st.valid_kmers = c->stats_h[ST_VALID];
@@ -353,6 +358,12 @@ static kc_status grow_records(kc_ctx* c, uint64_t need) {
 static const int kBucketBits = 16;
 static const size_t kMaxLds = 160 * 1024;  // LDS of one CU (gfx950): the P2 workgroup's ceiling
 static const uint64_t kDescCap = 1u << 20;  // P5 segment descriptors kept for the sorted finish
+// skm engine cardinality sample: buckets counted first, the smallest batch
+// (keys) sampled, and the distinct-key share above which the key-prefix engine
+// counts instead
+static const uint32_t kSkmSample = 256;
+static const uint64_t kSkmSampleMinKeys = 1ull << 24;
+static const double kSkmDistinctMax = 0.35;
 
 // Engine "partition": per batch of reads
 //   P1 hist   : digit (word0 >> 48) & 255 per segment of reads
@@ -525,6 +536,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             return s;
         }
         c->batches++;
+        c->engines_used |= 2u;
         done += nr;
     }
     c->st.reads += n_reads;
@@ -672,7 +684,11 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             max_reads = nr / 2;
             continue;
         }
-        c->skm_used = true;
+        if (getenv("KC_F_SKIP")) {  // timing experiment: records are invalid, stop after F
+            c->batches++;
+            done += nr;
+            continue;
+        }
         if (np > 0) {
             double gm[2] = {0, 0};
             if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, c->keys_b, pool_cap, nullptr, c->digs, np,
@@ -690,41 +706,80 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
             c->part_ms[3] += t;
-            uint64_t bound = (uint64_t)nb * (uint64_t)skm_lds_slots(W);
             const uint64_t kbound = nr * nw;
-            if (bound > kbound) bound = kbound;
-            const uint64_t rec0 = c->rec_n;
-            const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
-            for (;;) {
-                if ((s = grow_records(c, rec0 + bound))) return s;
-                // keys_b is free after S2: it takes P5's spills (W x key_cap words)
-                HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-                HIPCHK(c, launch_count_skm(W, (int)c->k, c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, nb,
-                                           c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
-                                           c->keys_b, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots, c->n_cu,
-                                           c->stream));
-                HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-                HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
-                if ((s = sync_stats(c))) return s;
-                HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-                c->part_ms[4] += t;
-                c->p5_launches++;
-                if (getenv("KC_DEBUG"))
-                    fprintf(stderr, "kc: skm F records=%llu P5 passes=%llu aborts=%llu max_m=%llu records=%llu %.3f ms\n",
-                            (unsigned long long)np, (unsigned long long)c->stats_h[ST_P5_PASSES],
-                            (unsigned long long)c->stats_h[ST_P5_ABORTS], (unsigned long long)c->stats_h[ST_P5_MAXM],
-                            (unsigned long long)c->rec_n, t);
-                if (!(c->stats_h[ST_ERR] & ERR_REC_OVERFLOW)) break;
-                if (bound >= kbound || c->stats_h[ST_CLAIMED] != claimed0 || c->stats_h[ST_SPILL2_FILL])
-                    return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
-                bound = kbound;
-                uint64_t err = c->stats_h[ST_ERR] & ~(uint64_t)ERR_REC_OVERFLOW;
-                HIPCHK(c, hipMemcpyAsync(c->stats + ST_ERR, &err, 8, hipMemcpyHostToDevice, c->stream));
-                HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec0, 8, hipMemcpyHostToDevice, c->stream));
-                HIPCHK(c, hipStreamSynchronize(c->stream));
-                c->stats_h[ST_ERR] = err;
-                c->rec_n = rec0;
+            const uint64_t rec_batch0 = c->rec_n;
+            // P5 over buckets [b0, b1); reruns with a bigger record buffer on
+            // overflow (safe while nothing went to the global table or spill)
+            auto p5_range = [&](uint32_t b0, uint32_t b1, bool count_keys) -> kc_status {
+                uint64_t bound = (uint64_t)(b1 - b0) * (uint64_t)skm_lds_slots(W);
+                if (bound > kbound) bound = kbound;
+                const uint64_t rec0 = c->rec_n;
+                const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
+                kc_status s2;
+                for (;;) {
+                    if ((s2 = grow_records(c, rec0 + bound))) return s2;
+                    // keys_b is free after S2: it takes P5's spills (W x key_cap words)
+                    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                    HIPCHK(c, launch_count_skm(W, (int)c->k, c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p,
+                                               b0, b1, count_keys, c->rec_keys, c->rec_cnts, c->rec_cap,
+                                               c->rec_cursor, c->table, c->cap, c->keys_b, c->key_cap, c->stats,
+                                               l.probe_limit, c->cfg.lds_slots, c->n_cu, c->stream));
+                    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                    HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+                    if ((s2 = sync_stats(c))) return s2;
+                    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                    c->part_ms[4] += t;
+                    c->p5_launches++;
+                    if (getenv("KC_DEBUG"))
+                        fprintf(stderr,
+                                "kc: skm F records=%llu P5[%u,%u) passes=%llu aborts=%llu max_m=%llu records=%llu %.3f ms\n",
+                                (unsigned long long)np, b0, b1, (unsigned long long)c->stats_h[ST_P5_PASSES],
+                                (unsigned long long)c->stats_h[ST_P5_ABORTS],
+                                (unsigned long long)c->stats_h[ST_P5_MAXM], (unsigned long long)c->rec_n, t);
+                    if (!(c->stats_h[ST_ERR] & ERR_REC_OVERFLOW)) return KC_OK;
+                    if (bound >= kbound || c->stats_h[ST_CLAIMED] != claimed0 || c->stats_h[ST_SPILL2_FILL])
+                        return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
+                    bound = kbound;
+                    uint64_t err = c->stats_h[ST_ERR] & ~(uint64_t)ERR_REC_OVERFLOW;
+                    HIPCHK(c, hipMemcpyAsync(c->stats + ST_ERR, &err, 8, hipMemcpyHostToDevice, c->stream));
+                    HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec0, 8, hipMemcpyHostToDevice, c->stream));
+                    HIPCHK(c, hipStreamSynchronize(c->stream));
+                    c->stats_h[ST_ERR] = err;
+                    c->rec_n = rec0;
+                }
+            };
+            // bucket 0xffff holds only the pool's padding records. Unless this
+            // context already knows its data, the first kSkmSample buckets are
+            // counted alone: if most of their keys are distinct (iid reads, no
+            // coverage) the key-prefix engine takes this batch and the rest,
+            // whose sorted finish needs no global sort
+            const uint32_t nbk = nb - 1;
+            uint32_t bs = 0;
+            if (!c->skm_force && !c->skm_checked && kbound >= kSkmSampleMinKeys) {
+                bs = kSkmSample;
+                if ((s = p5_range(0, bs, true))) return s;
+                c->skm_checked = true;
+                const uint64_t keys_s = c->stats_h[ST_P5_KEYS], dist_s = c->rec_n - rec_batch0;
+                if (keys_s > 0 && (double)dist_s > kSkmDistinctMax * (double)keys_s &&
+                    c->stats_h[ST_CLAIMED] == saved[ST_CLAIMED] && c->stats_h[ST_SPILL2_FILL] == 0) {
+                    HIPCHK(c, hipMemcpyAsync(c->stats, saved.data(), ST_N * 8, hipMemcpyHostToDevice, c->stream));
+                    HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec_batch0, 8, hipMemcpyHostToDevice, c->stream));
+                    HIPCHK(c, hipStreamSynchronize(c->stream));
+                    memcpy(c->stats_h, saved.data(), ST_N * 8);
+                    c->rec_n = rec_batch0;
+                    c->skm_hc = true;
+                    c->st.reads += done;
+                    c->st.windows += done * nw;
+                    if (getenv("KC_DEBUG"))
+                        fprintf(stderr, "kc: skm sample %llu distinct / %llu keys: key-prefix engine\n",
+                                (unsigned long long)dist_s, (unsigned long long)keys_s);
+                    return count_reads_part(c, seq_off ? base : base + done * (uint64_t)L,
+                                            seq_off ? seq_off + done : nullptr, n_reads - done, L);
+                }
             }
+            if ((s = p5_range(bs, nbk, false))) return s;
+            c->skm_used = true;
+            c->engines_used |= 1u;
             if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
             uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
             if (n2) {
@@ -749,7 +804,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
 static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
-    if (c->skm) {
+    if (c->skm && !c->skm_hc) {
         const SkmGeom g = skm_geometry((int)L, (int)c->k);
         if (g.ok) return count_reads_skm(c, base, seq_off, n_reads, L, g);
     }
@@ -862,7 +917,8 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
     if (M < (1u << 20)) M = 1u << 20;
     c->part = (cfg->flags & KC_FLAG_ENGINE_TABLE) == 0;
-    c->skm = c->part && (cfg->flags & KC_FLAG_ENGINE_SKM) != 0;
+    c->skm = c->part && (cfg->flags & KC_FLAG_ENGINE_PREFIX) == 0;
+    c->skm_force = (cfg->flags & KC_FLAG_ENGINE_SKM) != 0;
     size_t slot_bytes = 8 * (size_t)slot_words(c->W);
     size_t spill_bytes, tbytes;
     if (c->part) {
@@ -961,6 +1017,9 @@ kc_status kc_reset(kc_ctx* c) {
     c->part_keys = 0;
     c->p5_launches = 0;
     c->skm_used = false;
+    c->skm_checked = false;
+    c->skm_hc = false;
+    c->engines_used = 0;
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
@@ -1442,6 +1501,7 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     out->table_capacity = c->cap;
     out->valid_kmers = c->stats_h[ST_VALID];
     out->spill_runs = c->runs.size();
+    out->engines_used = c->engines_used;
     return KC_OK;
 }
 

@@ -20,6 +20,7 @@ enum Stat : int {
     ST_P5_ABORTS = 9,    // P5 passes aborted on a full LDS table (diagnostic)
     ST_P5_MAXM = 10,     // largest sub-range split m used (diagnostic)
     ST_DESC_FILL = 11,   // P5 segment descriptors written (may exceed capacity)
+    ST_P5_KEYS = 12,     // skm P5 sample launch: keys of the sampled buckets
     ST_N = 16
 };
 
@@ -196,6 +197,7 @@ struct SkmGeom {
     int Kp;         // key span in bases (k, or 32W when the last word is not masked)
     int nmax;       // keys per record at most
     int R, NG, HS;  // F tile: reads, code groups per read, m-mer hash slots per read
+    int hq;         // F: m-mer positions per hash item
     size_t lds;     // F dynamic LDS bytes
 };
 SkmGeom skm_geometry(int L, int k);
@@ -217,8 +219,9 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
                              uint8_t* emit, int eshift, int grid, hipStream_t s);
 int skm_lds_slots(int W);
 int seg_sort_cap(int W);  // longest segment seg_sort_k takes
+// buckets [b0, b1); count_keys: add the buckets' key counts to stats[ST_P5_KEYS]
 hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride, const uint64_t* starts,
-                            uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                            uint32_t b0, uint32_t b1, bool count_keys, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
                             uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s);
 

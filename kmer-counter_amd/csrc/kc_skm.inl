@@ -33,15 +33,15 @@
 //                         other bytes 3, bases past the read end 0), where K'
 //                         is the key span (k when the last key word is masked,
 //                         32W otherwise: GPUHandler.cu:181-186)
-//   low 6 bits            n, the number of keys (0 = padding record)
+//   low 6 bits            n, the number of keys (0 = padding record, bucket
+//                         0xffff, which no window is given)
 // Key i of the record = K' bases from base i (the window i positions after
 // the run start) = exactly the key extractKMers builds for that window.
 // nb <= 32 RW - 11, so n <= nmax = 32 RW - 10 - K'; longer runs are split.
 
 constexpr int kSkmBlock = 256;
-constexpr u32 kSkmChunk = 4096;  // pool records per allocation (>= records of one tile)
-constexpr u32 kDead = 0xffffffffu;
 constexpr int kSkmPf = 2;  // F: code words prefetched per thread
+constexpr int kSkmHq = 22;  // F: most m-mer positions per hash item
 
 __device__ __forceinline__ u32 fmix32(u32 x) {
     x ^= x >> 16;
@@ -79,6 +79,9 @@ struct SkmArgs {
     int G;
     u64 n_reads;
     int L, k, m, Kp, nmax, R, NG, HS;
+    int hq;     // m-mer positions per hash item
+    u64 chunk;  // pool records per wave allocation (>= records of one tile)
+    int skip;  // timing experiments only (KC_F_SKIP): 1 record stores, 2 runs + records, 4 minimizer, 8 hashes
     u64* pool;         // RW x pool_cap u64 (SoA)
     u64 pool_cap;
     u64* pool_cursor;  // chunk allocator (records handed out)
@@ -86,94 +89,117 @@ struct SkmArgs {
 };
 
 struct SkmLds {
-    size_t codes, inval, hm, winfo, rflag, sa, ea, misc, total;
+    size_t codes, inval, hm, wpk, rflag, sa, ea, total;
 };
 
-// LDS skew: a lane works on 8 consecutive windows, so lanes read hm / winfo
-// at a stride of 8 words; one pad word per 8 makes the stride 9 (no bank
-// conflicts)
+// LDS skew of the m-mer hashes: a lane works on 8 consecutive windows, so
+// lanes read hm at a stride of 8 words; one pad word per 8 makes the stride 9
+// (no bank conflicts)
 __host__ __device__ inline int skm_sk(int j) { return j + (j >> 3); }
 __host__ __device__ inline int skm_hsk(int HS) { return skm_sk(HS) + 1; }
 
+// One wave's LDS region (F). wpk: 16 B per 8-window chunk (the chunk's eight
+// 16-bit window buckets, 0xffff = no key); sa: run starts (window | bucket <<
+// 16); ea: run ends.
 __host__ __device__ inline SkmLds skm_lds_layout(int R, int NG, int HS, int nw) {
     SkmLds o;
     size_t p = 0;
+    const int nchr = (nw + 7) / 8;
+    o.wpk = p;
+    p += (size_t)R * nchr * 16;
     o.codes = p;
     p += (size_t)R * NG * 4;
     o.inval = p;
     p += (size_t)R * NG * 4;
     o.hm = p;
     p += (size_t)R * skm_hsk(HS) * 4;
-    o.winfo = p;
-    p += ((size_t)R * nw + ((size_t)R * nw >> 3) + 8) * 4;
     o.rflag = p;
     p += (size_t)R * 4;
     o.sa = p;
-    p += (size_t)R * nw * 2;
+    p += (size_t)R * nw * 4;
     o.ea = p;
     p += (size_t)R * nw * 2;
     p = (p + 15) & ~(size_t)15;
-    o.misc = p;
-    p += 128;
     o.total = p;
     return o;
 }
 
-// F: one 256-thread workgroup per tile of R reads.
-//   1. code words and masks of the tile into LDS (groups past the read: 0)
-//   2. hm[r][j] = mmer_hash of the m bases from j (8 positions per thread)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Inclusive scan of one u32 per lane over the wave (Hillis-Steele).
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+constexpr u32 kNoKey = 0xffffu;  // window bucket of a window without a key (dead)
+
+// F: every wave works alone on tiles of R reads (its own LDS region; no
+// workgroup barriers, so the waves of a CU hide each other's latency):
+//   1. code words and masks of the tile into LDS (prefetched into registers
+//      during the previous tile; groups past the read stay zero); per read:
+//      bit 0 = a base outside ACGT, bit 1 = an 8-base aligned all-A group
+//      (only such reads can hold a key 0^W: a key spans >= 18 real bases)
+//   2. hm[r][j] = mmer_hash of the m bases from j (hq positions per lane)
 //   3. per 8-window chunk: window minimum over its k-m+1 m-mers as
-//      min(left suffix, shared core, right prefix); live = valid and key != 0
-//      (the rolling key of count_front); winfo = bucket or kDead
-//   4. run starts (live, bucket differs from the previous window) and ends,
-//      compacted in tile order by one block scan: the i-th start pairs with
-//      the i-th end (runs never cross reads)
-//   5. runs -> pieces of <= nmax windows -> records, written at consecutive
-//      positions of the workgroup's current pool chunk (one global atomic per
-//      kSkmChunk records); the chunk tail is padded with n = 0 records at exit
+//      min(left suffix, shared core, right prefix); reads with a flag take
+//      the rolling-key check of count_front (valid, key != 0); the chunk's
+//      eight buckets (kNoKey: no key) packed into 16 bytes
+//   4. run starts (bucket differs from the previous window's) and ends from
+//      the packed buckets of the chunk and its two neighbours, compacted in
+//      tile order by a wave scan: the i-th start pairs with the i-th end
+//   5. runs -> pieces of <= nmax windows -> records at consecutive positions
+//      of the wave's current pool chunk (one global atomic per chunk); the
+//      chunk tail is padded with n = 0 records at exit
 template <int W>
 __global__ __launch_bounds__(kSkmBlock) void skm_front_k(SkmArgs a) {
     constexpr int RW = W + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int L = a.L, k = a.k, m = a.m, NG = a.NG, HS = a.HS, R = a.R, Kp = a.Kp;
+    const int L = a.L, k = a.k, m = a.m, NG = a.NG, HS = a.HS, R = a.R, Kp = a.Kp, G = a.G;
     const u32 nmax = (u32)a.nmax;
     const int nw = L - k + 1;
     const int wm = k - m + 1;  // m-mers per window (>= 8)
     const int nchr = (nw + 7) >> 3;
     const int HSK = skm_hsk(HS);
-    const FastDiv div_nchr((u32)nchr), div_hch((u32)((HS + 7) >> 3)), div_nw((u32)nw), div_g((u32)a.G);
+    const int hq = a.hq;
+    const int hch = (HS + hq - 1) / hq;
+    const FastDiv div_nchr((u32)nchr), div_hch((u32)hch), div_nw((u32)nw), div_g((u32)G);
     const SkmLds lay = skm_lds_layout(R, NG, HS, nw);
-    u32* codes = (u32*)(smem + lay.codes);
-    u32* inval = (u32*)(smem + lay.inval);
-    u32* hm = (u32*)(smem + lay.hm);
-    u32* winfo = (u32*)(smem + lay.winfo);
-    u32* rflag = (u32*)(smem + lay.rflag);
-    unsigned short* sa = (unsigned short*)(smem + lay.sa);
-    unsigned short* ea = (unsigned short*)(smem + lay.ea);
-    u64* ms = (u64*)(smem + lay.misc);  // [0] chunk cursor [1] chunk end [2] old cursor [3] room [4] new chunk
-    u32* scan_tmp = (u32*)(ms + 8);
-    const int tid = threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    unsigned char* wb = smem + (size_t)wave * lay.total;
+    u32* codes = (u32*)(wb + lay.codes);
+    u32* inval = (u32*)(wb + lay.inval);
+    u32* hm = (u32*)(wb + lay.hm);
+    v4u* wpk = (v4u*)(wb + lay.wpk);
+    u32* rflag = (u32*)(wb + lay.rflag);
+    u32* sa = (u32*)(wb + lay.sa);
+    unsigned short* ea = (unsigned short*)(wb + lay.ea);
     const bool mask_last = ((k + 3) / 4) < 8 * W;
     const u64 last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
     const u64 ntiles = (a.n_reads + R - 1) / R;
+    const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
+    const u64 nwaves = (u64)gridDim.x * (kSkmBlock / 64);
+    const u64 chunk = a.chunk;
+    const bool m16 = m <= 16;
     u64 my_valid = 0;
     bool my_hole = false;
-    if (tid == 0) {
-        ms[0] = 0;
-        ms[1] = 0;
-    }
-    // code groups past the read (g >= G) stay zero in LDS for the whole launch
-    for (int it = tid; it < R * NG; it += kSkmBlock) {
+    for (int it = lane; it < R * NG; it += 64) {
         codes[it] = 0;
         inval[it] = 0;
     }
-    // the next tile's code words are loaded into registers while the current
-    // tile is processed; a thread's (read, group) slots are the same in every tile
-    const int G = a.G;
     int pr[kSkmPf], pg[kSkmPf];
 #pragma unroll
     for (int j = 0; j < kSkmPf; j++) {
-        const int it = tid + j * kSkmBlock;
+        const int it = lane + j * 64;
         pr[j] = it / G;
         pg[j] = it - pr[j] * G;
     }
@@ -193,173 +219,226 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front_k(SkmArgs a) {
             pfi[j] = iv;
         }
     };
-    prefetch(blockIdx.x);
-    __syncthreads();
-    for (u64 tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    auto flag_of = [&](u32 cw, u32 iv, int g) -> u32 {
+        // aligned all-A halves of the read's groups (padding past L counts)
+        const bool za = g < G && ((cw & 0xffffu) == 0u || (cw >> 16) == 0u);
+        return (iv ? 1u : 0u) | (za ? 2u : 0u);
+    };
+    prefetch(wid);
+    u64 ccur = 0, cend = 0;  // the wave's pool chunk (wave-uniform)
+    wave_sync();
+    for (u64 tile = wid; tile < ntiles; tile += nwaves) {
         const u64 r0 = tile * (u64)R;
         const int nr = (int)min((u64)R, a.n_reads - r0);
-        // 1. codes (prefetched; a tile with more groups than kSkmPf per thread
-        //    loads the rest directly)
+        // 1. codes and read flags
+        for (int r = lane; r < nr; r += 64) rflag[r] = 0;
+        wave_sync();
 #pragma unroll
         for (int j = 0; j < kSkmPf; j++)
             if (pr[j] < nr) {
                 codes[pr[j] * NG + pg[j]] = pfc[j];
                 inval[pr[j] * NG + pg[j]] = pfi[j];
+                const u32 f = flag_of(pfc[j], pfi[j], pg[j]);
+                if (f) atomicOr(&rflag[pr[j]], f);
             }
-        for (int it = tid + kSkmPf * kSkmBlock; it < nr * G; it += kSkmBlock) {
+        for (int it = lane + kSkmPf * 64; it < nr * G; it += 64) {
             const int r = (int)div_g.div((u32)it), g = it - r * G;
             const u64 idx = (r0 + (u64)r) * (u64)G + (u64)g;
-            codes[r * NG + g] = a.codes[idx];
-            inval[r * NG + g] = a.inval[idx];
+            const u32 cw = a.codes[idx], iv = a.inval[idx];
+            codes[r * NG + g] = cw;
+            inval[r * NG + g] = iv;
+            const u32 f = flag_of(cw, iv, g);
+            if (f) atomicOr(&rflag[r], f);
         }
-        for (int r = tid; r < nr; r += kSkmBlock) rflag[r] = 0;
-        __syncthreads();
-        prefetch(tile + gridDim.x);
+        wave_sync();
+        prefetch(tile + nwaves);
         // 2. m-mer hashes (positions past L - m are never used by a window)
-        const int hch = (HS + 7) >> 3;
-        for (int it = tid; it < nr * hch; it += kSkmBlock) {
-            const int r = (int)div_hch.div((u32)it), j0 = (it - r * hch) * 8;
+        for (int it = lane; it < ((a.skip & 8) ? 0 : nr * hch); it += 64) {
+            const int r = (int)div_hch.div((u32)it), j0 = (it - r * hch) * hq;
             const u64 x = code_word(codes + r * NG, j0);
             u32* hr = hm + r * HSK;
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-                if (j0 + i < HS) hr[skm_sk(j0 + i)] = mmer_hash((x << (2 * i)) >> (64 - 2 * m));
+            if (m16) {
+                const u32 xh = (u32)(x >> 32), xl = (u32)x;
+                for (int i = 0; i < hq; i++) {
+                    const u32 w = i == 0 ? xh : (i < 16 ? __builtin_amdgcn_alignbit(xh, xl, 32 - 2 * i) : xl << (2 * i - 32));
+                    const u32 mm = w >> (32 - 2 * m);
+                    if (j0 + i < HS) hr[skm_sk(j0 + i)] = (mm ^ 0x5bd1e995u) * 0x9e3779b1u;
+                }
+            } else {
+                for (int i = 0; i < hq; i++)
+                    if (j0 + i < HS) hr[skm_sk(j0 + i)] = mmer_hash((x << (2 * i)) >> (64 - 2 * m));
+            }
         }
-        for (int it = tid; it < nr * G; it += kSkmBlock) {
-            const int r = (int)div_g.div((u32)it);
-            if (inval[r * NG + (it - r * G)]) atomicOr(&rflag[r], 1u);
-        }
-        __syncthreads();
-        // 3. windows
-        for (int c = tid; c < nr * nchr; c += kSkmBlock) {
+        wave_sync();
+        // 3. windows -> packed chunk buckets
+        for (int c = lane; c < nr * nchr; c += 64) {
             const int r = (int)div_nchr.div((u32)c), p0 = (c - r * nchr) * 8;
-            const u32* cr = codes + r * NG;
             const u32* hr = hm + r * HSK;
+            const int h0 = 9 * (p0 >> 3);  // skm_sk(p0 + i) = h0 + i for i < 8
             u32 core = ~0u;
-            for (int j = p0 + 7; j < p0 + wm; j++) core = min(core, hr[skm_sk(j)]);
-            u32 lft[8], rgt[8];
+            const int jl = p0 + wm - 1;
+            for (int jb = p0 + 7; jb <= ((a.skip & 4) ? -1 : jl); jb += 8) {
+                u32 v8[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) v8[i] = hr[skm_sk(min(jb + i, jl))];
+#pragma unroll
+                for (int i = 0; i < 8; i++) core = min(core, v8[i]);
+            }
+            u32 lft[8];
             lft[7] = ~0u;
 #pragma unroll
-            for (int i = 6; i >= 0; i--) lft[i] = min(lft[i + 1], hr[skm_sk(p0 + i)]);
-            rgt[0] = ~0u;
-#pragma unroll
-            for (int i = 1; i < 8; i++) rgt[i] = min(rgt[i - 1], hr[skm_sk(p0 + wm + i - 1)]);
-            u64 kr[W];
-#pragma unroll
-            for (int j = 0; j < W; j++) kr[j] = code_word(cr, p0 + 32 * j);
-            u64 tl = code_word(cr, p0 + 32 * W);
-            const bool clean = rflag[r] == 0;
-            u32 zeros = 0, valids = 0;
+            for (int i = 6; i >= 0; i--) lft[i] = min(lft[i + 1], hr[h0 + i]);
+            u32 rgt = ~0u;
+            u32 bk[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const int p = p0 + i;
-                const bool active = p < nw;
-                bool valid = active;
-                if (active && !clean) {
-                    const u32* ir = inval + r * NG;
-                    const int last = p + k - 1;
-                    for (int gg = p >> 4; gg <= (last >> 4); gg++) {
-                        const int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
-                        const u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
-                        if (ir[gg] & rm) valid = false;
-                    }
-                }
-                bool is_zero = (kr[W - 1] & last_mask) == 0ull;
-#pragma unroll
-                for (int j = 0; j < W - 1; j++) is_zero = is_zero && (kr[j] == 0ull);
-                my_hole |= active && !valid;
-                valids += valid ? 1u : 0u;
-                zeros += (valid && is_zero) ? 1u : 0u;
-                if (active)
-                    winfo[skm_sk(r * nw + p)] = (valid && !is_zero) ? (min(core, min(lft[i], rgt[i])) & 0xffffu) : kDead;
-#pragma unroll
-                for (int j = 0; j < W - 1; j++) kr[j] = (kr[j] << 2) | (kr[j + 1] >> 62);
-                kr[W - 1] = (kr[W - 1] << 2) | (tl >> 62);
-                tl <<= 2;
+                if (i > 0) rgt = min(rgt, hr[skm_sk(jl + i)]);
+                u32 b = min(core, min(lft[i], rgt)) & 0xffffu;
+                bk[i] = b == kNoKey ? kNoKey - 1u : b;
             }
-            my_valid += valids;
-            if (zeros) {
-                atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)zeros);
-                atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
-            }
-        }
-        __syncthreads();
-        // 4. run starts / ends, compacted in tile order
-        u32 sbase = 0, ebase = 0;
-        for (int c0 = 0; c0 < nr * nchr; c0 += kSkmBlock) {
-            const int c = c0 + tid;
-            u32 smask = 0, emask = 0;
-            int q0 = 0;
-            if (c < nr * nchr) {
-                const int r = (int)div_nchr.div((u32)c), p0 = (c - r * nchr) * 8;
-                q0 = r * nw + p0;
-                u32 prev = p0 > 0 ? winfo[skm_sk(q0 - 1)] : kDead;
+            const u32 fl = rflag[r];
+            u32 act = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) act += (p0 + i < nw) ? 1u : 0u;
+            if (fl == 0u) {
+                my_valid += act;
+            } else {
+                // invalid bases or a possible key 0^W: the rolling key check
+                const u32* cr = codes + r * NG;
+                u64 kr[W];
+#pragma unroll
+                for (int j = 0; j < W; j++) kr[j] = code_word(cr, p0 + 32 * j);
+                u64 tl = code_word(cr, p0 + 32 * W);
+                u32 zeros = 0, valids = 0;
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     const int p = p0 + i;
-                    if (p < nw) {
-                        const u32 v = winfo[skm_sk(q0 + i)];
-                        const u32 nx = p + 1 < nw ? winfo[skm_sk(q0 + i + 1)] : kDead;
-                        if (v != kDead) {
-                            if (v != prev) smask |= 1u << i;
-                            if (v != nx) emask |= 1u << i;
+                    const bool active = p < nw;
+                    bool valid = active;
+                    if (active && (fl & 1u)) {
+                        const u32* ir = inval + r * NG;
+                        const int last = p + k - 1;
+                        for (int gg = p >> 4; gg <= (last >> 4); gg++) {
+                            const int lo = max(p - 16 * gg, 0), hi = min(last - 16 * gg, 15);
+                            const u32 rm = (0xffffu >> lo) & (0xffffu << (15 - hi)) & 0xffffu;
+                            if (ir[gg] & rm) valid = false;
                         }
-                        prev = v;
                     }
+                    bool is_zero = (kr[W - 1] & last_mask) == 0ull;
+#pragma unroll
+                    for (int j = 0; j < W - 1; j++) is_zero = is_zero && (kr[j] == 0ull);
+                    my_hole |= active && !valid;
+                    valids += valid ? 1u : 0u;
+                    zeros += (valid && is_zero) ? 1u : 0u;
+                    if (!valid || is_zero) bk[i] = kNoKey;
+#pragma unroll
+                    for (int j = 0; j < W - 1; j++) kr[j] = (kr[j] << 2) | (kr[j + 1] >> 62);
+                    kr[W - 1] = (kr[W - 1] << 2) | (tl >> 62);
+                    tl <<= 2;
+                }
+                my_valid += valids;
+                if (zeros) {
+                    atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)zeros);
+                    atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
                 }
             }
-            u32 tot;
-            const u32 ex = block_excl_scan((u32)__popc(smask) | ((u32)__popc(emask) << 16), scan_tmp, &tot);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (p0 + i >= nw) bk[i] = kNoKey;
+            v4u pk;
+            pk.x = bk[0] | (bk[1] << 16);
+            pk.y = bk[2] | (bk[3] << 16);
+            pk.z = bk[4] | (bk[5] << 16);
+            pk.w = bk[6] | (bk[7] << 16);
+            wpk[c] = pk;
+        }
+        wave_sync();
+        if (a.skip & 2) continue;
+        // 4. run starts / ends, compacted in tile order
+        u32 sbase = 0, ebase = 0;
+        for (int c0 = 0; c0 < nr * nchr; c0 += 64) {
+            const int c = c0 + lane;
+            u32 smask = 0, emask = 0;
+            int q0 = 0;
+            u32 bk[8];
+            if (c < nr * nchr) {
+                const int r = (int)div_nchr.div((u32)c), p0 = (c - r * nchr) * 8;
+                q0 = r * nw + p0;
+                const v4u pk = wpk[c];
+                bk[0] = pk.x & 0xffffu;
+                bk[1] = pk.x >> 16;
+                bk[2] = pk.y & 0xffffu;
+                bk[3] = pk.y >> 16;
+                bk[4] = pk.z & 0xffffu;
+                bk[5] = pk.z >> 16;
+                bk[6] = pk.w & 0xffffu;
+                bk[7] = pk.w >> 16;
+                u32 prev = p0 > 0 ? (wpk[c - 1].w >> 16) : kNoKey;
+                const u32 nx8 = p0 + 8 < nw ? (wpk[c + 1].x & 0xffffu) : kNoKey;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const u32 v = bk[i];
+                    const u32 nx = i < 7 ? bk[i + 1] : nx8;
+                    if (v != kNoKey) {
+                        if (v != prev) smask |= 1u << i;
+                        if (v != nx) emask |= 1u << i;
+                    }
+                    prev = v;
+                }
+            }
+            const u32 v = (u32)__popc(smask) | ((u32)__popc(emask) << 16);
+            const u32 inc = wave_incl_scan(v);
+            const u32 ex = inc - v;
+            const u32 tot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
             u32 sp = sbase + (ex & 0xffffu), ep = ebase + (ex >> 16);
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                if ((smask >> i) & 1u) sa[sp++] = (unsigned short)(q0 + i);
+                if ((smask >> i) & 1u) sa[sp++] = (u32)(q0 + i) | (bk[i] << 16);
                 if ((emask >> i) & 1u) ea[ep++] = (unsigned short)(q0 + i);
             }
             sbase += tot & 0xffffu;
             ebase += tot >> 16;
         }
-        __syncthreads();
+        wave_sync();
         // 5. runs -> records
         const u32 T = sbase;
-        const u32 per = (T + kSkmBlock - 1) / kSkmBlock;
-        const u32 i0 = min(T, (u32)tid * per), i1 = min(T, i0 + per);
+        const u32 per = (T + 63) >> 6;
+        const u32 i0 = min(T, (u32)lane * per), i1 = min(T, i0 + per);
         u32 mine = 0;
         for (u32 i = i0; i < i1; i++) {
-            const u32 n = (u32)ea[i] - (u32)sa[i] + 1u;
-            mine += (n + nmax - 1) / nmax;
+            const u32 n = (u32)ea[i] - (sa[i] & 0xffffu) + 1u;
+            mine += n <= nmax ? 1u : (n + nmax - 1) / nmax;
         }
-        u32 ptot;
-        const u32 pb = block_excl_scan(mine, scan_tmp, &ptot);
-        if (tid == 0) {
-            const u64 cur = ms[0], end = ms[1];
-            const u64 room = end - cur;
-            ms[2] = cur;
-            ms[3] = room;
-            if ((u64)ptot > room) {
-                const u64 nb = atomicAdd((unsigned long long*)a.pool_cursor, (unsigned long long)kSkmChunk);
-                ms[4] = nb;
-                ms[0] = nb + ((u64)ptot - room);
-                ms[1] = nb + kSkmChunk;
-            } else {
-                ms[0] = cur + ptot;
-            }
+        const u32 pinc = wave_incl_scan(mine);
+        const u32 pb = pinc - mine;
+        const u32 ptot = (u32)__builtin_amdgcn_readlane((int)pinc, 63);
+        const u64 room = cend - ccur;
+        const u64 oc = ccur;
+        u64 nbase = 0;
+        if ((u64)ptot > room) {
+            u64 nb = 0;
+            if (lane == 0) nb = atomicAdd((unsigned long long*)a.pool_cursor, (unsigned long long)chunk);
+            nb = readlane64(nb, 0);
+            nbase = nb;
+            ccur = nb + ((u64)ptot - room);
+            cend = nb + chunk;
+        } else {
+            ccur += ptot;
         }
-        __syncthreads();
-        const u64 oc = ms[2], room = ms[3], nbase = ms[4];
         u32 g = pb;
         for (u32 i = i0; i < i1; i++) {
-            const u32 qs = sa[i];
+            const u32 sv = sa[i];
+            const u32 qs = sv & 0xffffu;
             const u32 n = (u32)ea[i] - qs + 1u;
             const int r = (int)div_nw.div(qs);
             const int ps0 = (int)qs - r * nw;
-            const u64 bk = winfo[skm_sk((int)qs)] & 0xffffu;
+            const u64 bkt = sv >> 16;
             const u32* cr = codes + r * NG;
             for (u32 off = 0; off < n; off += nmax, g++) {
                 const u32 nn = min(nmax, n - off);
                 const int ps = ps0 + (int)off;
                 u64 rec[RW];
-                rec[0] = (bk << 48) | (code_word(cr, ps) >> 16);
+                rec[0] = (bkt << 48) | (code_word(cr, ps) >> 16);
 #pragma unroll
                 for (int j = 1; j < RW; j++) rec[j] = code_word(cr, ps + 32 * j - 8);
                 const int vb = 16 + 2 * (Kp + (int)nn - 1);
@@ -371,25 +450,23 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front_k(SkmArgs a) {
                 }
                 rec[RW - 1] |= (u64)nn;
                 const u64 dst = (u64)g < room ? oc + g : nbase + ((u64)g - room);
-                if (dst < a.pool_cap) {
+                if (dst < a.pool_cap && !(a.skip & 1)) {
 #pragma unroll
                     for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + dst] = rec[j];
                 }
             }
         }
-        __syncthreads();
+        wave_sync();
     }
-    // pad the rest of the current chunk with n = 0 records (bucket 0)
-    {
-        const u64 cur = ms[0], end = ms[1];
-        for (u64 i = cur + (u64)tid; i < end; i += kSkmBlock)
-            if (i < a.pool_cap) {
+    // pad the rest of the wave's chunk with n = 0 records in bucket kNoKey,
+    // which no window takes: P5 never walks them
+    for (u64 i = ccur + (u64)lane; i < cend; i += 64)
+        if (i < a.pool_cap) {
 #pragma unroll
-                for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + i] = 0ull;
-            }
-    }
+            for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + i] = j == 0 ? ((u64)kNoKey << 48) : 0ull;
+        }
     wave_add(&a.stats[ST_VALID], my_valid);
-    if (__ballot(my_hole) && lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+    if (__ballot(my_hole) && lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
 }
 
 SkmGeom skm_geometry(int L, int k) {
@@ -414,12 +491,18 @@ SkmGeom skm_geometry(int L, int k) {
     if (nw > 4096) return g;  // a tile's records must fit one pool chunk
     g.NG = (L + 32 * RW + 64) / 16 + 3;
     g.HS = L - m + 8;
-    int R = kSkmBlock / nchr;
+    // a wave tile: R reads whose 8-window chunks fill the wave's 64 lanes
+    int R = 64 / nchr;
     if (R < 1) R = 1;
-    while (R > 1 && skm_lds_layout(R, g.NG, g.HS, nw).total > 48 * 1024) R--;
     g.R = R;
-    g.lds = skm_lds_layout(R, g.NG, g.HS, nw).total;
-    if (g.lds > 64 * 1024) return g;
+    int ipr = 64 / R;  // hash items per read
+    if (ipr < 1) ipr = 1;
+    g.hq = (g.HS + ipr - 1) / ipr;
+    if (g.hq > 32 - m + 1) g.hq = 32 - m + 1;
+    if (g.hq > 22) g.hq = 22;
+    if (g.hq < 1) g.hq = 1;
+    g.lds = (size_t)(kSkmBlock / 64) * skm_lds_layout(R, g.NG, g.HS, nw).total;
+    if (g.lds > 160 * 1024) return g;
     g.ok = true;
     return g;
 }
@@ -445,6 +528,13 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
     a.pool_cap = pool_cap;
     a.pool_cursor = pool_cursor;
     a.stats = l.stats;
+    a.hq = g.hq;
+    a.chunk = (u64)g.R * (u64)(l.L - l.k + 1);
+    if (a.chunk < 1024) a.chunk = 1024;
+    {
+        const char* e = getenv("KC_F_SKIP");
+        a.skip = e ? atoi(e) : 0;
+    }
     const u64 tiles = (l.n_reads + g.R - 1) / g.R;
     const int W = (l.k + 31) / 32;
     // one wave of workgroups: every workgroup walks the same number of tiles
@@ -732,8 +822,9 @@ struct SkmBucketArgs {
     const u64* recs;  // RW x stride (SoA), grouped by bucket
     u64 stride;
     const u64* starts;
-    u32 nbuckets;
+    u32 b0, nbuckets;  // buckets [b0, nbuckets)
     u32 lcap;
+    int count_keys;
     u64 last_mask;
     u64* rec_keys;
     u32* rec_cnts;
@@ -923,7 +1014,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     const u32 ng = a.lcap >> 2;
     const bool grouped = W == 1 && (a.lcap & 3u) == 0;
     constexpr u64 M48 = 0xffffffffffffull;
-    for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         if (tid == 0)
             *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT) &
@@ -933,6 +1024,11 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
         __syncthreads();
         if (stop) return;
         const u64 lo = a.starts[b], hi = a.starts[b + 1];
+        if (a.count_keys) {
+            u64 kn = 0;
+            for (u64 i = lo + tid; i < hi; i += kBucketBlock) kn += a.recs[(u64)(RW - 1) * a.stride + i] & 63u;
+            wave_add(&a.stats[ST_P5_KEYS], kn);
+        }
         u32 m = 1, sub = 0;
         while (sub < m) {
             const bool last = m >= mmax;
@@ -1153,7 +1249,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
 }
 
 hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride, const uint64_t* starts,
-                            uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                            uint32_t b0, uint32_t b1, bool count_keys, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
                             uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s) {
     SkmBucketArgs a;
@@ -1166,7 +1262,9 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
     a.recs = recs;
     a.stride = stride;
     a.starts = starts;
-    a.nbuckets = nbuckets;
+    a.b0 = b0;
+    a.nbuckets = b1;
+    a.count_keys = count_keys ? 1 : 0;
     a.lcap = (lcap == 0 || lcap > (u32)skm_lds_slots(W)) ? (u32)skm_lds_slots(W) : lcap;
     a.rec_keys = rec_keys;
     a.rec_cnts = rec_cnts;

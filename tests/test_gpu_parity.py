@@ -174,7 +174,7 @@ def test_partition_many_batches(kca, orc, k):
     """A small working set splits one block into many partition batches whose
     records are summed at finish."""
     fq = kca.synth_fastq(60000, 150, seed=21, genome_length=300_000, n_rate=0.0005)
-    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=1 << 21) as ctx:
+    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=1 << 21, engine="partition") as ctx:
         ctx.count_fastq(fq)
         got = ctx.records()
         st = ctx.stats()
@@ -422,7 +422,7 @@ def test_partition_subrange_passes(kca, orc, k, slots):
     passes, still entirely in LDS (no spill, no fallback-table claims)."""
     n, L = 40000, 150
     fq = kca.synth_fastq(n, L, seed=k + slots, n_rate=0.0005)
-    with kca.Context(kmer_length=k, line_length=L, lds_slots=slots) as ctx:
+    with kca.Context(kmer_length=k, line_length=L, lds_slots=slots, engine="partition") as ctx:
         ctx.count_fastq(fq)
         got = ctx.records()
         st = ctx.stats()
@@ -448,7 +448,7 @@ def test_config5_full_size_properties(kca):
 
     n, L, k = 20_000_000, 150, 55
     dev = torch.device("cuda", 0)
-    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=72 << 30) as ctx:
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=72 << 30, engine="partition") as ctx:
         ptr, nb = ctx.synth_device(n, L, 5, 0, 0.0, 0)
         assert ctx.count_fastq_device(ptr, nb) == n
         ctx.free_device(ptr)
@@ -507,7 +507,7 @@ def test_skewed_segment_uses_lsd_fallback(kca, orc, k):
     prefix = "ACGTTGCAACGTGA"
     reads = [prefix + "".join(rng.choice("ACGT") for _ in range(136)) for _ in range(3000)]
     fq = _fq(reads).encode()
-    with kca.Context(kmer_length=k, line_length=150) as ctx:
+    with kca.Context(kmer_length=k, line_length=150, engine="partition") as ctx:
         ctx.count_fastq(fq)
         got = ctx.records()
     assert got == orc.count_fastq(fq, k)

@@ -105,3 +105,42 @@ def test_skm_genome_reads_multi_block(kca, orc):
         got = ctx.records()
     want, _ = orc.refcpu(b"".join(blocks), 31, threads=8)
     assert got == want
+
+
+def test_auto_engine_switches_on_high_cardinality(kca, orc):
+    """iid reads (every key distinct): the skm sample sees no repeats and the
+    key-prefix engine counts the batch instead; output identical."""
+    n, L, k = 160_000, 150, 31
+    fq = kca.synth_fastq(n, L, seed=77)
+    with kca.Context(kmer_length=k, line_length=L, engine="auto", gpu_memory_limit=4 << 30) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["engines_used"] == 2
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_auto_engine_keeps_skm_on_genome_reads(kca, orc):
+    n, L, k = 160_000, 150, 31
+    fq = kca.synth_fastq(n, L, seed=78, genome_length=400_000)
+    with kca.Context(kmer_length=k, line_length=L, engine="auto", gpu_memory_limit=4 << 30) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["engines_used"] == 1
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_auto_engine_switch_after_skm_batches(kca, orc):
+    """A small working set: the first batches are below the sample threshold
+    (skm), a later one is sampled and switches; skm and key-prefix records
+    meet in one finish."""
+    L, k = 150, 31
+    blocks = [kca.synth_fastq(25_000, L, seed=79), kca.synth_fastq(175_000, L, seed=79, first_read=25_000)]
+    with kca.Context(kmer_length=k, line_length=L, engine="auto", gpu_memory_limit=3 << 30) as ctx:
+        for b in blocks:
+            ctx.count_fastq(b)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["engines_used"] == 3
+    assert got == orc.count_fastq(b"".join(blocks), k)

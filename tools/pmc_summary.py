@@ -44,20 +44,28 @@ for name, n, per in rows:
                                   "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE")))
 k = int(sys.argv[3]) if len(sys.argv) > 3 else 31
 W = (k + 31) // 32
-want = {"P2": f"count_front<{W}, 2, true>", "P3": f"p3_scatter_k<{W}>", "P5": f"count_buckets<{W}>"}
 rec = {"reads_per_gpu": reads, "k": k, "kernels": {},
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, --kernel-trace only "
                  "(tools/gpu_pmc.sh); HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), "
-                 "per the gfx950 FETCH_SIZE correction in MI355X_MICROARCH.md"}
-for tag, pat in want.items():
-    hit = [r for r in rows if pat in r[0]]
-    if not hit:
-        continue
-    name, n, per = hit[0]
+                 "per the gfx950 FETCH_SIZE correction in MI355X_MICROARCH.md; keyed by the kernel's "
+                 "short name (template arguments, no spaces)"}
+
+
+def short(name):
+    n = name.split("(")[0]
+    n = n.replace("void ", "").replace("kc::", "")
+    return n.replace(" ", "")
+
+
+for name, n, per in rows:
     rd = 2 * per.get("FETCH_SIZE", 0) * 1024
     wr = per.get("WRITE_SIZE", 0) * 1024
-    rec["kernels"][tag] = {"kernel": name, "bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr}
+    if rd + wr == 0:
+        continue
+    rec["kernels"][short(name)] = {"kernel": name, "bytes_per_launch": rd + wr, "read_bytes": rd,
+                                   "write_bytes": wr, "launches": n}
 os.makedirs("profiles", exist_ok=True)
 json.dump(rec, open("profiles/pmc_count_kmers.json", "w"), indent=1)
 json.dump(rec, open(os.path.join(out, "pmc_count_kmers.json"), "w"), indent=1)  # travels back from the box
-print("wrote profiles/pmc_count_kmers.json", {t: round(v["bytes_per_launch"] / 1e9, 2) for t, v in rec["kernels"].items()})
+print("wrote profiles/pmc_count_kmers.json", {t: round(v["bytes_per_launch"] / 1e9, 2) for t, v in rec["kernels"].items()
+                                             if v["bytes_per_launch"] > 1e8})
