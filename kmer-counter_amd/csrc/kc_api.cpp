@@ -708,6 +708,19 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             c->part_ms[3] += t;
             const uint64_t kbound = nr * nw;
             const uint64_t rec_batch0 = c->rec_n;
+            if (getenv("KC_DEBUG")) {
+                std::vector<uint64_t> st((size_t)nb + 1);
+                HIPCHK(c, hipMemcpy(st.data(), c->part_starts.p, st.size() * 8, hipMemcpyDeviceToHost));
+                uint64_t mx = 0, mb = 0;
+                for (uint32_t b = 0; b + 1 < nb; b++)
+                    if (st[b + 1] - st[b] > mx) {
+                        mx = st[b + 1] - st[b];
+                        mb = b;
+                    }
+                fprintf(stderr, "kc: skm buckets: mean %.0f records, max %llu (bucket %llu), padding %llu\n",
+                        (double)st[nb - 1] / (nb - 1), (unsigned long long)mx, (unsigned long long)mb,
+                        (unsigned long long)(st[nb] - st[nb - 1]));
+            }
             // P5 over buckets [b0, b1); reruns with a bigger record buffer on
             // overflow (safe while nothing went to the global table or spill)
             auto p5_range = [&](uint32_t b0, uint32_t b1, bool count_keys) -> kc_status {

@@ -56,6 +56,13 @@ __device__ __forceinline__ void wave_add(u64* ctr, u64 v) {
     if ((int)lane_id() == __ffsll((long long)act) - 1 && v) atomicAdd((unsigned long long*)ctr, v);
 }
 
+// n / d for n, d < 2^16 with one mul_hi (m = ceil(2^32 / d) is exact there)
+struct FastDivU {
+    u32 d, m;
+    __device__ __forceinline__ explicit FastDivU(u32 dd) : d(dd), m((u32)((0x100000000ull + dd - 1) / dd)) {}
+    __device__ __forceinline__ u32 div(u32 v) const { return d == 1 ? v : __umulhi(v, m); }
+};
+
 __device__ __forceinline__ u64 mix64(u64 x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdull;

@@ -60,13 +60,6 @@ __device__ __forceinline__ u32 mmer_hash(u64 mm) {
     return (x ^ 0x5bd1e995u) * 0x9e3779b1u;
 }
 
-// n / d for n, d < 2^16 with one mul_hi (m = ceil(2^32 / d) is exact there)
-struct FastDiv {
-    u32 d, m;
-    __device__ __forceinline__ explicit FastDiv(u32 dd) : d(dd), m((u32)((0x100000000ull + dd - 1) / dd)) {}
-    __device__ __forceinline__ u32 div(u32 n) const { return d == 1 ? n : __umulhi(n, m); }
-};
-
 __device__ __forceinline__ u64 readlane64(u64 v, int l) {
     const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, l);
     const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l);
@@ -172,7 +165,7 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front_k(SkmArgs a) {
     const int HSK = skm_hsk(HS);
     const int hq = a.hq;
     const int hch = (HS + hq - 1) / hq;
-    const FastDiv div_nchr((u32)nchr), div_hch((u32)hch), div_nw((u32)nw), div_g((u32)G);
+    const FastDivU div_nchr((u32)nchr), div_hch((u32)hch), div_nw((u32)nw), div_g((u32)G);
     const SkmLds lay = skm_lds_layout(R, NG, HS, nw);
     const int wave = threadIdx.x >> 6, lane = lane_id();
     unsigned char* wb = smem + (size_t)wave * lay.total;
@@ -922,7 +915,7 @@ struct SkmLdsTable {
 // last sub-range level the global table and the spill buffer. Out of line:
 // it runs once per 64 queued keys and keeps the hot loop small.
 template <int W>
-__device__ __noinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t, const u64* wq, u32 c, u64 lo,
+__device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t, const u64* wq, u32 c, u64 lo,
                                        bool last, u32 limit) {
     constexpr int RW = W + 1;
     const int lane = (int)lane_id();
@@ -1089,6 +1082,92 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 u64 win[RW];
                 skm_window<RW>(cur, 16u + 2u * ki, win);
                 const u64 wrec0 = base + (u64)(tid - lane) - lo;  // lane 0's record of this batch
+                // advance to the next key: roll one base in; past the record's
+                // last key move to the next record with keys (this wave's stage)
+                auto advance = [&](u32 t) {
+#pragma unroll
+                    for (int j = 0; j < RW - 1; j++) win[j] = (win[j] << 2) | (win[j + 1] >> 62);
+                    win[RW - 1] <<= 2;
+                    ++ki;
+                    if (ki == nn && s0 + t + 1 < s1) {
+                        do {
+                            ++o;
+#pragma unroll
+                            for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
+                            nn = (u32)(cur[RW - 1] & 63u);
+                        } while (nn == 0u);
+                        skm_window<RW>(cur, 16u, win);
+                        ki = 0;
+                    }
+                };
+                if (W == 1 && grouped) {
+                    // software pipeline: the home group of key t + 1 is loaded
+                    // while key t is resolved (a group read before a claim of
+                    // the slow path only sends that key to the slow path again)
+                    u64 key = win[0] & a.last_mask;
+                    bool act = s0 < s1;
+                    u32 kcur = ki;
+                    int ocur = o;
+                    u32 g = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key), ng);
+                    v2u64 a0 = ((const lds_v2u64*)(lkeys + 4 * g))[0], a1 = ((const lds_v2u64*)(lkeys + 4 * g))[1];
+                    for (u32 t = 0; t < per; t++) {
+                        advance(t);
+                        const bool act_n = s0 + t + 1 < s1;
+                        const u64 key_n = win[0] & a.last_mask;
+                        const u32 g_n = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key_n), ng);
+                        const lds_v2u64* gpn = (const lds_v2u64*)(lkeys + 4 * g_n);
+                        const v2u64 b0 = gpn[0], b1 = gpn[1];
+                        bool want = act && !a.skip;
+                        if (m > 1) want = want && (u32)(((key & M48) * (u64)m) >> 48) == sub;
+                        my_keys += want ? 1u : 0u;
+                        const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
+                        int hit = -1, emp = -1;
+#pragma unroll
+                        for (int i = 3; i >= 0; i--) {
+                            if (v[i] == key) hit = i;
+                            if (v[i] == 0ull) emp = i;
+                        }
+                        const bool found = want && hit >= 0 && (emp < 0 || hit < emp);
+                        if (found) atomicAdd(&lcnt[4 * g + hit], 1u);
+                        // a new key takes the group's first empty slot right
+                        // here; only a full group or a lost race queues it
+                        bool pend = want && !found;
+                        bool claim = false;
+                        if (pend && emp >= 0) {
+                            const u64 old = atomicCAS((unsigned long long*)&lkeys[4 * g + emp], 0ull,
+                                                      (unsigned long long)key);
+                            if (old == 0ull || old == key) {
+                                atomicAdd(&lcnt[4 * g + emp], 1u);
+                                claim = old == 0ull;
+                                pend = false;
+                            }
+                        }
+                        const u64 cm = __ballot(claim);
+                        if (cm && lane == 0) {
+                            const u32 f = atomicAdd(lfill, (u32)__popcll(cm)) + (u32)__popcll(cm);
+                            if (!last && f > limit) atomicOr(labort, 1u);
+                        }
+                        const u64 pb = __ballot(pend);
+                        if (pb) {
+                            if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = ((wrec0 + (u64)ocur) << 6) | kcur;
+                            qn += (u32)__popcll(pb);
+                            if (qn >= 64) {
+                                skm_drain<W>(a, tab, wq, 64, lo, last, limit);
+                                const u32 rest = qn - 64;
+                                const u64 keep = lane < (int)rest ? wq[64 + lane] : 0ull;
+                                if (lane < (int)rest) wq[lane] = keep;
+                                qn = rest;
+                            }
+                        }
+                        key = key_n;
+                        act = act_n;
+                        g = g_n;
+                        a0 = b0;
+                        a1 = b1;
+                        kcur = ki;
+                        ocur = o;
+                    }
+                } else {
                 for (u32 t = 0; t < per; t++) {
                     const bool act = s0 + t < s1;
                     u64 key[W];
@@ -1136,22 +1215,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                             qn = rest;
                         }
                     }
-                    // next key: roll one base in; past the record's last key
-                    // move to the next record with keys (the stage of this wave)
-#pragma unroll
-                    for (int j = 0; j < RW - 1; j++) win[j] = (win[j] << 2) | (win[j + 1] >> 62);
-                    win[RW - 1] <<= 2;
-                    ++ki;
-                    if (ki == nn && s0 + t + 1 < s1) {
-                        do {
-                            ++o;
-#pragma unroll
-                            for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
-                            nn = (u32)(cur[RW - 1] & 63u);
-                        } while (nn == 0u);
-                        skm_window<RW>(cur, 16u, win);
-                        ki = 0;
-                    }
+                    advance(t);
+                }
                 }
             }
             if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))

@@ -8,8 +8,8 @@ mkdir -p $OUT
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/g$i -o p -- python3 bench.py --reads 10000000 --steps 1 --warmup 0 --no-cpu --engine skm > $OUT/g$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/g$i -o p -- python3 bench.py --reads ${READS:-10000000} --steps 1 --warmup 0 --no-cpu --engine skm > $OUT/g$i.log 2>&1
   rc=$?; echo "group $i rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
-python3 tools/pmc_summary.py $OUT 10000000 31 2>&1 | grep -A3 "count_skm\|skm_front"
+python3 tools/pmc_summary.py $OUT ${READS:-10000000} 31 2>&1 | grep -A3 "count_skm\|skm_front"
