@@ -1667,41 +1667,47 @@ __device__ __forceinline__ u64 slot_frac(const u64 (&key)[W]) {
 
 // `frac` is a 48-bit uniform hash fraction; slot = frac * lcap >> 48.
 // *claimed is set when this key took an empty slot.
-template <int W>
+template <int W, int GS = 4>
 __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* lkeys, u32* lcnt, u32* lstate,
                                            u32 lcap, u32 max_probe, bool* claimed) {
+    static_assert(GS == 2 || GS == 4, "LDS group of 2 or 4 slots");
     u32 slot = (u32)((frac * (u64)lcap) >> 48);
     if constexpr (W == 1) {
-        if ((lcap & 3u) == 0) {
-            // groups of 4 slots: the home group is read with two 16-byte LDS
+        if ((lcap % GS) == 0) {
+            // groups of GS slots: the home group is read with GS/2 16-byte LDS
             // loads and a repeat (the common case) resolves with branch-free
             // compares and one add; probing continues group by group
-            const u32 ng = lcap >> 2;
+            const u32 ng = lcap / GS;
             u32 g = (u32)((frac * (u64)ng) >> 48);
-            for (u32 pr = 0; pr < max_probe; pr += 4) {
-                const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
-                const v2u64 a0 = gp[0], a1 = gp[1];
-                const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
+            for (u32 pr = 0; pr < max_probe; pr += GS) {
+                const lds_v2u64* gp = (const lds_v2u64*)(lkeys + GS * g);
+                u64 v[GS];
+#pragma unroll
+                for (int h = 0; h < GS / 2; h++) {
+                    const v2u64 a = gp[h];
+                    v[2 * h] = a.x;
+                    v[2 * h + 1] = a.y;
+                }
                 int hit = -1, emp = -1;
 #pragma unroll
-                for (int i = 3; i >= 0; i--) {
+                for (int i = GS - 1; i >= 0; i--) {
                     if (v[i] == key[0]) hit = i;
                     if (v[i] == 0ull) emp = i;
                 }
                 if (hit >= 0 && (emp < 0 || hit < emp)) {
-                    atomicAdd(&lcnt[4 * g + hit], 1u);
+                    atomicAdd(&lcnt[GS * g + hit], 1u);
                     return true;
                 }
                 if (emp >= 0) {
                     // claim the first empty slot; a lost race re-reads the group
                     const u64 old =
-                        atomicCAS((unsigned long long*)&lkeys[4 * g + emp], 0ull, (unsigned long long)key[0]);
+                        atomicCAS((unsigned long long*)&lkeys[GS * g + emp], 0ull, (unsigned long long)key[0]);
                     if (old == 0ull || old == key[0]) {
-                        atomicAdd(&lcnt[4 * g + emp], 1u);
+                        atomicAdd(&lcnt[GS * g + emp], 1u);
                         *claimed = old == 0ull;
                         return true;
                     }
-                    pr -= 4;  // same group again
+                    pr -= GS;  // same group again
                     continue;
                 }
                 if (++g == ng) g = 0;

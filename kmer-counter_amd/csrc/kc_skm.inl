@@ -852,6 +852,7 @@ __device__ __forceinline__ void skm_key(const u64 (&rw)[W + 1], u32 i, u64 last_
     key[W - 1] &= last_mask;
 }
 
+constexpr int kSkmGroup = 4;    // P5 LDS table: slots per group (two 16-byte loads per key)
 constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: record << 6 | key index)
 
 // P5 LDS: table (lcap slots) + misc (48 u32) + per-wave slow-path queues +
@@ -934,8 +935,8 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
     bool done = true, claimed = false, lclaim = false, full = false;
     if (act) {
         const u64 frac = (u64)skm_hash32<W>(qk) << 16;
-        if (!lds_insert<W>(qk, frac, t.lkeys, t.lcnt, t.lstate, a.lcap, last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u),
-                           &lclaim)) {
+        if (!lds_insert<W, kSkmGroup>(qk, frac, t.lkeys, t.lcnt, t.lstate, a.lcap,
+                                      last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u), &lclaim)) {
             if (!last) {
                 full = true;
             } else if constexpr (W == 1) {
@@ -1004,8 +1005,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     __syncthreads();
     const u32 limit = (a.lcap * 13u) >> 4;
     const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;
-    const u32 ng = a.lcap >> 2;
-    const bool grouped = W == 1 && (a.lcap & 3u) == 0;
+    const u32 ng = a.lcap / kSkmGroup;
+    const bool grouped = W == 1 && (a.lcap % kSkmGroup) == 0;
     constexpr u64 M48 = 0xffffffffffffull;
     for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         if (tid == 0)
@@ -1062,8 +1063,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 }
                 const u32 excl = inc - n;
                 const u32 T = (u32)__builtin_amdgcn_readlane((int)inc, 63);
-                if (T == 0) continue;
-                const u32 per = (T + 63) >> 6;
+                if (T == 0 || (a.skip & 4)) continue;
+                const u32 per = (a.skip & 2) ? 0u : (T + 63) >> 6;
                 const u32 s0 = min(T, (u32)lane * per), s1 = min(T, s0 + per);
                 // owner of key s0: the last record whose first key is <= s0
                 int o = 0;
@@ -1084,18 +1085,29 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 const u64 wrec0 = base + (u64)(tid - lane) - lo;  // lane 0's record of this batch
                 // advance to the next key: roll one base in; past the record's
                 // last key move to the next record with keys (this wave's stage)
+                // the record after the current one waits in registers (nxt),
+                // so a switch costs no LDS round trip
+                u64 nxt[RW];
+#pragma unroll
+                for (int j = 0; j < RW; j++) nxt[j] = o < 63 ? wst[(size_t)(o + 1) * RW + j] : 0ull;
                 auto advance = [&](u32 t) {
 #pragma unroll
                     for (int j = 0; j < RW - 1; j++) win[j] = (win[j] << 2) | (win[j + 1] >> 62);
                     win[RW - 1] <<= 2;
                     ++ki;
                     if (ki == nn && s0 + t + 1 < s1) {
-                        do {
+                        ++o;
+#pragma unroll
+                        for (int j = 0; j < RW; j++) cur[j] = nxt[j];
+                        nn = (u32)(cur[RW - 1] & 63u);
+                        while (nn == 0u) {  // padding between records (bucket 0xffff only)
                             ++o;
 #pragma unroll
                             for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
                             nn = (u32)(cur[RW - 1] & 63u);
-                        } while (nn == 0u);
+                        }
+#pragma unroll
+                        for (int j = 0; j < RW; j++) nxt[j] = o < 63 ? wst[(size_t)(o + 1) * RW + j] : 0ull;
                         skm_window<RW>(cur, 16u, win);
                         ki = 0;
                     }
@@ -1109,14 +1121,15 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     u32 kcur = ki;
                     int ocur = o;
                     u32 g = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key), ng);
-                    v2u64 a0 = ((const lds_v2u64*)(lkeys + 4 * g))[0], a1 = ((const lds_v2u64*)(lkeys + 4 * g))[1];
+                    v2u64 a0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[0];
+                    v2u64 a1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[1];
                     for (u32 t = 0; t < per; t++) {
                         advance(t);
                         const bool act_n = s0 + t + 1 < s1;
                         const u64 key_n = win[0] & a.last_mask;
                         const u32 g_n = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key_n), ng);
-                        const lds_v2u64* gpn = (const lds_v2u64*)(lkeys + 4 * g_n);
-                        const v2u64 b0 = gpn[0], b1 = gpn[1];
+                        const v2u64 b0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[0];
+                        const v2u64 b1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[1];
                         bool want = act && !a.skip;
                         if (m > 1) want = want && (u32)(((key & M48) * (u64)m) >> 48) == sub;
                         my_keys += want ? 1u : 0u;
@@ -1128,25 +1141,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                             if (v[i] == 0ull) emp = i;
                         }
                         const bool found = want && hit >= 0 && (emp < 0 || hit < emp);
-                        if (found) atomicAdd(&lcnt[4 * g + hit], 1u);
-                        // a new key takes the group's first empty slot right
-                        // here; only a full group or a lost race queues it
-                        bool pend = want && !found;
-                        bool claim = false;
-                        if (pend && emp >= 0) {
-                            const u64 old = atomicCAS((unsigned long long*)&lkeys[4 * g + emp], 0ull,
-                                                      (unsigned long long)key);
-                            if (old == 0ull || old == key) {
-                                atomicAdd(&lcnt[4 * g + emp], 1u);
-                                claim = old == 0ull;
-                                pend = false;
-                            }
-                        }
-                        const u64 cm = __ballot(claim);
-                        if (cm && lane == 0) {
-                            const u32 f = atomicAdd(lfill, (u32)__popcll(cm)) + (u32)__popcll(cm);
-                            if (!last && f > limit) atomicOr(labort, 1u);
-                        }
+                        if (found) atomicAdd(&lcnt[kSkmGroup * g + hit], 1u);
+                        const bool pend = want && !found;
                         const u64 pb = __ballot(pend);
                         if (pb) {
                             if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = ((wrec0 + (u64)ocur) << 6) | kcur;
@@ -1179,20 +1175,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     my_keys += want ? 1u : 0u;
                     bool found = false;
                     const u32 h = skm_hash32<W>(key);
-                    if (grouped) {
-                        const u32 g = __umulhi(h, ng);
-                        const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
-                        const v2u64 a0 = gp[0], a1 = gp[1];
-                        const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
-                        int hit = -1, emp = -1;
-#pragma unroll
-                        for (int i = 3; i >= 0; i--) {
-                            if (v[i] == key[0]) hit = i;
-                            if (v[i] == 0ull) emp = i;
-                        }
-                        found = want && hit >= 0 && (emp < 0 || hit < emp);
-                        if (found) atomicAdd(&lcnt[4 * g + hit], 1u);
-                    } else if constexpr (W >= 2) {
+                    if constexpr (W >= 2) {
                         const u32 sl = __umulhi(h, a.lcap);
                         if (__hip_atomic_load(&lstate[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
                             bool eq = true;
