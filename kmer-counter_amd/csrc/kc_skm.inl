@@ -154,7 +154,7 @@ constexpr u32 kNoKey = 0xffffu;  // window bucket of a window without a key (dea
 //      of the wave's current pool chunk (one global atomic per chunk); the
 //      chunk tail is padded with n = 0 records at exit
 template <int W>
-__global__ __launch_bounds__(kSkmBlock) void skm_front_k(SkmArgs a) {
+__global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void skm_front_k(SkmArgs a) {
     constexpr int RW = W + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int L = a.L, k = a.k, m = a.m, NG = a.NG, HS = a.HS, R = a.R, Kp = a.Kp, G = a.G;
@@ -856,9 +856,10 @@ constexpr int kSkmGroup = 4;    // P5 LDS table: slots per group (two 16-byte lo
 constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: record << 6 | key index)
 
 // P5 LDS: table (lcap slots) + misc (48 u32) + per-wave slow-path queues +
-// per-wave record stage (64 records of W + 1 words)
+// per-wave record stage (64 records of W + 1 words + one spare, so the record
+// after the last can be read unconditionally)
 static size_t skm_fixed_lds(int W) {
-    return 48 * 4 + (size_t)kBucketWaves * kSkmQueue * 8 + (size_t)kBucketWaves * 64 * (W + 1) * 8 + 16;
+    return 48 * 4 + (size_t)kBucketWaves * kSkmQueue * 8 + (size_t)kBucketWaves * 65 * (W + 1) * 8 + 16;
 }
 
 int skm_lds_slots(int W) {
@@ -989,7 +990,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     const int lane = (int)lane_id();
     const u64 lane_lt = lanemask_lt();
     u64* wq = (u64*)(misc + 48) + (tid >> 6) * kSkmQueue;
-    u64* wst = (u64*)(misc + 48) + kBucketWaves * kSkmQueue + (tid >> 6) * 64 * RW;  // this wave's record stage
+    u64* wst = (u64*)(misc + 48) + kBucketWaves * kSkmQueue + (tid >> 6) * 65 * RW;  // this wave's record stage (+1 spare)
     const SkmLdsTable tab = {lkeys, lcnt, lstate, lfill, labort};
     for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
@@ -1089,7 +1090,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 // so a switch costs no LDS round trip
                 u64 nxt[RW];
 #pragma unroll
-                for (int j = 0; j < RW; j++) nxt[j] = o < 63 ? wst[(size_t)(o + 1) * RW + j] : 0ull;
+                for (int j = 0; j < RW; j++) nxt[j] = wst[(size_t)(o + 1) * RW + j];
                 auto advance = [&](u32 t) {
 #pragma unroll
                     for (int j = 0; j < RW - 1; j++) win[j] = (win[j] << 2) | (win[j + 1] >> 62);
@@ -1106,9 +1107,13 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                             for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
                             nn = (u32)(cur[RW - 1] & 63u);
                         }
-#pragma unroll
-                        for (int j = 0; j < RW; j++) nxt[j] = o < 63 ? wst[(size_t)(o + 1) * RW + j] : 0ull;
                         skm_window<RW>(cur, 16u, win);
+                        // unconditional (spare record past the last) and issued
+                        // after cur's last use, into nxt's own registers: the value
+                        // is needed only at the next switch, so no wait here
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int j = 0; j < RW; j++) nxt[j] = wst[(size_t)(o + 1) * RW + j];
                         ki = 0;
                     }
                 };
@@ -1133,14 +1138,11 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         bool want = act && !a.skip;
                         if (m > 1) want = want && (u32)(((key & M48) * (u64)m) >> 48) == sub;
                         my_keys += want ? 1u : 0u;
-                        const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
-                        int hit = -1, emp = -1;
-#pragma unroll
-                        for (int i = 3; i >= 0; i--) {
-                            if (v[i] == key) hit = i;
-                            if (v[i] == 0ull) emp = i;
-                        }
-                        const bool found = want && hit >= 0 && (emp < 0 || hit < emp);
+                        // a key sits in at most one slot and is never 0 (key 0^W
+                        // is counted outside the table), so any equal slot is it
+                        const bool e0 = a0.x == key, e1 = a0.y == key, e2 = a1.x == key, e3 = a1.y == key;
+                        const int hit = e0 ? 0 : (e1 ? 1 : (e2 ? 2 : 3));
+                        const bool found = want && (e0 || e1 || e2 || e3);
                         if (found) atomicAdd(&lcnt[kSkmGroup * g + hit], 1u);
                         const bool pend = want && !found;
                         const u64 pb = __ballot(pend);
