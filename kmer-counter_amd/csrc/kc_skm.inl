@@ -1008,7 +1008,6 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;
     const u32 ng = a.lcap / kSkmGroup;
     const bool grouped = W == 1 && (a.lcap % kSkmGroup) == 0;
-    constexpr u64 M48 = 0xffffffffffffull;
     for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         if (tid == 0)
             *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
@@ -1027,20 +1026,28 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
         u32 m = 1, sub = 0;
         while (sub < m) {
             const bool last = m >= mmax;
+            // sub-range of a key: bits [48 - log2 m, 48) (m is a power of two),
+            // = ((key & M48) * m) >> 48 as in count_buckets
+            const u32 msh = 48u - (31u - (u32)__builtin_clz(m));
             u64 scanned = 0;
             u32 my_keys = 0;
             u32 qn = 0;
-            // records of the next PD batches (one per thread per batch) in flight
+            // every wave takes an equal contiguous share of the bucket's
+            // records, 64 at a time (no wave idles through a short last batch);
+            // the records of its next PD batches (one per lane) are in flight
+            const u64 nrec_b = hi - lo;
+            const u64 per_w = (nrec_b + kBucketWaves - 1) / kBucketWaves;
+            const u64 wlo = lo + min(nrec_b, (u64)(tid >> 6) * per_w), whi = lo + min(nrec_b, (u64)((tid >> 6) + 1) * per_w);
             u64 pf[PD][RW];
 #pragma unroll
             for (int d = 0; d < PD; d++) {
-                const u64 i = lo + (u64)d * kBucketBlock + tid;
+                const u64 i = wlo + (u64)d * 64 + lane;
 #pragma unroll
-                for (int j = 0; j < RW; j++) pf[d][j] = i < hi ? a.recs[(u64)j * a.stride + i] : 0ull;
+                for (int j = 0; j < RW; j++) pf[d][j] = i < whi ? a.recs[(u64)j * a.stride + i] : 0ull;
             }
-            for (u64 base = lo; base < hi; base += (u64)kBucketBlock) {
+            for (u64 base = wlo; base < whi; base += 64) {
                 if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                scanned += (u64)kBucketBlock;
+                scanned += 64;
                 // this batch's record -> the wave's LDS stage; next loads issued
 #pragma unroll
                 for (int j = 0; j < RW; j++) wst[(size_t)lane * RW + j] = pf[0][j];
@@ -1050,9 +1057,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
 #pragma unroll
                     for (int j = 0; j < RW; j++) pf[d][j] = pf[d + 1][j];
                 {
-                    const u64 i = base + (u64)PD * kBucketBlock + tid;
+                    const u64 i = base + (u64)PD * 64 + lane;
 #pragma unroll
-                    for (int j = 0; j < RW; j++) pf[PD - 1][j] = i < hi ? a.recs[(u64)j * a.stride + i] : 0ull;
+                    for (int j = 0; j < RW; j++) pf[PD - 1][j] = i < whi ? a.recs[(u64)j * a.stride + i] : 0ull;
                 }
                 // the wave's keys as one flat sequence: exclusive scan of the
                 // records' key counts; lane l takes keys [l*per, l*per + per)
@@ -1083,7 +1090,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 u32 nn = (u32)(cur[RW - 1] & 63u);
                 u64 win[RW];
                 skm_window<RW>(cur, 16u + 2u * ki, win);
-                const u64 wrec0 = base + (u64)(tid - lane) - lo;  // lane 0's record of this batch
+                const u64 wrec0 = base - lo;  // lane 0's record of this batch
                 // advance to the next key: roll one base in; past the record's
                 // last key move to the next record with keys (this wave's stage)
                 // the record after the current one waits in registers (nxt),
@@ -1100,13 +1107,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         ++o;
 #pragma unroll
                         for (int j = 0; j < RW; j++) cur[j] = nxt[j];
+                        // every record of a counted bucket has n >= 1: F writes
+                        // n = 0 padding only into bucket 0xffff, never counted
                         nn = (u32)(cur[RW - 1] & 63u);
-                        while (nn == 0u) {  // padding between records (bucket 0xffff only)
-                            ++o;
-#pragma unroll
-                            for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
-                            nn = (u32)(cur[RW - 1] & 63u);
-                        }
                         skm_window<RW>(cur, 16u, win);
                         // unconditional (spare record past the last) and issued
                         // after cur's last use, into nxt's own registers: the value
@@ -1136,7 +1139,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         const v2u64 b0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[0];
                         const v2u64 b1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[1];
                         bool want = act && !a.skip;
-                        if (m > 1) want = want && (u32)(((key & M48) * (u64)m) >> 48) == sub;
+                        want = want && ((u32)(key >> msh) & (m - 1u)) == sub;
                         my_keys += want ? 1u : 0u;
                         // a key sits in at most one slot and is never 0 (key 0^W
                         // is counted outside the table), so any equal slot is it
@@ -1173,7 +1176,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     for (int j = 0; j < W; j++) key[j] = win[j];
                     key[W - 1] &= a.last_mask;
                     bool want = act && !a.skip;
-                    if (m > 1) want = want && (u32)(((key[0] & M48) * (u64)m) >> 48) == sub;
+                    want = want && ((u32)(key[0] >> msh) & (m - 1u)) == sub;
                     my_keys += want ? 1u : 0u;
                     bool found = false;
                     const u32 h = skm_hash32<W>(key);
@@ -1216,8 +1219,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     // fraction f of its records: linear when keys repeat rarely
                     // in the scanned part, ~all seen already when they repeat
                     // often (genome coverage)
-                    const u64 nrec_b = hi - lo;
-                    const float f = (float)min(scanned, nrec_b) / (float)(nrec_b ? nrec_b : 1);
+                    // (wave 0's share stands for the bucket)
+                    const u64 w0n = min(nrec_b, per_w);
+                    const float f = (float)min(scanned, w0n) / (float)(w0n ? w0n : 1);
                     const float rep = (float)(*lkscan) / (float)(*lfill ? *lfill : 1u);
                     const float seen = rep >= 4.f ? 1.f : (rep >= 2.f ? fmaxf(f, 0.5f) : fmaxf(f, 1e-6f));
                     const u64 est = (u64)((float)(*lfill) * (float)m / seen);
