@@ -213,15 +213,17 @@ def main():
         # writes the records (8(W+1) B each); each of the two grouping scatters
         # reads and writes every record; P5 reads the records and writes the
         # distinct (key, count) records
+        # (S: two scatter launches per batch, each over all records; P5: the
+        # cardinality sample and the main launch together are one pass over
+        # the records, priced per batch)
         rec_step = st["keys"] or 1  # records handed out by F per step
         rb = 8 * (W + 1)
-        p5_per_step = max(1, st["p5_launches"])
         specs = [
             ("F", f"skm_front_k<{W}>", part_ms[1], launches, windows_step, "k-mers",
              (G * 6) / max(1, L - k + 1) + rb * rec_step / windows_step),
-            ("S", f"rp_scatter_k<{W + 1},false>", part_ms[2], 2 * steps * st["batches"], rec_step, "records",
+            ("S", f"rp_scatter_k<{W + 1},false>", part_ms[2], 2 * steps * st["batches"], 2 * rec_step, "records",
              2 * rb + 1),
-            ("P5", f"count_skm_k<{W}>", part_ms[4], steps * p5_per_step, rec_step, "records",
+            ("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], rec_step, "records",
              rb + (8 * W + 4) * recs_step / rec_step),
         ]
     elif used & 2:

@@ -1145,17 +1145,21 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
         uint64_t* fb_n = (uint64_t*)c->desc_lens.p;  // desc_lens is consumed by the scan above
         if ((s = ensure(c, c->desc_fb, ndesc * 4 + 16))) return s;
         fb = (uint32_t*)c->desc_fb.p;
+        // sorted straight into the packed output, after the key-0 record
+        if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
         HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, order, (const uint64_t*)c->desc_start.p,
                                   (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, k0 + off0,
-                                  c0 + off0, out_cap, c->stats, fb, fb_n, c->n_cu, c->stream));
-    }
-    if (key0) {
-        for (int j = 0; j < W; j++) HIPCHK(c, hipMemsetAsync(k0 + (size_t)j * out_cap, 0, 8, c->stream));
-        uint32_t kc0 = (uint32_t)c->stats_h[ST_KEY0];
-        HIPCHK(c, hipMemcpyAsync(c0, &kc0, 4, hipMemcpyHostToDevice, c->stream));
+                                  c0 + off0, out_cap, c->stats, fb, fb_n, c->n_cu, c->stream,
+                                  (char*)c->fin_packed.p + off0 * c->rs));
     }
     if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
-    HIPCHK(c, launch_pack(W, k0, out_cap, c0, n, c->fin_packed.p, c->stream));
+    // record 0: key 0^W (all-zero words) and its count (kept alive until the
+    // stream is synchronised below)
+    std::vector<uint32_t> r0((size_t)c->rs / 4, 0u);
+    if (key0) {
+        r0.back() = (uint32_t)c->stats_h[ST_KEY0];
+        HIPCHK(c, hipMemcpyAsync(c->fin_packed.p, r0.data(), c->rs, hipMemcpyHostToDevice, c->stream));
+    }
     if ((s = sync_stats(c))) return s;
     if (c->stats_h[ST_ERR] & ERR_SEG_TOO_LONG) return fail(c, KC_ERR_INTERNAL, "segment longer than its LDS sort");
     *n_out = n;
@@ -1224,12 +1228,19 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
         HIPCHK(c, hipMemcpyAsync(c->desc_len.p, lens.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, nb, c->stream));
         uint64_t* fb_n = (uint64_t*)((char*)c->desc_fb.p + (size_t)nb * 4);
+        // one batch, no table records: keys are distinct, so the groups are
+        // sorted straight into the packed output
+        if (!dups && (s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
         HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, (const uint32_t*)c->desc_v.p,
                                   (const uint64_t*)c->part_starts.p, (const uint32_t*)c->desc_len.p,
                                   (const uint64_t*)c->part_starts.p, nb, k0, c0, out_cap, c->stats,
-                                  (uint32_t*)c->desc_fb.p, fb_n, c->n_cu, c->stream));
+                                  (uint32_t*)c->desc_fb.p, fb_n, c->n_cu, c->stream, dups ? nullptr : c->fin_packed.p));
         if ((s = sync_stats(c))) return s;
         if (c->stats_h[ST_ERR] & ERR_SEG_TOO_LONG) return fail(c, KC_ERR_INTERNAL, "segment longer than its LDS sort");
+        if (!dups) {
+            *n_out = n;
+            return KC_OK;
+        }
         return reduce_pack(c, out_cap, n, 0, dups, n_out);
     }
     if (n) {

@@ -2474,6 +2474,26 @@ size_t seg_sort_lds(int W) {
     return (size_t)cap * (8 * W + 2) + (size_t)2 * kSegWaves * 256 * 4 + 512 * 4 + 2 * 4 * kSegWaves * 8 + 64;
 }
 
+// Output of a sorted record: SoA (okeys/ocnts) or, when `packed` is given,
+// straight into SortedKMerFile layout (W LE u64 words + LE u32 count).
+template <int W>
+__device__ __forceinline__ void seg_put(u64* __restrict__ okeys, u32* __restrict__ ocnts, u64 ostride,
+                                        u32* __restrict__ packed, u64 pos, const u64 (&k)[W], u32 cnt) {
+    if (packed) {
+        u32* o = packed + pos * (2 * W + 1);
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            o[2 * j] = (u32)k[j];
+            o[2 * j + 1] = (u32)(k[j] >> 32);
+        }
+        o[2 * W] = cnt;
+    } else {
+#pragma unroll
+        for (int j = 0; j < W; j++) okeys[(u64)j * ostride + pos] = k[j];
+        ocnts[pos] = cnt;
+    }
+}
+
 // MSD segment sort: the bits just below the bucket prefix and the pass's
 // sub-range bits (known from the descriptor) give a 12-bit digit; a counting
 // pass and a scatter pass stream the segment from global memory (L2-resident
@@ -2486,7 +2506,8 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
                                                         const u64* __restrict__ dstart, const u32* __restrict__ dlen,
                                                         const u64* __restrict__ out_off, u64 ndesc,
                                                         u64* __restrict__ okeys, u32* __restrict__ ocnts,
-                                                        u64 ostride, u64* __restrict__ stats, u32* __restrict__ fb,
+                                                        u64 ostride, u32* __restrict__ packed,
+                                                        u64* __restrict__ stats, u32* __restrict__ fb,
                                                         u64* __restrict__ fb_n) {
     constexpr int CAP = SegCfg<W>::CAP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2587,9 +2608,10 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         }
         __syncthreads();
         for (u32 p = tid; p < len; p += kSegBlock) {
+            u64 kk[W];
 #pragma unroll
-            for (int jj = 0; jj < W; jj++) okeys[(u64)jj * ostride + obase + p] = skey[(size_t)jj * CAP + p];
-            ocnts[obase + p] = rcnts[st + sidx[p]];
+            for (int jj = 0; jj < W; jj++) kk[jj] = skey[(size_t)jj * CAP + p];
+            seg_put<W>(okeys, ocnts, ostride, packed, obase + p, kk, rcnts[st + sidx[p]]);
         }
         __syncthreads();
     }
@@ -2603,7 +2625,8 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_lsd_k(const u64* __restric
                                                         const u64* __restrict__ dstart, const u32* __restrict__ dlen,
                                                         const u64* __restrict__ out_off, u64 ndesc,
                                                         u64* __restrict__ okeys, u32* __restrict__ ocnts,
-                                                        u64 ostride, u64* __restrict__ stats,
+                                                        u64 ostride, u32* __restrict__ packed,
+                                                        u64* __restrict__ stats,
                                                         const u32* __restrict__ fb, const u64* __restrict__ fb_n) {
     constexpr int CAP = SegCfg<W>::CAP;
     constexpr int ITEMS = SegCfg<W>::ITEMS;
@@ -2766,9 +2789,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_lsd_k(const u64* __restric
         for (int it = 0; it < ITEMS; it++) {
             const u32 p = (u32)(wave * 64 * R + it * 64 + lane);
             if (it < R && p < len) {
-#pragma unroll
-                for (int jj = 0; jj < W; jj++) okeys[(u64)jj * ostride + obase + p] = key[it][jj];
-                ocnts[obase + p] = rcnts[st + idx[it]];
+                seg_put<W>(okeys, ocnts, ostride, packed, obase + p, key[it], rcnts[st + idx[it]]);
             }
         }
     }
@@ -2777,7 +2798,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_lsd_k(const u64* __restric
 hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, uint64_t rstride, const uint32_t* order,
                            const uint64_t* dstart, const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc,
                            uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, uint32_t* fb,
-                           uint64_t* fb_n, int grid, hipStream_t s) {
+                           uint64_t* fb_n, int grid, hipStream_t s, void* packed) {
     if (ndesc == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(fb_n, 0, 8, s);
     if (e != hipSuccess) return e;
@@ -2785,9 +2806,10 @@ hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, 
     const size_t lds = (seg_sort_lds(W) + 15) & ~(size_t)15;
 #define KC_SEG(WW)                                                                                                  \
     hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds_msd, s, rkeys, rcnts, rstride, order,       \
-                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, stats, fb, fb_n);                       \
+                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, fb, fb_n);       \
     hipLaunchKernelGGL(seg_sort_lsd_k<WW>, dim3(grid), dim3(kSegBlock), lds, s, rkeys, rcnts, rstride, order,       \
-                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, stats, (const u32*)fb, (const u64*)fb_n)
+                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, (const u32*)fb,   \
+                       (const u64*)fb_n)
     switch (W) {
     case 1: KC_SEG(1); break;
     case 2: KC_SEG(2); break;
