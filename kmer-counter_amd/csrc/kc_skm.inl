@@ -354,10 +354,12 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
             u32 smask = 0, emask = 0;
             int q0 = 0;
             u32 bk[8];
+            v4u pkv;
             if (c < nr * nchr) {
                 const int r = (int)div_nchr.div((u32)c), p0 = (c - r * nchr) * 8;
                 q0 = r * nw + p0;
                 const v4u pk = wpk[c];
+                pkv = pk;
                 bk[0] = pk.x & 0xffffu;
                 bk[1] = pk.x >> 16;
                 bk[2] = pk.y & 0xffffu;
@@ -384,11 +386,13 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
             const u32 ex = inc - v;
             const u32 tot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
             u32 sp = sbase + (ex & 0xffffu), ep = ebase + (ex >> 16);
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                if ((smask >> i) & 1u) sa[sp++] = (u32)(q0 + i) | (bk[i] << 16);
-                if ((emask >> i) & 1u) ea[ep++] = (unsigned short)(q0 + i);
+            // set bits only (a lane holds one or two starts and ends)
+            for (u32 mm = smask; mm; mm &= mm - 1u) {
+                const int i = __builtin_ctz(mm);
+                const u32 wv = (i & 4) ? ((i & 2) ? pkv.w : pkv.z) : ((i & 2) ? pkv.y : pkv.x);
+                sa[sp++] = (u32)(q0 + i) | (((wv >> (16 * (i & 1))) & 0xffffu) << 16);
             }
+            for (u32 mm = emask; mm; mm &= mm - 1u) ea[ep++] = (unsigned short)(q0 + __builtin_ctz(mm));
             sbase += tot & 0xffffu;
             ebase += tot >> 16;
         }
