@@ -52,12 +52,20 @@ __device__ __forceinline__ u32 fmix32(u32 x) {
     return x;
 }
 
-// m-mer order: m <= 16 (one u32) uses a multiplicative hash of the m-mer,
-// whose low 16 bits (the bucket) are a bijection of its last 8 bases; longer
-// m-mers are folded to 32 bits first
+// m-mer order: m <= 12 uses a 24-bit multiplicative hash of the m-mer (full
+// rate), m <= 16 a 32-bit one; either way the low 16 bits (the bucket) are a
+// bijection of its last 8 bases. Longer m-mers are folded to 32 bits first.
 __device__ __forceinline__ u32 mmer_hash(u64 mm) {
     const u32 x = (u32)mm ^ ((u32)(mm >> 32) * 0x9e3779b1u);
     return (x ^ 0x5bd1e995u) * 0x9e3779b1u;
+}
+
+// full-rate 24 x 24 -> low 32 bits multiply by a uniform b (the compiler
+// keeps v_mul_lo_u32)
+__device__ __forceinline__ u32 mul_u24(u32 a, u32 b) {
+    u32 r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(b), "v"(a));
+    return r;
 }
 
 __device__ __forceinline__ u64 readlane64(u64 v, int l) {
@@ -162,11 +170,11 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
     const int nw = L - k + 1;
     const int wm = k - m + 1;  // m-mers per window (>= 8)
     const int nchr = (nw + 7) >> 3;
-    const int HSK = skm_hsk(HS);
     const int hq = a.hq;
     const int hch = (HS + hq - 1) / hq;
+    const int HSK = skm_hsk(hch * hq);  // hash items cover hch * hq positions
     const FastDivU div_nchr((u32)nchr), div_hch((u32)hch), div_nw((u32)nw), div_g((u32)G);
-    const SkmLds lay = skm_lds_layout(R, NG, HS, nw);
+    const SkmLds lay = skm_lds_layout(R, NG, hch * hq, nw);
     const int wave = threadIdx.x >> 6, lane = lane_id();
     unsigned char* wb = smem + (size_t)wave * lay.total;
     u32* codes = (u32*)(wb + lay.codes);
@@ -182,7 +190,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
     const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
     const u64 nwaves = (u64)gridDim.x * (kSkmBlock / 64);
     const u64 chunk = a.chunk;
-    const bool m16 = m <= 16;
+    const bool m16 = m <= 16, m12 = m <= 12;
     u64 my_valid = 0;
     bool my_hole = false;
     for (int it = lane; it < R * NG; it += 64) {
@@ -250,7 +258,17 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
             const int r = (int)div_hch.div((u32)it), j0 = (it - r * hch) * hq;
             const u64 x = code_word(codes + r * NG, j0);
             u32* hr = hm + r * HSK;
-            if (m16) {
+            if (m12) {
+                // m <= 12: the m-mer fits 24 bits, so the full-rate 24-bit
+                // multiply orders it (odd constant: a bijection)
+                // (hm is padded to hch * hq positions: no bound check)
+                u64 xs = x;
+                for (int i = 0; i < hq; i++) {
+                    const u32 mm = (u32)(xs >> (64 - 2 * m));
+                    hr[skm_sk(j0 + i)] = mul_u24(mm ^ 0xd1e995u, 0x9e3779u);
+                    xs <<= 2;
+                }
+            } else if (m16) {
                 const u32 xh = (u32)(x >> 32), xl = (u32)x;
                 for (int i = 0; i < hq; i++) {
                     const u32 w = i == 0 ? xh : (i < 16 ? __builtin_amdgcn_alignbit(xh, xl, 32 - 2 * i) : xl << (2 * i - 32));
@@ -498,7 +516,7 @@ SkmGeom skm_geometry(int L, int k) {
     if (g.hq > 32 - m + 1) g.hq = 32 - m + 1;
     if (g.hq > 22) g.hq = 22;
     if (g.hq < 1) g.hq = 1;
-    g.lds = (size_t)(kSkmBlock / 64) * skm_lds_layout(R, g.NG, g.HS, nw).total;
+    g.lds = (size_t)(kSkmBlock / 64) * skm_lds_layout(R, g.NG, (g.HS + g.hq - 1) / g.hq * g.hq, nw).total;
     if (g.lds > 160 * 1024) return g;
     g.ok = true;
     return g;
