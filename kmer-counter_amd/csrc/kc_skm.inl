@@ -125,10 +125,12 @@ __host__ __device__ inline SkmLds skm_lds_layout(int R, int NG, int HS, int nw) 
     return o;
 }
 
+// Intra-wave LDS hand-off (lane a writes, lane b reads): the fences are
+// limited to LDS, so they never wait for global loads in flight (prefetch)
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 // Inclusive scan of one u32 per lane over the wave (Hillis-Steele).
@@ -875,7 +877,7 @@ __device__ __forceinline__ void skm_key(const u64 (&rw)[W + 1], u32 i, u64 last_
 }
 
 constexpr int kSkmGroup = 4;    // P5 LDS table: slots per group (two 16-byte loads per key)
-constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: record << 6 | key index)
+constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: key at W = 1, else record << 6 | key index)
 
 // P5 LDS: table (lcap slots) + misc (48 u32) + per-wave slow-path queues +
 // per-wave record stage (64 records of W + 1 words + one spare, so the record
@@ -934,7 +936,8 @@ struct SkmLdsTable {
     u32* labort;
 };
 
-// Slow path for the first c entries of a wave's queue (record << 6 | key):
+// Slow path for the first c entries of a wave's queue (the key itself at
+// W = 1, else record << 6 | key index):
 // full probing insert into the LDS table, fill/abort accounting, and at the
 // last sub-range level the global table and the spill buffer. Out of line:
 // it runs once per 64 queued keys and keeps the hot loop small.
@@ -949,11 +952,15 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
     for (int j = 0; j < W; j++) qk[j] = 0;
     if (act) {
         const u64 e = wq[lane];
-        const u64 ri = lo + (e >> 6);
-        u64 rw[RW];
+        if constexpr (W == 1) {
+            qk[0] = e;  // W = 1 queues the key itself
+        } else {
+            const u64 ri = lo + (e >> 6);
+            u64 rw[RW];
 #pragma unroll
-        for (int j = 0; j < RW; j++) rw[j] = a.recs[(u64)j * a.stride + ri];
-        skm_key<W>(rw, (u32)(e & 63u), a.last_mask, qk);
+            for (int j = 0; j < RW; j++) rw[j] = a.recs[(u64)j * a.stride + ri];
+            skm_key<W>(rw, (u32)(e & 63u), a.last_mask, qk);
+        }
     }
     bool done = true, claimed = false, lclaim = false, full = false;
     if (act) {
@@ -1104,7 +1111,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     if (e <= s0) o += st;
                 }
                 u32 ki = s0 - (u32)__shfl((int)excl, o);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
                 __builtin_amdgcn_wave_barrier();
                 u64 cur[RW];
 #pragma unroll
@@ -1148,8 +1155,6 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     // the slow path only sends that key to the slow path again)
                     u64 key = win[0] & a.last_mask;
                     bool act = s0 < s1;
-                    u32 kcur = ki;
-                    int ocur = o;
                     u32 g = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key), ng);
                     v2u64 a0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[0];
                     v2u64 a1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[1];
@@ -1172,7 +1177,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         const bool pend = want && !found;
                         const u64 pb = __ballot(pend);
                         if (pb) {
-                            if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = ((wrec0 + (u64)ocur) << 6) | kcur;
+                            if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = key;
                             qn += (u32)__popcll(pb);
                             if (qn >= 64) {
                                 skm_drain<W>(a, tab, wq, 64, lo, last, limit);
@@ -1187,8 +1192,6 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         g = g_n;
                         a0 = b0;
                         a1 = b1;
-                        kcur = ki;
-                        ocur = o;
                     }
                 } else {
                 for (u32 t = 0; t < per; t++) {
@@ -1215,7 +1218,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     const bool pend = want && !found;
                     const u64 pb = __ballot(pend);
                     if (pb) {
-                        if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = ((wrec0 + (u64)o) << 6) | ki;
+                        if (pend)
+                            wq[qn + (u32)__popcll(pb & lane_lt)] = W == 1 ? key[0] : (((wrec0 + (u64)o) << 6) | ki);
                         qn += (u32)__popcll(pb);
                         if (qn >= 64) {
                             skm_drain<W>(a, tab, wq, 64, lo, last, limit);
