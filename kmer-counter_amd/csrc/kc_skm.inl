@@ -687,6 +687,8 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
         }
     };
     load(blockIdx.x);
+    // this tile's 256 global run starts, loaded one tile ahead like the items
+    u64 npos = (tid < 256 && blockIdx.x < ntiles) ? pos[(u64)blockIdx.x * 256 + tid] : 0ull;
     for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
         u64 lo, hi;
         rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
@@ -700,9 +702,10 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
             pv[i] = PAY ? np[i] : 0u;
         }
         for (int i = tid; i < 16 * 128; i += kP3Block) wc[i] = 0;
-        if (tid < 256) gpos[tid] = pos[t * 256 + tid];
+        if (tid < 256) gpos[tid] = npos;
         __syncthreads();
         load(t + gridDim.x);
+        if (tid < 256 && t + gridDim.x < ntiles) npos = pos[(t + gridDim.x) * 256 + tid];
         u32 rank[KPT];
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
