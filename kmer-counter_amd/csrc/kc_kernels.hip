@@ -794,7 +794,10 @@ __global__ __launch_bounds__(kBlock) void encode_reads_k(const uint8_t* __restri
         const u64 off = (seq_off ? seq_off[gr] : gr * (u64)L) + 16 * (u64)g;
         const int nb = min(16, L - 16 * g);
         const uintptr_t addr = (uintptr_t)(base + off);
-        const u32* dw = (const u32*)(addr & ~(uintptr_t)3);
+        // (global address space spelled out: the integer round trip would
+        // otherwise leave FLAT loads)
+        typedef __attribute__((address_space(1))) const u32 g32;
+        const g32* dw = (const g32*)(addr & ~(uintptr_t)3);
         const int sh = (int)(addr & 3);
         // only dwords holding a byte of this group are read (no load past the text)
         u32 d[5];
@@ -3052,7 +3055,8 @@ __global__ __launch_bounds__(kBlock) void fq_count_k(const uint8_t* __restrict__
             uintptr_t addr = A + c * kFqChunk + (u64)it * 4096 + (u64)threadIdx.x * 16;
             long long rel0 = (long long)(addr - (uintptr_t)base);
             if (rel0 + 16 <= 0 || rel0 >= (long long)n) continue;
-            uint4 v = *(const uint4*)addr;
+            const v4u w4 = *(const __attribute__((address_space(1))) v4u*)addr;
+            const uint4 v = make_uint4(w4.x, w4.y, w4.z, w4.w);
             cnt += __popc(nl_mask16(v, rel0, n));
         }
         for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
@@ -3080,7 +3084,8 @@ __global__ __launch_bounds__(kBlock) void fq_emit_k(const uint8_t* __restrict__ 
             long long rel0 = (long long)(addr - (uintptr_t)base);
             u32 m = 0;
             if (!(rel0 + 16 <= 0 || rel0 >= (long long)n)) {
-                uint4 v = *(const uint4*)addr;
+                const v4u w4 = *(const __attribute__((address_space(1))) v4u*)addr;
+            const uint4 v = make_uint4(w4.x, w4.y, w4.z, w4.w);
                 m = nl_mask16(v, rel0, n);
             }
             u32 total;
