@@ -801,8 +801,19 @@ __global__ __launch_bounds__(kBlock) void encode_reads_k(const uint8_t* __restri
         const int sh = (int)(addr & 3);
         // only dwords holding a byte of this group are read (no load past the text)
         u32 d[5];
+        if (sh + nb > 12) {
+            // the first four dwords in one (4-byte aligned) 16-byte load
+            typedef v4u v4u_a4 __attribute__((aligned(4)));
+            const v4u q = __builtin_nontemporal_load((const __attribute__((address_space(1))) v4u_a4*)dw);
+            d[0] = q.x;
+            d[1] = q.y;
+            d[2] = q.z;
+            d[3] = q.w;
+            d[4] = (16 < sh + nb) ? __builtin_nontemporal_load(dw + 4) : 0u;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 5; i++) d[i] = (4 * i < sh + nb) ? __builtin_nontemporal_load(dw + i) : 0u;
+            for (int i = 0; i < 5; i++) d[i] = (4 * i < sh + nb) ? __builtin_nontemporal_load(dw + i) : 0u;
+        }
         const u32 x0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
         const u32 x1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
         const u32 x2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
