@@ -3028,7 +3028,8 @@ hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, 
 // copies (the line before each '+' line, FASTQFileReader.cpp:57-63).
 // ---------------------------------------------------------------------------
 
-constexpr u64 kFqChunk = 65536;  // 256 threads x 16 B x 16 iterations
+constexpr u64 kFqChunk = 16384;  // one wave: 64 lanes x 16 B x 16 iterations
+constexpr int kFqWaves = kBlock / 64;
 
 uint64_t fq_chunks(const void* base, uint64_t n) {
     u64 lead = (u64)((uintptr_t)base & 15);
@@ -3055,58 +3056,85 @@ __device__ __forceinline__ u32 nl_mask16(const uint4 v, long long rel0, u64 n) {
     return m & 0xffffu;
 }
 
+// 16 bytes of the block (global address space spelled out: no FLAT load)
+__device__ __forceinline__ uint4 fq_load16(uintptr_t addr) {
+    const v4u w4 = *(const __attribute__((address_space(1))) v4u*)addr;
+    return make_uint4(w4.x, w4.y, w4.z, w4.w);
+}
+
+// Every wave counts the newlines of its own chunks (no workgroup barrier).
 __global__ __launch_bounds__(kBlock) void fq_count_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                      u64* __restrict__ counts) {
-    __shared__ u32 part[4];
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
-    for (u64 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    for (u64 c = (u64)blockIdx.x * kFqWaves + wave; c < nchunks; c += (u64)gridDim.x * kFqWaves) {
         u32 cnt = 0;
 #pragma unroll 4
         for (int it = 0; it < 16; it++) {
-            uintptr_t addr = A + c * kFqChunk + (u64)it * 4096 + (u64)threadIdx.x * 16;
-            long long rel0 = (long long)(addr - (uintptr_t)base);
+            const uintptr_t addr = A + c * kFqChunk + (u64)it * 1024 + (u64)lane * 16;
+            const long long rel0 = (long long)(addr - (uintptr_t)base);
             if (rel0 + 16 <= 0 || rel0 >= (long long)n) continue;
-            const v4u w4 = *(const __attribute__((address_space(1))) v4u*)addr;
-            const uint4 v = make_uint4(w4.x, w4.y, w4.z, w4.w);
-            cnt += __popc(nl_mask16(v, rel0, n));
+            cnt += __popc(nl_mask16(fq_load16(addr), rel0, n));
         }
         for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
-        if (lane_id() == 0) part[threadIdx.x >> 6] = cnt;
-        __syncthreads();
-        if (threadIdx.x == 0) counts[c] = (u64)part[0] + part[1] + part[2] + part[3];
-        __syncthreads();
+        if (lane == 0) counts[c] = cnt;
     }
 }
 
+// The byte after byte b of a 16-byte load (at block offset q): from the load
+// itself, from the next lane's load (nxw: its first word) for the last byte,
+// from memory only at the wave's last lane (the caller checks q + 1 < n).
+__device__ __forceinline__ u32 fq_next_byte(const uint4 v, u32 nxw, int b, const uint8_t* __restrict__ base, u64 q) {
+    if (b == 15) return lane_id() < 63 ? (nxw & 255u) : (u32)base[q + 1];
+    const int i = b + 1;
+    const u32 w = (i & 8) ? ((i & 4) ? v.w : v.z) : ((i & 4) ? v.y : v.x);
+    return (w >> (8 * (i & 3))) & 255u;
+}
+
+// Every wave numbers the newlines of its own chunks from the chunk's line
+// base (wave scans only, no workgroup barrier; the next 1 KiB slice is
+// loaded while this one is emitted).
 __global__ __launch_bounds__(kBlock) void fq_emit_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                     const u64* __restrict__ line_base, u64* __restrict__ seq_off,
                                                     u64* __restrict__ seq_end, u64 max_rec, u64* stats) {
-    __shared__ u32 scan_tmp[4];
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
     u64 err = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (n == 0 || base[0] != '@') err |= ERR_FQ_NOT_AT;
         if (n > 0 && base[n - 1] != '\n') err |= ERR_FQ_NO_FINAL_NL;
     }
-    for (u64 c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    auto load = [&](u64 c, int it, long long* rel) {
+        const uintptr_t addr = A + c * kFqChunk + (u64)it * 1024 + (u64)lane * 16;
+        *rel = (long long)(addr - (uintptr_t)base);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (!(*rel + 16 <= 0 || *rel >= (long long)n)) v = fq_load16(addr);
+        return v;
+    };
+    for (u64 c = (u64)blockIdx.x * kFqWaves + wave; c < nchunks; c += (u64)gridDim.x * kFqWaves) {
         u64 run = line_base[c];
+        long long reln;
+        uint4 vn = load(c, 0, &reln);
         for (int it = 0; it < 16; it++) {
-            uintptr_t addr = A + c * kFqChunk + (u64)it * 4096 + (u64)threadIdx.x * 16;
-            long long rel0 = (long long)(addr - (uintptr_t)base);
-            u32 m = 0;
-            if (!(rel0 + 16 <= 0 || rel0 >= (long long)n)) {
-                const v4u w4 = *(const __attribute__((address_space(1))) v4u*)addr;
-            const uint4 v = make_uint4(w4.x, w4.y, w4.z, w4.w);
-                m = nl_mask16(v, rel0, n);
+            const uint4 v = vn;
+            const long long rel0 = reln;
+            if (it < 15) vn = load(c, it + 1, &reln);
+            u32 m = (rel0 + 16 <= 0 || rel0 >= (long long)n) ? 0u : nl_mask16(v, rel0, n);
+            const u32 nxw = (u32)__shfl_down((int)v.x, 1);
+            const u32 cnt = (u32)__popc(m);
+            u32 inc = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
             }
-            u32 total;
-            u32 before = block_excl_scan((u32)__popc(m), scan_tmp, &total);
-            u64 j = run + before;
+            u64 j = run + (inc - cnt);
+            run += (u32)__shfl((int)inc, 63);
             while (m) {
-                int b = __ffs(m) - 1;
+                const int b = __ffs(m) - 1;
                 m &= m - 1;
-                u64 q = (u64)(rel0 + b);
-                u64 rec = j >> 2;
+                const u64 q = (u64)(rel0 + b);
+                const u64 rec = j >> 2;
                 switch (j & 3) {
                 case 0:
                     if (rec < max_rec) seq_off[rec] = q + 1;
@@ -3115,16 +3143,15 @@ __global__ __launch_bounds__(kBlock) void fq_emit_k(const uint8_t* __restrict__ 
                 case 1:
                     if (rec < max_rec) seq_end[rec] = q;
                     else err |= ERR_FQ_TOO_MANY;
-                    if (q + 1 >= n || base[q + 1] != '+') err |= ERR_FQ_NO_PLUS;
+                    if (q + 1 >= n || fq_next_byte(v, nxw, b, base, q) != '+') err |= ERR_FQ_NO_PLUS;
                     break;
                 case 3:
-                    if (q + 1 < n && base[q + 1] != '@') err |= ERR_FQ_NOT_AT;
+                    if (q + 1 < n && fq_next_byte(v, nxw, b, base, q) != '@') err |= ERR_FQ_NOT_AT;
                     break;
                 default: break;
                 }
                 j++;
             }
-            run += total;
         }
     }
     if (err) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)err);
@@ -3142,7 +3169,7 @@ __global__ __launch_bounds__(kBlock) void fq_validate_k(const u64* __restrict__ 
 
 hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hipStream_t s) {
     u64 nch = fq_chunks(base, n);
-    int g = (int)hmin(nch, 16384);
+    int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
     hipLaunchKernelGGL(fq_count_k, dim3(g ? g : 1), dim3(kBlock), 0, s, base, n, nch, counts);
     return hipGetLastError();
 }
@@ -3150,7 +3177,7 @@ hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hi
 hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t* seq_off,
                           uint64_t* seq_end, uint64_t max_rec, uint64_t* stats, hipStream_t s) {
     u64 nch = fq_chunks(base, n);
-    int g = (int)hmin(nch, 16384);
+    int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
     hipLaunchKernelGGL(fq_emit_k, dim3(g ? g : 1), dim3(kBlock), 0, s, base, n, nch, line_base, seq_off, seq_end,
                        max_rec, stats);
     return hipGetLastError();
