@@ -2474,17 +2474,17 @@ constexpr int kSegWaves = kSegBlock / 64;
 
 template <int W>
 struct SegCfg {
-    static constexpr int CAP = (W == 1) ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));  // >= bucket_lds_slots
+    static constexpr int CAP = (W == 1) ? 11840 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));  // >= bucket_lds_slots
     static constexpr int ITEMS = (CAP + kSegBlock - 1) / kSegBlock;
 };
 
 size_t seg_sort_msd_lds(int W) {
-    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));
-    return (size_t)cap * (8 * W + 2) + 4096 * 4 + 32 * 4 + 16;
+    int cap = W == 1 ? 11840 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));
+    return (size_t)cap * (8 * W + 4) + 4096 * 4 + 32 * 4 + 16;
 }
 
 size_t seg_sort_lds(int W) {
-    int cap = W == 1 ? 12288 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));
+    int cap = W == 1 ? 11840 : (W == 2 ? 6144 : (W == 3 ? 4480 : 3584));
     return (size_t)cap * (8 * W + 2) + (size_t)2 * kSegWaves * 256 * 4 + 512 * 4 + 2 * 4 * kSegWaves * 8 + 64;
 }
 
@@ -2525,9 +2525,9 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
                                                         u64* __restrict__ fb_n) {
     constexpr int CAP = SegCfg<W>::CAP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    u64* skey = (u64*)smem;                                            // W x CAP
-    unsigned short* sidx = (unsigned short*)(skey + (size_t)W * CAP);  // CAP
-    u32* bcnt = (u32*)(sidx + CAP);                                    // 4096 bins
+    u64* skey = (u64*)smem;                      // W x CAP
+    u32* scnt = (u32*)(skey + (size_t)W * CAP);  // CAP counts, moved with their keys
+    u32* bcnt = scnt + CAP;                      // 4096 bins
     u32* misc = bcnt + 4096;                                           // [0] skew flag, [1..16] wave sums
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     for (u64 di = blockIdx.x; di < ndesc; di += gridDim.x) {
@@ -2581,10 +2581,11 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             u64 k[W];
 #pragma unroll
             for (int j = 0; j < W; j++) k[j] = rkeys[(u64)j * rstride + st + p];
+            const u32 cv = rcnts[st + p];
             const u32 q = atomicAdd(&bcnt[(u32)(k[0] >> sh) & 4095u], 1u);
 #pragma unroll
             for (int j = 0; j < W; j++) skey[(size_t)j * CAP + q] = k[j];
-            sidx[q] = (unsigned short)p;
+            scnt[q] = cv;
         }
         __syncthreads();
         // insertion sort of this thread's 4 bins [bs, bs + sum)
@@ -2596,7 +2597,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
                 u64 kx[W];
 #pragma unroll
                 for (int jj = 0; jj < W; jj++) kx[jj] = skey[(size_t)jj * CAP + x];
-                const unsigned short ix = sidx[x];
+                const u32 ix = scnt[x];
                 u32 y = x;
                 while (y > s0) {
                     bool less = false, eq = true;
@@ -2611,12 +2612,12 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
                     if (!less) break;
 #pragma unroll
                     for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = skey[(size_t)jj * CAP + y - 1];
-                    sidx[y] = sidx[y - 1];
+                    scnt[y] = scnt[y - 1];
                     y--;
                 }
 #pragma unroll
                 for (int jj = 0; jj < W; jj++) skey[(size_t)jj * CAP + y] = kx[jj];
-                sidx[y] = ix;
+                scnt[y] = ix;
             }
             s0 = e0;
         }
@@ -2625,7 +2626,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             u64 kk[W];
 #pragma unroll
             for (int jj = 0; jj < W; jj++) kk[jj] = skey[(size_t)jj * CAP + p];
-            seg_put<W>(okeys, ocnts, ostride, packed, obase + p, kk, rcnts[st + sidx[p]]);
+            seg_put<W>(okeys, ocnts, ostride, packed, obase + p, kk, scnt[p]);
         }
         __syncthreads();
     }
