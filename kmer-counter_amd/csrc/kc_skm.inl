@@ -802,7 +802,10 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
                              const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,
                              uint8_t* emit, int eshift, int grid, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    const int g = (int)hmin(ntiles, (u64)grid);
+    // one persistent workgroup per CU (the LDS tile allows no second one): a
+    // larger grid would run as two rounds of workgroups, each restarting its
+    // prefetch pipeline
+    const int g = (int)hmin(ntiles, (u64)(grid / 2 > 0 ? grid / 2 : 1));
     const size_t lds = (rp_scatter_lds(NW, pay) + 15) & ~(size_t)15;
 #define KC_RPS(NWV, PAYV)                                                                                          \
     hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kP3Block), lds, s, kin, istride, kout, ostride, pin, \
