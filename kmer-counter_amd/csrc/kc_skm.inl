@@ -499,7 +499,9 @@ SkmGeom skm_geometry(int L, int k) {
     // m-mers: a window's minimizer lives ~(k - m + 1) windows; runs longer
     // than nmax are split, so aim k - m + 1 <= nmax (m in [11, 24])
     int m = k - g.nmax + 1;
-    if (m < 11) m = 11;
+    int mmin = 11;
+    if (const char* e = getenv("KC_SKM_MMIN")) mmin = atoi(e);  // tuning experiments
+    if (m < mmin) m = mmin;
     if (m > 24) m = 24;
     if (k - m + 1 < 8) m = k - 7;
     g.m = m;
