@@ -1012,7 +1012,7 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
 template <int W>
 __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     constexpr int RW = W + 1;
-    constexpr int PD = 4;  // record batches in flight
+    constexpr int PD = 2;  // record batches in flight
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* lkeys = (u64*)smem;                         // W x lcap
     u32* lcnt = (u32*)(lkeys + (size_t)W * a.lcap);  // lcap
