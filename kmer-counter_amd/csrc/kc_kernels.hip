@@ -2530,6 +2530,33 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
     u32* bcnt = scnt + CAP;                      // 4096 bins
     u32* misc = bcnt + 4096;                                           // [0] skew flag, [1..16] wave sums
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    // the segment's first PI items per thread (6144 / W records: every segment
+    // of a balanced input) are loaded into registers one segment ahead, so
+    // the counting and scatter passes do not wait on memory; longer
+    // segments read the rest in place
+    constexpr int ITEMS = SegCfg<W>::ITEMS;
+    constexpr int PI = ITEMS < 6 / W ? ITEMS : 6 / W;
+    u64 nk[PI][W];
+    u32 nc[PI];
+    auto load_seg = [&](u64 d) {
+        u64 s0 = 0;
+        u32 l0 = 0;
+        if (d < ndesc) {
+            const u32 od = order[d];
+            s0 = dstart[od];
+            l0 = dlen[od] & 0xffffffu;
+            if (l0 > (u32)CAP) l0 = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < PI; i++) {
+            const u32 p = (u32)tid + (u32)i * kSegBlock;
+            const bool ok = p < l0;
+#pragma unroll
+            for (int j = 0; j < W; j++) nk[i][j] = ok ? rkeys[(u64)j * rstride + s0 + p] : 0ull;
+            nc[i] = ok ? rcnts[s0 + p] : 0u;
+        }
+    };
+    load_seg(blockIdx.x);
     for (u64 di = blockIdx.x; di < ndesc; di += gridDim.x) {
         const u32 o = order[di];
         const u64 st = dstart[o];
@@ -2538,6 +2565,15 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         const int l2m = (int)(lw >> 24);
         const u64 obase = out_off[di];
         const int sh = 36 - l2m;  // digit = word0 bits [sh, sh + 12)
+        u64 ck[PI][W];
+        u32 cc[PI];
+#pragma unroll
+        for (int i = 0; i < PI; i++) {
+#pragma unroll
+            for (int j = 0; j < W; j++) ck[i][j] = nk[i][j];
+            cc[i] = nc[i];
+        }
+        load_seg(di + gridDim.x);
         for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
         if (tid == 0) misc[0] = 0;
         __syncthreads();
@@ -2546,7 +2582,11 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             __syncthreads();
             continue;
         }
-        for (u32 p = tid; p < len; p += kSegBlock) atomicAdd(&bcnt[(u32)(rkeys[st + p] >> sh) & 4095u], 1u);
+#pragma unroll
+        for (int i = 0; i < PI; i++)
+            if ((u32)tid + (u32)i * kSegBlock < len) atomicAdd(&bcnt[(u32)(ck[i][0] >> sh) & 4095u], 1u);
+        for (u32 p = tid + PI * kSegBlock; p < len; p += kSegBlock)
+            atomicAdd(&bcnt[(u32)(rkeys[st + p] >> sh) & 4095u], 1u);
         __syncthreads();
         // bin starts: 4 bins per thread, block-wide exclusive scan; skew check
         const u32 c0 = bcnt[4 * tid], c1 = bcnt[4 * tid + 1], c2 = bcnt[4 * tid + 2], c3 = bcnt[4 * tid + 3];
@@ -2577,15 +2617,22 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         bcnt[4 * tid + 3] = bs + c0 + c1 + c2;
         __syncthreads();
         // scatter into bins (bcnt becomes each bin's end)
-        for (u32 p = tid; p < len; p += kSegBlock) {
+#pragma unroll
+        for (int i = 0; i < PI; i++) {
+            if ((u32)tid + (u32)i * kSegBlock >= len) continue;
+            const u32 q = atomicAdd(&bcnt[(u32)(ck[i][0] >> sh) & 4095u], 1u);
+#pragma unroll
+            for (int j = 0; j < W; j++) skey[(size_t)j * CAP + q] = ck[i][j];
+            scnt[q] = cc[i];
+        }
+        for (u32 p = tid + PI * kSegBlock; p < len; p += kSegBlock) {
             u64 k[W];
 #pragma unroll
             for (int j = 0; j < W; j++) k[j] = rkeys[(u64)j * rstride + st + p];
-            const u32 cv = rcnts[st + p];
             const u32 q = atomicAdd(&bcnt[(u32)(k[0] >> sh) & 4095u], 1u);
 #pragma unroll
             for (int j = 0; j < W; j++) skey[(size_t)j * CAP + q] = k[j];
-            scnt[q] = cv;
+            scnt[q] = rcnts[st + p];
         }
         __syncthreads();
         // insertion sort of this thread's 4 bins [bs, bs + sum)
