@@ -1045,6 +1045,23 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;
     const u32 ng = a.lcap / kSkmGroup;
     const bool grouped = W == 1 && (a.lcap % kSkmGroup) == 0;
+    // the first PD batches of a pass are loaded while the previous pass ends
+    // (speculatively the next bucket's; a sub-range pass of the same bucket
+    // reloads): pfb is the bucket pf holds the pass-start batches of
+    u64 pf[PD][RW];
+    u32 pfb = ~0u;
+    auto prefetch_pass = [&](u32 bb) {
+        const u64 l0 = a.starts[bb], h0 = a.starts[bb + 1];
+        const u64 nr0 = h0 - l0, pw = (nr0 + kBucketWaves - 1) / kBucketWaves;
+        const u64 w0 = l0 + min(nr0, (u64)(tid >> 6) * pw), w1 = l0 + min(nr0, (u64)((tid >> 6) + 1) * pw);
+#pragma unroll
+        for (int d = 0; d < PD; d++) {
+            const u64 i = w0 + (u64)d * 64 + lane;
+#pragma unroll
+            for (int j = 0; j < RW; j++) pf[d][j] = i < w1 ? a.recs[(u64)j * a.stride + i] : 0ull;
+        }
+        pfb = bb;
+    };
     for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         if (tid == 0)
             *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
@@ -1075,13 +1092,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
             const u64 nrec_b = hi - lo;
             const u64 per_w = (nrec_b + kBucketWaves - 1) / kBucketWaves;
             const u64 wlo = lo + min(nrec_b, (u64)(tid >> 6) * per_w), whi = lo + min(nrec_b, (u64)((tid >> 6) + 1) * per_w);
-            u64 pf[PD][RW];
-#pragma unroll
-            for (int d = 0; d < PD; d++) {
-                const u64 i = wlo + (u64)d * 64 + lane;
-#pragma unroll
-                for (int j = 0; j < RW; j++) pf[d][j] = i < whi ? a.recs[(u64)j * a.stride + i] : 0ull;
-            }
+            if (pfb != b) prefetch_pass(b);
+            pfb = ~0u;
             for (u64 base = wlo; base < whi; base += 64) {
                 if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 scanned += 64;
@@ -1241,6 +1253,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 }
                 }
             }
+            // next bucket's first batches in flight during the drain, the abort
+            // check and the emission (unless another pass of this bucket follows)
+            if (sub + 1 >= m && b + gridDim.x < a.nbuckets) prefetch_pass(b + gridDim.x);
             if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 skm_drain<W>(a, tab, wq, qn, lo, last, limit);
             __syncthreads();
