@@ -556,7 +556,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
 // stable over level 1's regions, back into `a`. ms[0] += histogram + scan
 // time, ms[1] += scatter time (HIP events).
 static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, uint32_t* pa, uint64_t* b,
-                         uint64_t sb, uint32_t* pb, uint8_t* digs, uint64_t n, double* ms) {
+                         uint64_t sb, uint32_t* pb, uint8_t* digs, uint64_t n, double* ms,
+                         const uint8_t* dig1 = nullptr) {
     if (n == 0) return KC_OK;
     kc_status s;
     const uint64_t tile = (uint64_t)rp_tile(NW, pay);
@@ -576,7 +577,9 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
     h[3] = nt1;
     HIPCHK(c, hipMemcpyAsync(rt, h.data(), 4 * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_rp_hist(nullptr, a, 48, rt, rt + 2, 1, nt1, (uint32_t)tile, pos, tmp, grid, c->stream));
+    // first pass digit: the producer's byte per item when it wrote one, else word 0 bits 48..55
+    HIPCHK(c, launch_rp_hist(dig1, dig1 ? nullptr : a, 48, rt, rt + 2, 1, nt1, (uint32_t)tile, pos, tmp, grid,
+                             c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     HIPCHK(c, hipEventSynchronize(c->ev1));
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -664,7 +667,10 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
         c->part_ms[0] += t;
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_skm_front(l, g, c->keys_a, pool_cap, c->pool_cursor, 8 * c->n_cu, c->stream));
+        // digs: the second half takes F's first-pass digits, the first half the
+        // second pass's (written by the first pass)
+        uint8_t* dig1 = 2 * pool_cap <= c->key_cap ? c->digs + pool_cap : nullptr;
+        HIPCHK(c, launch_skm_front(l, g, c->keys_a, pool_cap, c->pool_cursor, 8 * c->n_cu, c->stream, dig1));
         HIPCHK(c, hipEventRecord(c->ev1, c->stream));
         uint64_t np = 0;
         HIPCHK(c, hipMemcpyAsync(&np, c->pool_cursor, 8, hipMemcpyDeviceToHost, c->stream));
@@ -692,7 +698,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         if (np > 0) {
             double gm[2] = {0, 0};
             if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, c->keys_b, pool_cap, nullptr, c->digs, np,
-                             gm)))
+                             gm, dig1)))
                 return s;
             c->part_ms[3] += gm[0];
             c->part_ms[2] += gm[1];

@@ -206,8 +206,10 @@ SkmGeom skm_geometry(int L, int k);
 // F: records (RW = W + 1 words, SoA at pool_cap) of the launch's reads; *pool_cursor
 // (zeroed by the caller) ends as the number of records handed out (padding
 // included); > pool_cap means the pool overflowed and nothing may be used.
+// dig1 (optional, pool_cap bytes): each record's low bucket byte, the first
+// grouping pass's digit (its histogram then reads a byte per record, not word 0)
 hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* pool, uint64_t pool_cap,
-                            uint64_t* pool_cursor, int grid_cap, hipStream_t s);
+                            uint64_t* pool_cursor, int grid_cap, hipStream_t s, uint8_t* dig1 = nullptr);
 // rp_*: radix grouping passes over NW-word SoA items (+ optional u32 payload)
 int rp_tile(int NW, bool pay);
 uint64_t* rp_digit_base(uint64_t* tmp, uint64_t ntiles);  // exclusive digit bases after launch_rp_hist

@@ -86,6 +86,7 @@ struct SkmArgs {
     u64* pool;         // RW x pool_cap u64 (SoA)
     u64 pool_cap;
     u64* pool_cursor;  // chunk allocator (records handed out)
+    unsigned char* dig1;  // optional: a record's low bucket byte (the first grouping pass's digit)
     u64* stats;
 };
 
@@ -470,6 +471,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
                 if (dst < a.pool_cap && !(a.skip & 1)) {
 #pragma unroll
                     for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + dst] = rec[j];
+                    if (a.dig1) a.dig1[dst] = (unsigned char)bkt;
                 }
             }
         }
@@ -481,6 +483,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
         if (i < a.pool_cap) {
 #pragma unroll
             for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + i] = j == 0 ? ((u64)kNoKey << 48) : 0ull;
+            if (a.dig1) a.dig1[i] = (unsigned char)kNoKey;
         }
     wave_add(&a.stats[ST_VALID], my_valid);
     if (__ballot(my_hole) && lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
@@ -527,7 +530,7 @@ SkmGeom skm_geometry(int L, int k) {
 }
 
 hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* pool, uint64_t pool_cap,
-                            uint64_t* pool_cursor, int grid_cap, hipStream_t s) {
+                            uint64_t* pool_cursor, int grid_cap, hipStream_t s, uint8_t* dig1) {
     if (l.n_reads == 0) return hipSuccess;
     if (!g.ok || !l.codes || !l.inval) return hipErrorInvalidValue;
     SkmArgs a;
@@ -546,6 +549,7 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
     a.pool = pool;
     a.pool_cap = pool_cap;
     a.pool_cursor = pool_cursor;
+    a.dig1 = dig1;
     a.stats = l.stats;
     a.hq = g.hq;
     a.chunk = (u64)g.R * (u64)(l.L - l.k + 1);
