@@ -67,7 +67,9 @@ struct kc_ctx {
     uint64_t* pool_cursor = nullptr;  // device u64: skm pool allocator
     uint64_t key_cap = 0;          // keys per batch
     uint64_t* keys_a = nullptr;    // W x key_cap
-    uint8_t* digs = nullptr;       // key_cap: P3 digit (word0 >> 56) of keys_a[i], written by P2
+    uint8_t* digs = nullptr;       // digs_bytes: P3 digit (word0 >> 56) of keys_a[i], written by P2; the skm
+                                   // engine keeps two digit bytes per record (both grouping passes)
+    uint64_t digs_bytes = 0;
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
@@ -667,9 +669,11 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
         c->part_ms[0] += t;
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        // digs: the second half takes F's first-pass digits, the first half the
-        // second pass's (written by the first pass)
-        uint8_t* dig1 = 2 * pool_cap <= c->key_cap ? c->digs + pool_cap : nullptr;
+        // digs: the second array (16-byte aligned, for the histogram's 16-byte
+        // loads) takes F's first-pass digits, the first the second pass's
+        // (written by the first pass)
+        const uint64_t dig1_off = (pool_cap + 15) & ~15ull;
+        uint8_t* dig1 = dig1_off + pool_cap <= c->digs_bytes ? c->digs + dig1_off : nullptr;
         HIPCHK(c, launch_skm_front(l, g, c->keys_a, pool_cap, c->pool_cursor, 8 * c->n_cu, c->stream, dig1));
         HIPCHK(c, hipEventRecord(c->ev1, c->stream));
         uint64_t np = 0;
@@ -964,7 +968,13 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     if (c->part) {
         if (hipMalloc((void**)&c->keys_a, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->keys_b, (size_t)c->key_cap * 8 * c->W) != hipSuccess) return bail(KC_ERR_NOMEM);
-        if (hipMalloc((void**)&c->digs, (size_t)c->key_cap + 16) != hipSuccess) return bail(KC_ERR_NOMEM);
+        // key_cap digit bytes for the partition engine; the skm engine's two digit
+        // arrays (2 x pool_cap, pool_cap = W key_cap / (W + 1)) with the second one
+        // 16-byte aligned
+        c->digs_bytes = c->key_cap;
+        const uint64_t pool_max = (uint64_t)c->W * c->key_cap / (c->W + 1);
+        if (((pool_max + 15) & ~15ull) + pool_max > c->digs_bytes) c->digs_bytes = ((pool_max + 15) & ~15ull) + pool_max;
+        if (hipMalloc((void**)&c->digs, (size_t)c->digs_bytes + 16) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->rec_cursor, 8) != hipSuccess) return bail(KC_ERR_NOMEM);
         if (hipMalloc((void**)&c->pool_cursor, 8) != hipSuccess) return bail(KC_ERR_NOMEM);
         hipDeviceProp_t prop;

@@ -635,7 +635,8 @@ __global__ __launch_bounds__(kBlock) void rp_upsweep_k(const unsigned char* __re
         rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
         u32* hw = h + wave * 256;
         if (digs) {
-            const u64 alo = min(hi, (lo + 15) & ~15ull);
+            // 16-byte loads from the first 16-byte aligned address on
+            const u64 alo = min(hi, lo + ((16u - (u32)((uintptr_t)(digs + lo) & 15u)) & 15u));
             for (u64 i = lo + tid; i < alo; i += kBlock) atomicAdd(&hw[digs[i]], 1u);
             const u64 ahi = alo + ((hi - alo) & ~15ull);
             for (u64 i = alo + 16 * (u64)tid; i < ahi; i += 16 * (u64)kBlock) {
