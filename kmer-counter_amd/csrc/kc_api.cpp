@@ -374,8 +374,10 @@ static const double kSkmDistinctMax = 0.35;
 //               word0 >> 48, the key's first 8 bases: buckets are in key order
 //   P4        : bucket ranges (binary search)
 //   P5        : per-bucket LDS hash count -> (key, count) records
+// pre0 >= 0: the reads are already encoded (fq_encode) in part_codes /
+// part_inval from read index pre0 on; kernel E is skipped
 static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
-                                  int64_t L) {
+                                  int64_t L, int64_t pre0) {
     if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     const int W = c->W;
     const uint64_t nw = (uint64_t)(L - c->k + 1);
@@ -405,12 +407,16 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         if ((s = ensure(c, c->part_hist, hn * 8)) || (s = ensure(c, c->part_base, hn * 8)) ||
             (s = ensure(c, c->part_tmp, scan_tmp_elems(hn) * 8)))
             return s;
-        const uint64_t ng = nr * (uint64_t)groups_per_read((int)L);
-        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
-        l.codes = (const uint32_t*)c->part_codes.p;
-        l.inval = (const uint16_t*)c->part_inval.p;
+        const uint64_t G = (uint64_t)groups_per_read((int)L);
+        const uint64_t ng = nr * G;
+        if (pre0 < 0 && ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))))
+            return s;
+        const uint64_t g0 = pre0 < 0 ? 0 : ((uint64_t)pre0 + done) * G;
+        l.codes = (const uint32_t*)c->part_codes.p + g0;
+        l.inval = (const uint16_t*)c->part_inval.p + g0;
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
+        if (pre0 < 0)
+            HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
         HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 48, c->stream));
         HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn, (uint64_t*)c->part_tmp.p,
                                   c->stream));
@@ -623,7 +629,7 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
 // part_ms slots for this engine: [0] E + F, [1] F, [2] S1/S2 scatters,
 // [3] S1/S2 histograms + scans + P4, [4] P5.
 static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
-                                 int64_t L, const SkmGeom& g) {
+                                 int64_t L, const SkmGeom& g, int64_t pre0) {
     if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     const int W = c->W;
     const int RW = W + 1;
@@ -655,15 +661,19 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         l.spill_cap = c->spill_cap;
         l.stats = c->stats;
         l.probe_limit = probe_limit(c);
-        const uint64_t ng = nr * (uint64_t)groups_per_read((int)L);
-        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
-        l.codes = (const uint32_t*)c->part_codes.p;
-        l.inval = (const uint16_t*)c->part_inval.p;
+        const uint64_t G = (uint64_t)groups_per_read((int)L);
+        const uint64_t ng = nr * G;
+        if (pre0 < 0 && ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))))
+            return s;
+        const uint64_t g0 = pre0 < 0 ? 0 : ((uint64_t)pre0 + done) * G;
+        l.codes = (const uint32_t*)c->part_codes.p + g0;
+        l.inval = (const uint16_t*)c->part_inval.p + g0;
         if ((s = sync_stats(c))) return s;
         std::vector<uint64_t> saved(c->stats_h, c->stats_h + ST_N);
         HIPCHK(c, hipMemsetAsync(c->pool_cursor, 0, 8, c->stream));
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
+        if (pre0 < 0)
+            HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
         HIPCHK(c, hipEventRecord(c->ev1, c->stream));
         HIPCHK(c, hipEventSynchronize(c->ev1));
         HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -797,7 +807,8 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                         fprintf(stderr, "kc: skm sample %llu distinct / %llu keys: key-prefix engine\n",
                                 (unsigned long long)dist_s, (unsigned long long)keys_s);
                     return count_reads_part(c, seq_off ? base : base + done * (uint64_t)L,
-                                            seq_off ? seq_off + done : nullptr, n_reads - done, L);
+                                            seq_off ? seq_off + done : nullptr, n_reads - done, L,
+                                            pre0 < 0 ? -1 : pre0 + (int64_t)done);
                 }
             }
             if ((s = p5_range(bs, nbk, false))) return s;
@@ -824,19 +835,34 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
     return KC_OK;
 }
 
-static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L) {
+// The engine count_reads takes for L reads (same order of tests): the skm and
+// key-prefix engines read 2-bit codes, the table engine the text
+static bool engine_reads_codes(const kc_ctx* c, int64_t L) {
+    if (c->skm && !c->skm_hc && skm_geometry((int)L, (int)c->k).ok) return true;
+    return c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= kMaxLds;
+}
+
+// pre0 >= 0: the reads are pre-encoded in part_codes / part_inval from read pre0
+static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L,
+                             int64_t pre0 = -1) {
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
     if (c->skm && !c->skm_hc) {
         const SkmGeom g = skm_geometry((int)L, (int)c->k);
-        if (g.ok) return count_reads_skm(c, base, seq_off, n_reads, L, g);
+        if (g.ok) return count_reads_skm(c, base, seq_off, n_reads, L, g, pre0);
     }
     if (c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= kMaxLds)
-        return count_reads_part(c, base, seq_off, n_reads, L);
+        return count_reads_part(c, base, seq_off, n_reads, L, pre0);
+    if (pre0 >= 0) return fail(c, KC_ERR_INTERNAL, "pre-encoded reads reached the table engine");
     return count_reads_table(c, base, seq_off, n_reads, L);
 }
 
-static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out) {
+// K1. With `encoded` (counting), when the engine reads codes and the block is
+// one batch, the emit pass also encodes every read (fq_encode: the text is read
+// twice instead of three times) and *encoded is set; seq_off is then unset.
+static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out,
+                             bool* encoded = nullptr) {
+    if (encoded) *encoded = false;
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
     if ((s = ensure(c, c->fq_counts, nch * 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
@@ -855,11 +881,21 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
     if (lines % 4 != 0)
         return fail(c, KC_ERR_FORMAT, "FASTQ block has %llu lines, not a multiple of 4", (unsigned long long)lines);
     uint64_t n_rec = lines / 4;
-    if ((s = ensure(c, c->seq_off, n_rec * 8 + 8)) || (s = ensure(c, c->seq_end, n_rec * 8 + 8))) return s;
-    HIPCHK(c, launch_fq_emit(base, n, (uint64_t*)c->fq_base.p, (uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p,
-                             n_rec, c->stats, c->stream));
-    HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
-                                 c->stream));
+    const uint64_t nw = (uint64_t)(L - c->k + 1);
+    const bool fuse = encoded && !getenv("KC_NO_FQ_ENCODE") && L >= c->k && engine_reads_codes(c, L) &&
+                      n_rec * nw <= c->key_cap;
+    if (fuse) {
+        const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
+        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
+        HIPCHK(c, launch_fq_encode(base, n, (uint64_t*)c->fq_base.p, n_rec, (int)L, (uint32_t*)c->part_codes.p,
+                                   (uint16_t*)c->part_inval.p, c->stats, c->stream));
+    } else {
+        if ((s = ensure(c, c->seq_off, n_rec * 8 + 8)) || (s = ensure(c, c->seq_end, n_rec * 8 + 8))) return s;
+        HIPCHK(c, launch_fq_emit(base, n, (uint64_t*)c->fq_base.p, (uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p,
+                                 n_rec, c->stats, c->stream));
+        HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
+                                     c->stream));
+    }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     if ((s = sync_stats(c))) return s;
     float t = 0.f;
@@ -879,6 +915,7 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
                     why.c_str());
     }
     *n_rec_out = n_rec;
+    if (encoded) *encoded = fuse;
     return KC_OK;
 }
 
@@ -1092,8 +1129,11 @@ static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_
     if (s) return s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     uint64_t n_rec = 0;
-    if ((s = index_fastq(c, (const uint8_t*)d_fastq, n, L, &n_rec))) return s;
-    if (count && (s = count_reads(c, (const uint8_t*)d_fastq, (const uint64_t*)c->seq_off.p, n_rec, L))) return s;
+    bool enc = false;
+    if ((s = index_fastq(c, (const uint8_t*)d_fastq, n, L, &n_rec, count ? &enc : nullptr))) return s;
+    if (count && (s = count_reads(c, (const uint8_t*)d_fastq, enc ? nullptr : (const uint64_t*)c->seq_off.p, n_rec, L,
+                                  enc ? 0 : -1)))
+        return s;
     if (n_reads) *n_reads = n_rec;
     return KC_OK;
 }

@@ -191,6 +191,11 @@ hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_
                           uint64_t* seq_end, uint64_t max_rec, uint64_t* stats, hipStream_t s);
 hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, uint64_t n_rec, int L,
                               uint64_t* stats, hipStream_t s);
+// K1 emit + E in one pass (after fq_count + scan): codes / inval of every read
+// of the block (groups_per_read(L) each, read r at r * G), the same format
+// checks as fq_emit + fq_validate; seq_off / seq_end are not written.
+hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
+                            uint32_t* codes, uint16_t* inval, uint64_t* stats, hipStream_t s);
 
 // ---- super-k-mer engine (kc_skm.inl) ----
 struct SkmGeom {

@@ -3215,6 +3215,248 @@ __global__ __launch_bounds__(kBlock) void fq_validate_k(const u64* __restrict__ 
         atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_FQ_SEQ_LEN);
 }
 
+// K1 emit + E fused (engines that read codes, when the block is one batch):
+// fq_emit_k's newline walk and encode_reads_k's encoding with one read of the
+// text. Every wave takes its chunk in two halves of 8 KiB. A half and the next
+// KiB are staged in the wave's LDS. The half is walked in two rounds of 64
+// bytes per lane (one 64-bit newline mask per lane; the lanes' newline counts
+// are scanned by ballots of their bits); every newline gets its line index
+// from the chunk's line base, the '+' / '@' checks read the staged bytes, and
+// the records whose header ends in the half are listed (sequence start per
+// record). Then the wave encodes those reads, one (read, 16-base group) per
+// lane, from LDS (groups past the staged bytes from global memory) into codes /
+// inval at the read's index. The sequence-length check of fq_validate_k is
+// done inline: no newline inside [s, s + L) and a newline at s + L, which is
+// exactly seq_end - seq_off == L. Nothing is written to seq_off / seq_end.
+constexpr int kFqHalf = 8192;
+constexpr int kFqStage = kFqHalf + 1024;
+
+int fq_encode_list_cap(int L) { return kFqHalf / (L + 6) + 2; }  // records with an L-base sequence are >= L + 6 bytes
+
+static size_t fq_encode_wave_lds(int L) {
+    return (size_t)kFqStage + (((size_t)fq_encode_list_cap(L) * 2 + 15) & ~(size_t)15);
+}
+
+// bit b set when byte b of w is '\n'
+__device__ __forceinline__ u32 nl_nib(u32 w) {
+    const u32 t = w ^ 0x0a0a0a0au;
+    const u32 z = ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | (z >> 28);
+}
+
+// newline bytes among the first nv bytes of a dword (any)
+__device__ __forceinline__ bool has_nl(u32 x, int nv) {
+    if (nv <= 0) return false;
+    const u32 t = x ^ 0x0a0a0a0au;
+    const u32 z = ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
+    const u32 vm = nv >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - nv)));
+    return (z & vm) != 0u;
+}
+
+// bytes_to_codes by SWAR: 4 bytes -> 4 2-bit codes in the low byte (first
+// byte highest; ((c >> 1) ^ (c >> 2)) & 3 is A0 C1 G2 T3) and the 4-bit
+// not-ACGT mask (a byte is ACGT iff it equals the ACGT byte of its code,
+// looked up by v_perm); non-ACGT bytes code 3, bytes >= nv code 0 and valid
+__device__ __forceinline__ u32 swar_codes(u32 x, int nv, u32* bad4) {
+    const u32 vm = nv >= 4 ? ~0u : (nv <= 0 ? 0u : (~0u >> (8 * (4 - nv))));
+    u32 t = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+    const u32 y = __builtin_amdgcn_perm(0u, 0x54474341u, t) ^ x;
+    const u32 bad = (((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u & vm;
+    t = (t & vm) | (bad >> 7) | (bad >> 6);
+    *bad4 = ((bad >> 4) & 8u) | ((bad >> 13) & 4u) | ((bad >> 22) & 2u) | (bad >> 31);
+    return ((t << 6) | (t >> 4) | (t >> 14) | (t >> 24)) & 255u;
+}
+
+__global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
+                                                      const u64* __restrict__ line_base, u64 max_rec, int L, int G,
+                                                      int lcap, u32* __restrict__ codes,
+                                                      unsigned short* __restrict__ inval, u64* stats) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const u64 lt = lanemask_lt();
+    const size_t wbytes = (size_t)kFqStage + (((size_t)lcap * 2 + 15) & ~(size_t)15);
+    unsigned char* txt = smem + (size_t)wave * wbytes;
+    unsigned short* lst = (unsigned short*)(txt + kFqStage);
+    const FastDivU divg((u32)G);
+    u64 err = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (n == 0 || base[0] != '@') err |= ERR_FQ_NOT_AT;
+        if (n > 0 && base[n - 1] != '\n') err |= ERR_FQ_NO_FINAL_NL;
+    }
+    auto sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    };
+    for (u64 c = (u64)blockIdx.x * kFqWaves + wave; c < nchunks; c += (u64)gridDim.x * kFqWaves) {
+        u64 run = line_base[c];
+        for (int h = 0; h < 2; h++) {
+            const uintptr_t hb = A + c * kFqChunk + (u64)h * kFqHalf;
+            const long long hrel = (long long)(hb - (uintptr_t)base);
+            if (hrel >= (long long)n) break;
+            // rounds 0, 1: lane l holds bytes [4096 rd + 64 l, + 64); x: the next KiB
+            uint4 v[2][4], x;
+#pragma unroll
+            for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int o = rd * 4096 + lane * 64 + i * 16;
+                    const long long rel = hrel + o;
+                    v[rd][i] = (rel + 16 <= 0 || rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+                }
+            {
+                const int o = kFqHalf + lane * 16;
+                const long long rel = hrel + o;
+                x = (rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+            }
+#pragma unroll
+            for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    v4u w;
+                    w.x = v[rd][i].x;
+                    w.y = v[rd][i].y;
+                    w.z = v[rd][i].z;
+                    w.w = v[rd][i].w;
+                    *(v4u*)(txt + rd * 4096 + lane * 64 + i * 16) = w;
+                }
+            {
+                v4u w;
+                w.x = x.x;
+                w.y = x.y;
+                w.z = x.z;
+                w.w = x.w;
+                *(v4u*)(txt + kFqHalf + lane * 16) = w;
+            }
+            sync();
+            const u64 rec0 = (run + 3) >> 2;  // first record whose header may end in this half
+#pragma unroll
+            for (int rd = 0; rd < 2; rd++) {
+                u64 m = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const u32 q4 = nl_nib(v[rd][i].x) | (nl_nib(v[rd][i].y) << 4) | (nl_nib(v[rd][i].z) << 8) |
+                                   (nl_nib(v[rd][i].w) << 12);
+                    m |= (u64)q4 << (16 * i);
+                }
+                const long long rel0 = hrel + rd * 4096 + lane * 64;
+                if (rel0 < 0) m = (rel0 <= -64) ? 0ull : (m & (~0ull << (u32)(-rel0)));
+                if (rel0 + 64 > (long long)n) m = (rel0 >= (long long)n) ? 0ull : (m & (~0ull >> (u32)(rel0 + 64 - (long long)n)));
+                const u32 cnt = (u32)__popcll(m);
+                u32 ex = 0, tot = 0;
+                if (__ballot(cnt > 7u) == 0ull) {
+                    // counts below 8: the prefix from three bit-plane ballots
+#pragma unroll
+                    for (int bp = 0; bp < 3; bp++) {
+                        const u64 bl = __ballot((cnt >> bp) & 1u);
+                        ex += (u32)__popcll(bl & lt) << bp;
+                        tot += (u32)__popcll(bl) << bp;
+                    }
+                } else {
+                    u32 inc = cnt;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const u32 y = __shfl_up(inc, o);
+                        if (lane >= o) inc += y;
+                    }
+                    ex = inc - cnt;
+                    tot = (u32)__shfl((int)inc, 63);
+                }
+                u64 j = run + ex;
+                run += tot;
+                while (m) {
+                    const int b = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    const int o = rd * 4096 + lane * 64 + b;  // staged position of the newline
+                    const u64 q = (u64)(hrel + o);
+                    const u32 jc = (u32)j & 3u;
+                    if (jc == 0u) {
+                        const u64 li = (j >> 2) - rec0;
+                        if ((j >> 2) >= max_rec) err |= ERR_FQ_TOO_MANY;
+                        else if (li < (u64)lcap) lst[li] = (unsigned short)(o + 1);
+                        else err |= ERR_FQ_SEQ_LEN;  // more records than L-base sequences allow
+                    } else if (jc != 2u) {
+                        // after the sequence: '+'; after the quality line: '@' (or the block end)
+                        const u32 nx = q + 1 < n ? (u32)txt[o + 1] : 0u;
+                        if (jc == 1u ? nx != (u32)'+' : (q + 1 < n && nx != (u32)'@'))
+                            err |= jc == 1u ? ERR_FQ_NO_PLUS : ERR_FQ_NOT_AT;
+                    }
+                    j++;
+                }
+            }
+            sync();
+            // records [rec0, rec1) have their header newline in this half
+            u64 rec1 = (run + 3) >> 2;
+            if (rec1 > max_rec) rec1 = max_rec;
+            const u32 nrec = rec1 > rec0 ? (u32)min(rec1 - rec0, (u64)lcap) : 0u;
+            for (u32 item = (u32)lane; item < nrec * (u32)G; item += 64) {
+                const u32 r = divg.div(item);
+                const int g = (int)(item - r * (u32)G);
+                const int s0 = (int)lst[r] + 16 * g;  // staged offset of the group's first base
+                const int nb = min(16, L - 16 * g);
+                const bool lastg = g == G - 1;
+                const int need = nb + (lastg ? 1 : 0);  // the group (+ the byte after the read)
+                const int sh = s0 & 3;
+                u32 d[5];
+                if ((s0 & ~3) + 20 <= kFqStage) {
+                    const u32* lw = (const u32*)(txt + (s0 & ~3));
+#pragma unroll
+                    for (int i = 0; i < 5; i++) d[i] = lw[i];
+                } else {
+                    // past the staged bytes: global dwords holding a byte of [s0, s0 + need) below n
+                    const long long gq = hrel + s0;
+                    typedef __attribute__((address_space(1))) const u32 g32;
+                    const g32* dw = (const g32*)((uintptr_t)(base + gq) & ~(uintptr_t)3);
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        const long long first = gq - sh + 4 * i;  // block offset of dword i
+                        d[i] = (4 * i < sh + need && first < (long long)n) ? dw[i] : 0u;
+                    }
+                }
+                const u32 x0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+                const u32 x1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+                const u32 x2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+                const u32 x3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+                u32 b0, b1, b2, b3;
+                const u32 c0 = swar_codes(x0, nb, &b0);
+                const u32 c1 = swar_codes(x1, nb - 4, &b1);
+                const u32 c2 = swar_codes(x2, nb - 8, &b2);
+                const u32 c3 = swar_codes(x3, nb - 12, &b3);
+                const u32 bad = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
+                // a newline is a non-ACGT byte: the exact test only for such groups
+                bool wrong = bad != 0u &&
+                             (has_nl(x0, nb) || has_nl(x1, nb - 4) || has_nl(x2, nb - 8) || has_nl(x3, nb - 12));
+                if (lastg) {
+                    const int e = sh + nb;  // the byte after the read, in d
+                    const u32 nxt = (d[e >> 2] >> (8 * (e & 3))) & 255u;
+                    wrong = wrong || nxt != (u32)'\n' || hrel + s0 + nb >= (long long)n;
+                }
+                if (wrong) err |= ERR_FQ_SEQ_LEN;
+                const u64 at = (rec0 + r) * (u64)G + (u64)g;
+                codes[at] = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+                inval[at] = (unsigned short)bad;
+            }
+            sync();
+        }
+    }
+    if (err) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)err);
+}
+
+hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
+                            uint32_t* codes, uint16_t* inval, uint64_t* stats, hipStream_t s) {
+    if (L < 1 || L > 32767) return hipErrorInvalidValue;
+    u64 nch = fq_chunks(base, n);
+    const int G = groups_per_read(L);
+    const int lcap = fq_encode_list_cap(L);
+    if ((u64)lcap * (u64)G >= 65536) return hipErrorInvalidValue;  // FastDivU range
+    const size_t lds = (size_t)kFqWaves * fq_encode_wave_lds(L);
+    int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
+    hipLaunchKernelGGL(fq_encode_k, dim3(g ? g : 1), dim3(kBlock), lds, s, base, n, nch, line_base, max_rec, L, G,
+                       lcap, codes, (unsigned short*)inval, stats);
+    return hipGetLastError();
+}
+
 hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hipStream_t s) {
     u64 nch = fq_chunks(base, n);
     int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
