@@ -19,7 +19,9 @@ import subprocess
 from typing import List, Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkc_hip.so")
+# KC_LIB: tuning experiments only (tools/build_variant.sh builds variants of
+# the same sources under kmer-counter_amd/variants/)
+LIB_PATH = os.environ.get("KC_LIB") or os.path.join(_HERE, "libkc_hip.so")
 CLI_PATH = os.path.join(_HERE, "kmer-counter")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kc.h")
 

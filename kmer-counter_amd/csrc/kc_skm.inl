@@ -165,7 +165,10 @@ constexpr u32 kNoKey = 0xffffu;  // window bucket of a window without a key (dea
 //      of the wave's current pool chunk (one global atomic per chunk); the
 //      chunk tail is padded with n = 0 records at exit
 template <int W>
-__global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void skm_front_k(SkmArgs a) {
+#ifndef KC_F_WPE
+#define KC_F_WPE 5  // F: waves per SIMD the register budget is cut for
+#endif
+__global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_WPE, 8))) void skm_front_k(SkmArgs a) {
     constexpr int RW = W + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int L = a.L, k = a.k, m = a.m, NG = a.NG, HS = a.HS, R = a.R, Kp = a.Kp, G = a.G;
@@ -489,6 +492,427 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(5, 8)
     if (__ballot(my_hole) && lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
 }
 
+// ---------------------------------------------------------------------------
+// F2: skm_front2_k<W, K>, F for a compile-time k whose minimizer length is 11
+// (every k of W = 1; skm_geometry picks m = 11 there). Same records, buckets
+// and statistics as skm_front_k; what changes is the instruction count:
+//   - k, K', nmax, m and the window span are constants: the m-mers of a hash
+//     item (16 positions of one code-word pair) are extracted with immediate
+//     shifts, written two per LDS store at immediate offsets, and a chunk's
+//     k - m + 8 hashes are read at immediate offsets into registers
+//   - the chunk's eight buckets stay in registers; the neighbouring chunks'
+//     first / last bucket come from the neighbouring lanes (wave shuffles)
+//   - the tile's start / end counts are scanned by ballots of their bits
+//     (counts <= 8), and the ends' positions follow from the starts' (a run
+//     open across a chunk boundary is the only difference)
+//   - every lane's roles (prefetch item, hash item, chunk) are fixed for the
+//     kernel (divisions once), record words are assembled branch-free
+// Requirements (launch_skm_front checks them): ceil((L - k + 1) / 8) <= 64.
+// ---------------------------------------------------------------------------
+
+template <int W, int K>
+struct F2Cfg {
+    static constexpr int RW = W + 1;
+    static constexpr bool MASK = ((K + 3) / 4) < 8 * W;
+    static constexpr int KP = MASK ? K : 32 * W;
+    static constexpr int NMAX0 = 32 * RW - 10 - KP;
+    static constexpr int NMAX = NMAX0 > 63 ? 63 : NMAX0;
+    static constexpr int M = 11;
+    static constexpr int WM = K - M + 1;  // m-mers per window
+    static constexpr u64 LAST_MASK = MASK ? (~0ull << (64 - 2 * (K & 31))) : ~0ull;
+    static_assert(WM >= 8, "a window spans at least 8 m-mers");
+};
+
+struct F2Args {
+    const u32* codes;             // kernel E output, G u32 per read
+    const unsigned short* inval;  //   not-ACGT masks, G u16 per read
+    u64 n_reads, ntiles;
+    int G, nw, nchr, R, NG, NI, HSK;
+    u32 o_inval, o_hm, o_rflag, o_sa, o_ea, wbytes;  // a wave's LDS region (bytes)
+    u64 chunk;  // pool records per wave allocation (>= records of one tile)
+    u64* pool;
+    u64 pool_cap;
+    u64* pool_cursor;
+    unsigned char* dig1;
+    u64* stats;
+};
+
+constexpr int kF2Pf = 2;  // F2: code words prefetched per lane
+
+// 22-bit m-mer (m = 11) at base i of the 32 bases {c0, c1} (MSB first)
+template <int I>
+__device__ __forceinline__ u32 f2_mmer(u32 c0, u32 c1) {
+    if constexpr (I <= 5)
+        return (c0 >> (10 - 2 * I)) & 0x3fffffu;
+    else
+        return __builtin_amdgcn_alignbit(c0, c1, 42 - 2 * I) & 0x3fffffu;
+}
+
+template <int I>
+__device__ __forceinline__ void f2_hash_pair(u32* hp, u32 c0, u32 c1) {
+    // hp[sk(i)]: positions 2j, 2j + 1 of an 8-group are adjacent words
+    const u32 h0 = mul_u24(f2_mmer<I>(c0, c1) ^ 0xd1e995u, 0x9e3779u);
+    const u32 h1 = mul_u24(f2_mmer<I + 1>(c0, c1) ^ 0xd1e995u, 0x9e3779u);
+    hp[I + (I >> 3)] = h0;
+    hp[I + 1 + (I >> 3)] = h1;
+}
+
+// 64 bits from base b of a code row (MSB first), branch-free
+__device__ __forceinline__ u64 f2_code_word(const u32* cr, int b) {
+    const int g = b >> 4, o = b & 15;
+    const u32 c0 = cr[g], c1 = cr[g + 1], c2 = cr[g + 2];
+    const u32 hi = o ? __builtin_amdgcn_alignbit(c0, c1, 32 - 2 * o) : c0;
+    const u32 lo = o ? __builtin_amdgcn_alignbit(c1, c2, 32 - 2 * o) : c1;
+    return ((u64)hi << 32) | lo;
+}
+
+// exclusive prefix over the wave of v < 16 (4 bit-plane ballots); *tot = sum
+__device__ __forceinline__ u32 f2_scan16(u32 v, u32* tot) {
+    const u64 lt = lanemask_lt();
+    u32 ex = 0, t = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const u64 bl = __ballot((v >> b) & 1u);
+        ex += (u32)__popcll(bl & lt) << b;
+        t += (u32)__popcll(bl) << b;
+    }
+    *tot = t;
+    return ex;
+}
+
+template <int W, int K>
+__global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_WPE, 8))) void skm_front2_k(F2Args a) {
+    using C = F2Cfg<W, K>;
+    constexpr int RW = C::RW;
+    constexpr int WM = C::WM;
+    constexpr u32 NMAX = (u32)C::NMAX;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6, lane = lane_id();
+    unsigned char* wb = smem + (size_t)wave * a.wbytes;
+    u32* codes = (u32*)wb;
+    u32* inval = (u32*)(wb + a.o_inval);
+    u32* hm = (u32*)(wb + a.o_hm);
+    u32* rflag = (u32*)(wb + a.o_rflag);
+    u32* sa = (u32*)(wb + a.o_sa);
+    unsigned short* ea = (unsigned short*)(wb + a.o_ea);
+    const int G = a.G, NG = a.NG, R = a.R, nw = a.nw, nchr = a.nchr, NI = a.NI, HSK = a.HSK;
+    const int RG = R * G;
+    const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
+    const u64 nwaves = (u64)gridDim.x * (kSkmBlock / 64);
+    for (int it = lane; it < R * NG; it += 64) {
+        codes[it] = 0;
+        inval[it] = 0;
+    }
+    // fixed roles of this lane
+    const FastDivU div_g((u32)G), div_ni((u32)NI), div_nw((u32)nw);
+    int pr[kF2Pf], pg[kF2Pf];
+#pragma unroll
+    for (int j = 0; j < kF2Pf; j++) {
+        const int it = lane + 64 * j;
+        pr[j] = (int)div_g.div((u32)it);
+        pg[j] = it - pr[j] * G;
+    }
+    const int hr0 = (int)div_ni.div((u32)lane), hq0 = lane - hr0 * NI;  // first hash item
+    const int cr_ = lane / nchr, cc = lane - (lane / nchr) * nchr;     // chunk: read, chunk of the read
+    const int p0 = 8 * cc;
+    u32 pfc[kF2Pf], pfi[kF2Pf];
+    auto prefetch = [&](u64 tile) {
+        const u64 r0 = tile * (u64)R;
+        const int nr = tile < a.ntiles ? (int)min((u64)R, a.n_reads - r0) : 0;
+        const u64 base = tile * (u64)RG;
+#pragma unroll
+        for (int j = 0; j < kF2Pf; j++) {
+            u32 cw = 0, iv = 0;
+            if (pr[j] < nr) {
+                cw = __builtin_nontemporal_load(a.codes + base + (u64)(lane + 64 * j));
+                iv = __builtin_nontemporal_load(a.inval + base + (u64)(lane + 64 * j));
+            }
+            pfc[j] = cw;
+            pfi[j] = iv;
+        }
+    };
+    auto flag_of = [&](u32 cw, u32 iv, int g) -> u32 {
+        // non-ACGT bases; aligned all-A halves of the read's groups (padding
+        // past L counts): only such reads can hold a key 0^W
+        const bool za = g < G && ((cw & 0xffffu) == 0u || (cw >> 16) == 0u);
+        return (iv ? 1u : 0u) | (za ? 2u : 0u);
+    };
+    prefetch(wid);
+    u64 my_valid = 0;
+    bool my_hole = false;
+    u64 ccur = 0, cend = 0;  // the wave's pool chunk (wave-uniform)
+    wave_sync();
+    for (u64 tile = wid; tile < a.ntiles; tile += nwaves) {
+        const u64 r0 = tile * (u64)R;
+        const int nr = (int)min((u64)R, a.n_reads - r0);
+        // 1. code words, masks and read flags into LDS
+        if (lane < nr) rflag[lane] = 0;
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < kF2Pf; j++)
+            if (pr[j] < nr) {
+                codes[pr[j] * NG + pg[j]] = pfc[j];
+                inval[pr[j] * NG + pg[j]] = pfi[j];
+                const u32 f = flag_of(pfc[j], pfi[j], pg[j]);
+                if (f) atomicOr(&rflag[pr[j]], f);
+            }
+        for (int it = lane + kF2Pf * 64; it < nr * G; it += 64) {
+            const int r = (int)div_g.div((u32)it), g = it - r * G;
+            const u64 idx = tile * (u64)RG + (u64)it;
+            const u32 cw = a.codes[idx], iv = a.inval[idx];
+            codes[r * NG + g] = cw;
+            inval[r * NG + g] = iv;
+            const u32 f = flag_of(cw, iv, g);
+            if (f) atomicOr(&rflag[r], f);
+        }
+        wave_sync();
+        prefetch(tile + nwaves);
+        // 2. m-mer hashes, 16 positions per item
+        for (int it2 = lane; it2 < nr * NI; it2 += 64) {
+            int hr = hr0, hq = hq0;
+            if (it2 != lane) {
+                hr = (int)div_ni.div((u32)it2);
+                hq = it2 - hr * NI;
+            }
+            const u32* crow = codes + hr * NG + hq;
+            const u32 c0 = crow[0], c1 = crow[1];
+            u32* hp = hm + hr * HSK + 18 * hq;
+            f2_hash_pair<0>(hp, c0, c1);
+            f2_hash_pair<2>(hp, c0, c1);
+            f2_hash_pair<4>(hp, c0, c1);
+            f2_hash_pair<6>(hp, c0, c1);
+            f2_hash_pair<8>(hp, c0, c1);
+            f2_hash_pair<10>(hp, c0, c1);
+            f2_hash_pair<12>(hp, c0, c1);
+            f2_hash_pair<14>(hp, c0, c1);
+        }
+        wave_sync();
+        // 3. this lane's chunk: eight window buckets (kNoKey: no key)
+        const bool live_lane = lane < nr * nchr;
+        u32 bk[8];
+        {
+            const u32* hb = hm + (live_lane ? cr_ : 0) * HSK + 9 * cc;
+            u32 h[WM + 7];
+#pragma unroll
+            for (int j = 0; j < WM + 7; j++) h[j] = hb[j + (j >> 3)];
+            u32 core = h[7];
+#pragma unroll
+            for (int j = 8; j < WM; j++) core = min(core, h[j]);
+            u32 lf[8];
+            lf[7] = ~0u;
+#pragma unroll
+            for (int i = 6; i >= 0; i--) lf[i] = min(lf[i + 1], h[i]);
+            u32 rt = ~0u;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if (i > 0) rt = min(rt, h[WM - 1 + i]);
+                const u32 b = min(core, min(lf[i], rt)) & 0xffffu;
+                bk[i] = min(b, kNoKey - 1u);
+            }
+        }
+        u32 act = 0;
+        if (live_lane) {
+            const u32 fl = rflag[cr_];
+            act = (u32)min(8, nw - p0);
+            if (fl == 0u) {
+                my_valid += act;
+            } else {
+                // invalid bases (flag 1): a window is dead when one of its K
+                // bases is not ACGT (not-ACGT bits of bases p0 .. p0 + 55 in
+                // one 64-bit word); a possible key 0^W (flag 2): rolling keys
+                const u32* crw = codes + cr_ * NG;
+                const u32* ir = inval + cr_ * NG;
+                u32 badm = 0;
+                if (fl & 1u) {
+                    const int g0 = p0 >> 4;
+                    const u64 X = (((u64)ir[g0] << 48) | ((u64)ir[g0 + 1] << 32) | ((u64)ir[g0 + 2] << 16) |
+                                   (u64)ir[g0 + 3])
+                                  << (p0 & 15);
+                    constexpr u64 KM = ~0ull << (64 - K);  // a window's K bases
+#pragma unroll
+                    for (int i = 0; i < 8; i++) badm |= ((X & (KM >> i)) ? 1u : 0u) << i;
+                }
+                u32 zm = 0;
+                if (fl & 2u) {
+                    u64 kr[W];
+#pragma unroll
+                    for (int j = 0; j < W; j++) kr[j] = f2_code_word(crw, p0 + 32 * j);
+                    u64 tl = f2_code_word(crw, p0 + 32 * W);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        bool is_zero = (kr[W - 1] & C::LAST_MASK) == 0ull;
+#pragma unroll
+                        for (int j = 0; j < W - 1; j++) is_zero = is_zero && (kr[j] == 0ull);
+                        zm |= (is_zero ? 1u : 0u) << i;
+#pragma unroll
+                        for (int j = 0; j < W - 1; j++) kr[j] = (kr[j] << 2) | (kr[j + 1] >> 62);
+                        kr[W - 1] = (kr[W - 1] << 2) | (tl >> 62);
+                        tl <<= 2;
+                    }
+                }
+                const u32 actm = (1u << act) - 1u;
+                const u32 validm = actm & ~badm;
+                const u32 zeros = (u32)__popc(validm & zm);
+                my_hole |= (actm & badm) != 0u;
+                my_valid += (u32)__popc(validm);
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+                    if ((((validm & ~zm) >> i) & 1u) == 0u) bk[i] = kNoKey;
+                if (zeros) {
+                    atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)zeros);
+                    atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            if (!live_lane || i >= (int)act) bk[i] = kNoKey;
+        // 4. run starts / ends; neighbouring chunks from the neighbouring lanes
+        u32 prev = (u32)__shfl_up((int)bk[7], 1);
+        u32 nxt = (u32)__shfl_down((int)bk[0], 1);
+        if (cc == 0) prev = kNoKey;
+        if (cc == nchr - 1) nxt = kNoKey;
+        u32 smask = 0, emask = 0;
+        {
+            u32 pv = prev;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const u32 v = bk[i];
+                const u32 nx = i < 7 ? bk[i + 1] : nxt;
+                if (v != kNoKey) {
+                    smask |= (v != pv ? 1u : 0u) << i;
+                    emask |= (v != nx ? 1u : 0u) << i;
+                }
+                pv = v;
+            }
+        }
+        const u32 open = (bk[0] != kNoKey && bk[0] == prev) ? 1u : 0u;  // a run continues into this chunk
+        u32 T;
+        const u32 ex = f2_scan16((u32)__popc(smask), &T);
+        {
+            const u32 q0 = (u32)(cr_ * nw + p0);
+            u32 sp = ex, ep = ex - open;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if ((smask >> i) & 1u) sa[sp++] = (q0 + (u32)i) | (bk[i] << 16);
+                if ((emask >> i) & 1u) ea[ep++] = (unsigned short)(q0 + (u32)i);
+            }
+        }
+        wave_sync();
+        // 5. runs -> pieces of <= nmax windows -> records at consecutive
+        // positions of the wave's pool chunk (one global atomic per chunk)
+        for (u32 i0 = 0; i0 < T; i0 += 64) {
+            const u32 i = i0 + (u32)lane;
+            u32 qs = 0, n = 0, sv = 0;
+            if (i < T) {
+                sv = sa[i];
+                qs = sv & 0xffffu;
+                n = (u32)ea[i] - qs + 1u;
+            }
+            const u32 pieces = n <= NMAX ? (n ? 1u : 0u) : (n + NMAX - 1u) / NMAX;
+            u32 ptot, pb;
+            if (__ballot(pieces > 15u) == 0ull) {
+                pb = f2_scan16(pieces, &ptot);
+            } else {
+                const u32 inc = wave_incl_scan(pieces);
+                pb = inc - pieces;
+                ptot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+            const u64 room = cend - ccur;
+            const u64 oc = ccur;
+            u64 nbase = 0;
+            if ((u64)ptot > room) {
+                u64 nb = 0;
+                if (lane == 0) nb = atomicAdd((unsigned long long*)a.pool_cursor, (unsigned long long)a.chunk);
+                nb = readlane64(nb, 0);
+                nbase = nb;
+                ccur = nb + ((u64)ptot - room);
+                cend = nb + a.chunk;
+            } else {
+                ccur += ptot;
+            }
+            if (n == 0) continue;
+            const int r = (int)div_nw.div(qs);
+            const int ps0 = (int)qs - r * nw;
+            const u64 bkt = sv >> 16;
+            const u32* crw = codes + r * NG;
+            u32 g = pb;
+            for (u32 off = 0; off < n; off += NMAX, g++) {
+                const u32 nn = min(NMAX, n - off);
+                const int ps = ps0 + (int)off;
+                u64 rec[RW];
+                rec[0] = (bkt << 48) | (f2_code_word(crw, ps) >> 16);
+#pragma unroll
+                for (int j = 1; j < RW; j++) rec[j] = f2_code_word(crw, ps + 32 * j - 8);
+                const int vb = 16 + 2 * (C::KP + (int)nn - 1);
+#pragma unroll
+                for (int j = 0; j < RW; j++) {
+                    const int bits = vb - 64 * j;
+                    const u64 msk = bits >= 64 ? ~0ull : (bits <= 0 ? 0ull : (~0ull << (64 - bits)));
+                    rec[j] &= msk;
+                }
+                rec[RW - 1] |= (u64)nn;
+                const u64 dst = (u64)g < room ? oc + g : nbase + ((u64)g - room);
+                if (dst < a.pool_cap) {
+#pragma unroll
+                    for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + dst] = rec[j];
+                    if (a.dig1) a.dig1[dst] = (unsigned char)bkt;
+                }
+            }
+        }
+        wave_sync();
+    }
+    // pad the rest of the wave's chunk with n = 0 records in bucket kNoKey
+    for (u64 i = ccur + (u64)lane; i < cend; i += 64)
+        if (i < a.pool_cap) {
+#pragma unroll
+            for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + i] = j == 0 ? ((u64)kNoKey << 48) : 0ull;
+            if (a.dig1) a.dig1[i] = (unsigned char)kNoKey;
+        }
+    wave_add(&a.stats[ST_VALID], my_valid);
+    if (__ballot(my_hole) && lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+}
+
+// F2 geometry for (L, k) (W = 1, m = 11): false when F2 does not apply
+static bool f2_args(const CountLaunch& l, const SkmGeom& g, F2Args* a, size_t* lds) {
+    const int W = (l.k + 31) / 32;
+    if (W != 1 || g.m != 11 || l.k < 18 || l.k > 32 || getenv("KC_NO_F2")) return false;
+    const int nw = l.L - l.k + 1;
+    const int nchr = (nw + 7) / 8;
+    if (nchr > 64 || nw <= 0) return false;
+    const int RW = W + 1;
+    a->G = groups_per_read(l.L);
+    a->nw = nw;
+    a->nchr = nchr;
+    a->R = 64 / nchr;
+    // hash positions needed: [0, 8 nchr + wm + 7)
+    const int wm = l.k - 11 + 1;
+    a->NI = (8 * nchr + wm + 7 + 15) / 16;
+    a->HSK = 18 * a->NI + 1;
+    // code words: records read 3 words from (ps + 32 j - 8) / 16, hashes NI + 1
+    int ng = (8 * nchr + 32 * RW) / 16 + 4;
+    if (ng < a->NI + 2) ng = a->NI + 2;
+    if (ng < a->G + 1) ng = a->G + 1;
+    a->NG = ng;
+    size_t p = (size_t)a->R * ng * 4;
+    a->o_inval = (u32)p;
+    p += (size_t)a->R * ng * 4;
+    a->o_hm = (u32)p;
+    p += (size_t)a->R * a->HSK * 4;
+    a->o_rflag = (u32)p;
+    p += 64 * 4;
+    a->o_sa = (u32)p;
+    p += (size_t)a->R * nchr * 8 * 4;
+    a->o_ea = (u32)p;
+    p += (size_t)a->R * nchr * 8 * 2;
+    p = (p + 15) & ~(size_t)15;
+    a->wbytes = (u32)p;
+    *lds = p * (kSkmBlock / 64);
+    if (*lds > 64 * 1024) return false;
+    if ((u64)a->NI * 64 >= 65536 || (u64)a->G * 64 * kF2Pf >= 65536) return false;  // FastDivU range
+    return true;
+}
+
 SkmGeom skm_geometry(int L, int k) {
     SkmGeom g;
     g.ok = false;
@@ -557,6 +981,43 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
     {
         const char* e = getenv("KC_F_SKIP");
         a.skip = e ? atoi(e) : 0;
+    }
+    {
+        F2Args f2;
+        size_t f2lds = 0;
+        if (f2_args(l, g, &f2, &f2lds)) {
+            f2.codes = l.codes;
+            f2.inval = (const unsigned short*)l.inval;
+            f2.n_reads = l.n_reads;
+            f2.ntiles = (l.n_reads + f2.R - 1) / f2.R;
+            f2.chunk = (u64)f2.R * (u64)f2.nw;
+            if (f2.chunk < 1024) f2.chunk = 1024;
+            f2.pool = pool;
+            f2.pool_cap = pool_cap;
+            f2.pool_cursor = pool_cursor;
+            f2.dig1 = dig1;
+            f2.stats = l.stats;
+            int per_cu = 0, n_cu = 0, dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+#define KC_F2(KK)                                                                                               \
+    case KK:                                                                                                    \
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, skm_front2_k<1, KK>, kSkmBlock, f2lds);    \
+        {                                                                                                       \
+            u64 cap = (per_cu > 0 && n_cu > 0) ? (u64)per_cu * (u64)n_cu : (u64)grid_cap;                      \
+            if (cap > (u64)grid_cap) cap = (u64)grid_cap;                                                       \
+            hipLaunchKernelGGL((skm_front2_k<1, KK>), dim3((int)hmin(f2.ntiles, cap)), dim3(kSkmBlock), f2lds, \
+                               s, f2);                                                                          \
+        }                                                                                                       \
+        break;
+            switch (l.k) {
+                KC_F2(18) KC_F2(19) KC_F2(20) KC_F2(21) KC_F2(22) KC_F2(23) KC_F2(24) KC_F2(25)
+                KC_F2(26) KC_F2(27) KC_F2(28) KC_F2(29) KC_F2(30) KC_F2(31) KC_F2(32)
+            default: return hipErrorInvalidValue;
+            }
+#undef KC_F2
+            return hipGetLastError();
+        }
     }
     const u64 tiles = (l.n_reads + g.R - 1) / g.R;
     const int W = (l.k + 31) / 32;

@@ -148,3 +148,57 @@ def test_auto_engine_switch_after_skm_batches(kca, orc):
         st = ctx.stats()
     assert st["engines_used"] == 3
     assert got == orc.count_fastq(b"".join(blocks), k)
+
+
+def _special_reads(L, n, seed):
+    """Reads that reach F's slow path: not-ACGT bases, aligned all-A groups
+    (possible key 0^W), poly-A / poly-T stretches, lowercase bases."""
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        s = [rng.choice("ACGT") for _ in range(L)]
+        kind = i % 6
+        if kind == 1:
+            for _ in range(rng.randrange(1, 4)):
+                s[rng.randrange(L)] = rng.choice("Nn.")
+        elif kind == 2:
+            a = rng.randrange(0, max(1, L - 40))
+            s[a:a + 40] = "A" * min(40, L - a)
+        elif kind == 3:
+            s = list("A" * L)
+        elif kind == 4:
+            a = rng.randrange(0, max(1, L - 20))
+            s[a:a + 20] = "T" * min(20, L - a)
+            s[rng.randrange(L)] = "N"
+        out.append("".join(s))
+    return out
+
+
+@pytest.mark.parametrize("k", list(range(18, 33)))
+def test_skm_front2_every_k(kca, orc, k):
+    """F2 (skm_front2_k<1, k>, every k of W = 1) against the oracle and
+    against the generic F (KC_NO_F2) on reads that take its slow path, plus
+    genome reads that take its fast path."""
+    L = 150
+    reads = _special_reads(L, 3000, k)
+    fq = _fq(reads) + kca.synth_fastq(20000, L, seed=k, genome_length=200_000, first_read=3000)
+    with kca.Context(kmer_length=k, line_length=L, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("k,L", [(31, 40), (31, 63), (21, 200), (32, 300), (25, 530), (31, 600)])
+def test_skm_front2_read_lengths(kca, orc, monkeypatch, k, L):
+    """Read lengths from one chunk per read to 64 chunks (the F2 limit) and
+    past it (L = 600: the generic F); F2 and the generic F give the same bytes."""
+    fq = _fq(_special_reads(L, 400, L)) + kca.synth_fastq(3000, L, seed=L, genome_length=100_000, first_read=400)
+    outs = []
+    for no_f2 in (False, True):
+        if no_f2:
+            monkeypatch.setenv("KC_NO_F2", "1")
+        with kca.Context(kmer_length=k, line_length=L, engine="skm") as ctx:
+            ctx.count_fastq(fq)
+            outs.append(ctx.records())
+    assert outs[0] == outs[1]
+    assert outs[0] == orc.count_fastq(fq, k)
