@@ -72,6 +72,7 @@ struct kc_ctx {
     uint64_t digs_bytes = 0;
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
+    DevBuf part_dedup;  // skm P5a: per-bucket list starts (u64) and lengths (u32), list cursor
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
     // P5 segment descriptors (see finish_part_sorted) and their sort scratch
     DevBuf desc_key, desc_start, desc_len, desc_k2, desc_v, desc_v2, desc_lens, desc_offs, desc_fb;
@@ -728,6 +729,25 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             c->part_ms[3] += t;
             const uint64_t kbound = nr * nw;
             const uint64_t rec_batch0 = c->rec_n;
+            // P5a (W = 1): each bucket's distinct records and multiplicities,
+            // written to the free tail of the pool arrays (counts into the
+            // digit bytes, free after S2); P5 walks those lists
+            SkmDedup dd = {};
+            const bool dedup = W == 1 && !getenv("KC_NO_DEDUP") && pool_cap > np;
+            uint64_t dcap = 0;
+            if (dedup) {
+                if ((s = ensure(c, c->part_dedup, ((size_t)nb + 1) * 12 + 64))) return s;
+                uint64_t* dstart = (uint64_t*)c->part_dedup.p;
+                uint32_t* dlen = (uint32_t*)(dstart + nb + 1);
+                HIPCHK(c, hipMemsetAsync(dstart + nb, 0, 8, c->stream));  // list cursor
+                dcap = pool_cap - np;
+                if (dcap > c->digs_bytes / 4) dcap = c->digs_bytes / 4;
+                dd.recs = c->keys_a + np;
+                dd.stride = pool_cap;
+                dd.cnt = (const uint32_t*)c->digs;
+                dd.start = dstart;
+                dd.len = dlen;
+            }
             if (getenv("KC_DEBUG")) {
                 std::vector<uint64_t> st((size_t)nb + 1);
                 HIPCHK(c, hipMemcpy(st.data(), c->part_starts.p, st.size() * 8, hipMemcpyDeviceToHost));
@@ -749,6 +769,23 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 const uint64_t rec0 = c->rec_n;
                 const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
                 kc_status s2;
+                if (dedup) {
+                    uint64_t* dstart = (uint64_t*)c->part_dedup.p;
+                    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                    HIPCHK(c, launch_count_rec(c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, b0, b1,
+                                               c->keys_a + np, pool_cap, (uint32_t*)c->digs, dcap, dstart + nb,
+                                               dstart, (uint32_t*)(dstart + nb + 1), c->n_cu, c->stream));
+                    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                    HIPCHK(c, hipEventSynchronize(c->ev1));
+                    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                    c->part_ms[4] += t;
+                    if (getenv("KC_DEBUG")) {
+                        uint64_t dn = 0;
+                        HIPCHK(c, hipMemcpy(&dn, dstart + nb, 8, hipMemcpyDeviceToHost));
+                        fprintf(stderr, "kc: skm P5a[%u,%u) distinct records so far %llu of %llu, %.3f ms\n", b0, b1,
+                                (unsigned long long)dn, (unsigned long long)np, t);
+                    }
+                }
                 for (;;) {
                     if ((s2 = grow_records(c, rec0 + bound))) return s2;
                     // keys_b is free after S2: it takes P5's spills (W x key_cap words)
@@ -756,7 +793,8 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                     HIPCHK(c, launch_count_skm(W, (int)c->k, c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p,
                                                b0, b1, count_keys, c->rec_keys, c->rec_cnts, c->rec_cap,
                                                c->rec_cursor, c->table, c->cap, c->keys_b, c->key_cap, c->stats,
-                                               l.probe_limit, c->cfg.lds_slots, c->n_cu, c->stream));
+                                               l.probe_limit, c->cfg.lds_slots, c->n_cu, c->stream,
+                                               dedup ? &dd : nullptr));
                     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                     HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
                     if ((s2 = sync_stats(c))) return s2;

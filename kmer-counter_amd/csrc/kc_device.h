@@ -228,11 +228,26 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
                              uint8_t* emit, int eshift, int grid, hipStream_t s);
 int skm_lds_slots(int W);
 int seg_sort_cap(int W);  // longest segment seg_sort_k takes
-// buckets [b0, b1); count_keys: add the buckets' key counts to stats[ST_P5_KEYS]
+// P5a (W = 1): per bucket of [b0, b1), its distinct records (2 x ostride SoA
+// at a cursor position, at most ocap in all) with their multiplicities:
+// dstart[b], dlen[b] (kRawList 0xffffffff: not deduplicated)
+hipError_t launch_count_rec(const uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
+                            uint64_t* out, uint64_t ostride, uint32_t* ocnt, uint64_t ocap, uint64_t* ocursor,
+                            uint64_t* dstart, uint32_t* dlen, int grid, hipStream_t s);
+struct SkmDedup {
+    const uint64_t* recs;  // P5a output
+    uint64_t stride;
+    const uint32_t* cnt;
+    const uint64_t* start;
+    const uint32_t* len;
+};
+// buckets [b0, b1); count_keys: add the buckets' key counts to stats[ST_P5_KEYS];
+// dd (optional): P5a's lists, walked instead of the buckets' records
 hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride, const uint64_t* starts,
                             uint32_t b0, uint32_t b1, bool count_keys, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
-                            uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s);
+                            uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s,
+                            const SkmDedup* dd = nullptr);
 
 // Synthetic FASTQ generator (bench/test input).
 struct SynthArgs {

@@ -178,14 +178,16 @@ CountGeom count_geometry(int L, int k) {
 // (possibly stale) load can only be wrong in the EMPTY direction: a non-zero
 // value is the slot's final key and a repeat costs one atomic (the count add);
 // an EMPTY reading is confirmed or corrected by the CAS.
-__device__ __forceinline__ bool insert_w1(u64 key, u64* __restrict__ table, u64 cap, u32 limit, bool* claimed) {
+// w: the count added (a deduplicated super-k-mer's multiplicity; 1 otherwise)
+__device__ __forceinline__ bool insert_w1(u64 key, u64* __restrict__ table, u64 cap, u32 limit, bool* claimed,
+                                          u32 w = 1u) {
     u64 s = __umul64hi(mix64(key ^ 0x9e3779b97f4a7c15ull), cap);
     for (u32 pr = 0; pr < limit; ++pr) {
         u64* slot = table + 2 * s;
         u64 cur = __builtin_nontemporal_load(slot);
         if (cur == 0ull) cur = atomicCAS((unsigned long long*)slot, 0ull, (unsigned long long)key);
         if (cur == 0ull || cur == key) {
-            atomicAdd((unsigned int*)(slot + 1), 1u);
+            atomicAdd((unsigned int*)(slot + 1), w);
             *claimed = (cur == 0ull);
             return true;
         }
@@ -202,7 +204,7 @@ __device__ __forceinline__ bool insert_w1(u64 key, u64* __restrict__ table, u64 
 // which keeps the count exact.
 template <int W>
 __device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict__ table, u64 cap, u32 limit,
-                                            bool* claimed) {
+                                            bool* claimed, u32 w = 1u) {
     // One attempt per iteration and no spin inside divergent code: a lane that
     // finds the slot being published (state 1) retries it next iteration. The
     // claimer publishes within its own iteration, so a lane of the same
@@ -221,7 +223,7 @@ __device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict
 #pragma unroll
                 for (int j = 0; j < W; j++)
                     __hip_atomic_store(slot + j, key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd(cnt, 1u);
+                atomicAdd(cnt, w);
                 __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(state, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 *claimed = true;
@@ -238,7 +240,7 @@ __device__ __forceinline__ bool insert_wide(const u64 (&key)[W], u64* __restrict
         for (int j = 0; j < W; j++)
             eq = eq && (__hip_atomic_load(slot + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key[j]);
         if (eq) {
-            atomicAdd(cnt, 1u);
+            atomicAdd(cnt, w);
             return true;
         }
         if (++pr >= limit) return false;
@@ -1683,7 +1685,7 @@ __device__ __forceinline__ u64 slot_frac(const u64 (&key)[W]) {
 // *claimed is set when this key took an empty slot.
 template <int W, int GS = 4>
 __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* lkeys, u32* lcnt, u32* lstate,
-                                           u32 lcap, u32 max_probe, bool* claimed) {
+                                           u32 lcap, u32 max_probe, bool* claimed, u32 w = 1u) {
     static_assert(GS == 2 || GS == 4, "LDS group of 2 or 4 slots");
     u32 slot = (u32)((frac * (u64)lcap) >> 48);
     if constexpr (W == 1) {
@@ -1709,7 +1711,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
                     if (v[i] == 0ull) emp = i;
                 }
                 if (hit >= 0 && (emp < 0 || hit < emp)) {
-                    atomicAdd(&lcnt[GS * g + hit], 1u);
+                    atomicAdd(&lcnt[GS * g + hit], w);
                     return true;
                 }
                 if (emp >= 0) {
@@ -1717,7 +1719,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
                     const u64 old =
                         atomicCAS((unsigned long long*)&lkeys[GS * g + emp], 0ull, (unsigned long long)key[0]);
                     if (old == 0ull || old == key[0]) {
-                        atomicAdd(&lcnt[GS * g + emp], 1u);
+                        atomicAdd(&lcnt[GS * g + emp], w);
                         *claimed = old == 0ull;
                         return true;
                     }
@@ -1734,7 +1736,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
             u64 old = __hip_atomic_load(&lkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (old == 0ull) old = atomicCAS((unsigned long long*)&lkeys[slot], 0ull, (unsigned long long)key[0]);
             if (old == 0ull || old == key[0]) {
-                atomicAdd(&lcnt[slot], 1u);
+                atomicAdd(&lcnt[slot], w);
                 *claimed = old == 0ull;
                 return true;
             }
@@ -1751,7 +1753,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
                 if (prev == 0u) {
 #pragma unroll
                     for (int j = 0; j < W; j++) lkeys[(size_t)j * lcap + slot] = key[j];
-                    atomicAdd(&lcnt[slot], 1u);
+                    atomicAdd(&lcnt[slot], w);
                     __hip_atomic_store(&lstate[slot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     *claimed = true;
                     return true;
@@ -1763,7 +1765,7 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
 #pragma unroll
             for (int j = 0; j < W; j++) eq = eq && lkeys[(size_t)j * lcap + slot] == key[j];
             if (eq) {
-                atomicAdd(&lcnt[slot], 1u);
+                atomicAdd(&lcnt[slot], w);
                 return true;
             }
             if (++pr >= max_probe) return false;

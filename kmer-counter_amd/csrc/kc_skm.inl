@@ -1329,7 +1329,18 @@ struct SkmBucketArgs {
     u64* stats;
     u32 probe_limit;
     int skip;
+    // deduplicated records (P5a, count_rec_k): bucket b's dlen[b] distinct
+    // records from index dstart[b] of drecs (RW x dstride SoA) with their
+    // multiplicities dcnt; drecs == nullptr or dlen[b] == kRawList: the
+    // bucket's own records from recs (multiplicity 1)
+    const u64* drecs;
+    u64 dstride;
+    const u32* dcnt;
+    const u64* dstart;
+    const u32* dlen;
 };
+
+constexpr u32 kRawList = 0xffffffffu;  // P5a: bucket not deduplicated
 
 // key i of a record (see the record layout above)
 template <int W>
@@ -1356,8 +1367,10 @@ constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: key
 // P5 LDS: table (lcap slots) + misc (48 u32) + per-wave slow-path queues +
 // per-wave record stage (64 records of W + 1 words + one spare, so the record
 // after the last can be read unconditionally)
+// (+ per-wave u32 weights of the queue and of the record stage)
 static size_t skm_fixed_lds(int W) {
-    return 48 * 4 + (size_t)kBucketWaves * kSkmQueue * 8 + (size_t)kBucketWaves * 65 * (W + 1) * 8 + 16;
+    return 48 * 4 + (size_t)kBucketWaves * kSkmQueue * 8 + (size_t)kBucketWaves * 65 * (W + 1) * 8 +
+           (size_t)kBucketWaves * (kSkmQueue + 65) * 4 + 16;
 }
 
 int skm_lds_slots(int W) {
@@ -1416,14 +1429,15 @@ struct SkmLdsTable {
 // last sub-range level the global table and the spill buffer. Out of line:
 // it runs once per 64 queued keys and keeps the hot loop small.
 template <int W>
-__device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t, const u64* wq, u32 c, u64 lo,
-                                       bool last, u32 limit) {
+__device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t, const u64* wq, const u32* wqw, u32 c,
+                                       const u64* recs, u64 stride, u64 lo, bool last, u32 limit) {
     constexpr int RW = W + 1;
     const int lane = (int)lane_id();
     const bool act = lane < (int)c;
     u64 qk[W];
 #pragma unroll
     for (int j = 0; j < W; j++) qk[j] = 0;
+    const u32 w = act ? wqw[lane] : 0u;  // the key's multiplicity
     if (act) {
         const u64 e = wq[lane];
         if constexpr (W == 1) {
@@ -1432,7 +1446,7 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
             const u64 ri = lo + (e >> 6);
             u64 rw[RW];
 #pragma unroll
-            for (int j = 0; j < RW; j++) rw[j] = a.recs[(u64)j * a.stride + ri];
+            for (int j = 0; j < RW; j++) rw[j] = recs[(u64)j * stride + ri];
             skm_key<W>(rw, (u32)(e & 63u), a.last_mask, qk);
         }
     }
@@ -1440,13 +1454,13 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
     if (act) {
         const u64 frac = (u64)skm_hash32<W>(qk) << 16;
         if (!lds_insert<W, kSkmGroup>(qk, frac, t.lkeys, t.lcnt, t.lstate, a.lcap,
-                                      last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u), &lclaim)) {
+                                      last ? a.lcap : (a.lcap < 64u ? a.lcap : 64u), &lclaim, w)) {
             if (!last) {
                 full = true;
             } else if constexpr (W == 1) {
-                done = insert_w1(qk[0], a.table, a.cap, a.probe_limit, &claimed);
+                done = insert_w1(qk[0], a.table, a.cap, a.probe_limit, &claimed, w);
             } else {
-                done = insert_wide<W>(qk, a.table, a.cap, a.probe_limit, &claimed);
+                done = insert_wide<W>(qk, a.table, a.cap, a.probe_limit, &claimed, w);
             }
         }
     }
@@ -1460,13 +1474,20 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
         u64 cm = __ballot(claimed);
         if (cm && lane == __ffsll((long long)cm) - 1)
             atomicAdd((unsigned long long*)&a.stats[ST_CLAIMED], (unsigned long long)__popcll(cm));
-        bool spill = !done;
-        if (__ballot(spill)) {
-            u64 idx = wave_reserve(a.spill_ctr, spill);
-            if (spill) {
-                if (idx < a.spill_cap) {
+        // a spilled key is written once per unit of its multiplicity (the
+        // spill runs are counted by sort + run length)
+        const u32 ws = done ? 0u : w;
+        if (__ballot(ws != 0u)) {
+            const u32 inc = wave_incl_scan(ws);
+            const u32 tot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
+            u64 base = 0;
+            if (lane == 0) base = atomicAdd((unsigned long long*)a.spill_ctr, (unsigned long long)tot);
+            base = readlane64(base, 0);
+            const u64 idx = base + (inc - ws);
+            for (u32 r = 0; r < ws; r++) {
+                if (idx + r < a.spill_cap) {
 #pragma unroll
-                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx] = qk[j];
+                    for (int j = 0; j < W; j++) a.spill[(u64)j * a.spill_cap + idx + r] = qk[j];
                 } else {
                     atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_SPILL_OVERFLOW);
                 }
@@ -1494,6 +1515,10 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     const u64 lane_lt = lanemask_lt();
     u64* wq = (u64*)(misc + 48) + (tid >> 6) * kSkmQueue;
     u64* wst = (u64*)(misc + 48) + kBucketWaves * kSkmQueue + (tid >> 6) * 65 * RW;  // this wave's record stage (+1 spare)
+    u32* wqw = (u32*)((u64*)(misc + 48) + kBucketWaves * kSkmQueue + kBucketWaves * 65 * RW) +
+               (tid >> 6) * kSkmQueue;                                  // queue multiplicities
+    u32* wsw = (u32*)((u64*)(misc + 48) + kBucketWaves * kSkmQueue + kBucketWaves * 65 * RW) +
+               kBucketWaves * kSkmQueue + (tid >> 6) * 65;              // stage multiplicities
     const SkmLdsTable tab = {lkeys, lcnt, lstate, lfill, labort};
     for (u32 i = tid; i < a.lcap; i += kBucketBlock) {
 #pragma unroll
@@ -1515,16 +1540,38 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     // (speculatively the next bucket's; a sub-range pass of the same bucket
     // reloads): pfb is the bucket pf holds the pass-start batches of
     u64 pf[PD][RW];
+    u32 pfw[PD];
     u32 pfb = ~0u;
+    // bucket bb's record source: deduplicated list or its own records
+    auto source = [&](u32 bb, const u64** rp, u64* st, const u32** cp, u64* l0, u64* h0) {
+        const u32 dl = a.drecs ? a.dlen[bb] : kRawList;
+        if (dl != kRawList) {
+            *rp = a.drecs;
+            *st = a.dstride;
+            *cp = a.dcnt;
+            *l0 = a.dstart[bb];
+            *h0 = *l0 + dl;
+        } else {
+            *rp = a.recs;
+            *st = a.stride;
+            *cp = nullptr;
+            *l0 = a.starts[bb];
+            *h0 = a.starts[bb + 1];
+        }
+    };
     auto prefetch_pass = [&](u32 bb) {
-        const u64 l0 = a.starts[bb], h0 = a.starts[bb + 1];
+        const u64* rp;
+        u64 rst, l0, h0;
+        const u32* cp;
+        source(bb, &rp, &rst, &cp, &l0, &h0);
         const u64 nr0 = h0 - l0, pw = (nr0 + kBucketWaves - 1) / kBucketWaves;
         const u64 w0 = l0 + min(nr0, (u64)(tid >> 6) * pw), w1 = l0 + min(nr0, (u64)((tid >> 6) + 1) * pw);
 #pragma unroll
         for (int d = 0; d < PD; d++) {
             const u64 i = w0 + (u64)d * 64 + lane;
 #pragma unroll
-            for (int j = 0; j < RW; j++) pf[d][j] = i < w1 ? a.recs[(u64)j * a.stride + i] : 0ull;
+            for (int j = 0; j < RW; j++) pf[d][j] = i < w1 ? rp[(u64)j * rst + i] : 0ull;
+            pfw[d] = (cp && i < w1) ? cp[i] : 1u;
         }
         pfb = bb;
     };
@@ -1537,10 +1584,14 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
         const bool stop = *lnext != 0u;
         __syncthreads();
         if (stop) return;
-        const u64 lo = a.starts[b], hi = a.starts[b + 1];
+        const u64* brecs;
+        u64 bstride, lo, hi;
+        const u32* bcnt;
+        source(b, &brecs, &bstride, &bcnt, &lo, &hi);
         if (a.count_keys) {
             u64 kn = 0;
-            for (u64 i = lo + tid; i < hi; i += kBucketBlock) kn += a.recs[(u64)(RW - 1) * a.stride + i] & 63u;
+            for (u64 i = lo + tid; i < hi; i += kBucketBlock)
+                kn += (brecs[(u64)(RW - 1) * bstride + i] & 63u) * (u64)(bcnt ? bcnt[i] : 1u);
             wave_add(&a.stats[ST_P5_KEYS], kn);
         }
         u32 m = 1, sub = 0;
@@ -1566,15 +1617,19 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 // this batch's record -> the wave's LDS stage; next loads issued
 #pragma unroll
                 for (int j = 0; j < RW; j++) wst[(size_t)lane * RW + j] = pf[0][j];
+                wsw[lane] = pfw[0];
                 const u32 n = (u32)(pf[0][RW - 1] & 63u);
 #pragma unroll
-                for (int d = 0; d + 1 < PD; d++)
+                for (int d = 0; d + 1 < PD; d++) {
 #pragma unroll
                     for (int j = 0; j < RW; j++) pf[d][j] = pf[d + 1][j];
+                    pfw[d] = pfw[d + 1];
+                }
                 {
                     const u64 i = base + (u64)PD * 64 + lane;
 #pragma unroll
-                    for (int j = 0; j < RW; j++) pf[PD - 1][j] = i < whi ? a.recs[(u64)j * a.stride + i] : 0ull;
+                    for (int j = 0; j < RW; j++) pf[PD - 1][j] = i < whi ? brecs[(u64)j * bstride + i] : 0ull;
+                    pfw[PD - 1] = (bcnt && i < whi) ? bcnt[i] : 1u;
                 }
                 // the wave's keys as one flat sequence: exclusive scan of the
                 // records' key counts; lane l takes keys [l*per, l*per + per)
@@ -1602,6 +1657,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 u64 cur[RW];
 #pragma unroll
                 for (int j = 0; j < RW; j++) cur[j] = wst[(size_t)o * RW + j];
+                u32 wcur = wsw[o];  // the current record's multiplicity
                 u32 nn = (u32)(cur[RW - 1] & 63u);
                 u64 win[RW];
                 skm_window<RW>(cur, 16u + 2u * ki, win);
@@ -1613,6 +1669,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 u64 nxt[RW];
 #pragma unroll
                 for (int j = 0; j < RW; j++) nxt[j] = wst[(size_t)(o + 1) * RW + j];
+                u32 wnxt = wsw[o + 1];
                 auto advance = [&](u32 t) {
 #pragma unroll
                     for (int j = 0; j < RW - 1; j++) win[j] = (win[j] << 2) | (win[j + 1] >> 62);
@@ -1622,6 +1679,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         ++o;
 #pragma unroll
                         for (int j = 0; j < RW; j++) cur[j] = nxt[j];
+                        wcur = wnxt;
                         // every record of a counted bucket has n >= 1: F writes
                         // n = 0 padding only into bucket 0xffff, never counted
                         nn = (u32)(cur[RW - 1] & 63u);
@@ -1632,6 +1690,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int j = 0; j < RW; j++) nxt[j] = wst[(size_t)(o + 1) * RW + j];
+                        wnxt = wsw[o + 1];
                         ki = 0;
                     }
                 };
@@ -1640,6 +1699,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     // while key t is resolved (a group read before a claim of
                     // the slow path only sends that key to the slow path again)
                     u64 key = win[0] & a.last_mask;
+                    u32 kw = wcur;
                     bool act = s0 < s1;
                     u32 g = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key), ng);
                     v2u64 a0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[0];
@@ -1648,6 +1708,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         advance(t);
                         const bool act_n = s0 + t + 1 < s1;
                         const u64 key_n = win[0] & a.last_mask;
+                        const u32 kw_n = wcur;
                         const u32 g_n = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key_n), ng);
                         const v2u64 b0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[0];
                         const v2u64 b1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[1];
@@ -1659,21 +1720,30 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                         const bool e0 = a0.x == key, e1 = a0.y == key, e2 = a1.x == key, e3 = a1.y == key;
                         const int hit = e0 ? 0 : (e1 ? 1 : (e2 ? 2 : 3));
                         const bool found = want && (e0 || e1 || e2 || e3);
-                        if (found) atomicAdd(&lcnt[kSkmGroup * g + hit], 1u);
+                        if (found) atomicAdd(&lcnt[kSkmGroup * g + hit], kw);
                         const bool pend = want && !found;
                         const u64 pb = __ballot(pend);
                         if (pb) {
-                            if (pend) wq[qn + (u32)__popcll(pb & lane_lt)] = key;
+                            if (pend) {
+                                const u32 at = qn + (u32)__popcll(pb & lane_lt);
+                                wq[at] = key;
+                                wqw[at] = kw;
+                            }
                             qn += (u32)__popcll(pb);
                             if (qn >= 64) {
-                                skm_drain<W>(a, tab, wq, 64, lo, last, limit);
+                                skm_drain<W>(a, tab, wq, wqw, 64, brecs, bstride, lo, last, limit);
                                 const u32 rest = qn - 64;
                                 const u64 keep = lane < (int)rest ? wq[64 + lane] : 0ull;
-                                if (lane < (int)rest) wq[lane] = keep;
+                                const u32 keepw = lane < (int)rest ? wqw[64 + lane] : 0u;
+                                if (lane < (int)rest) {
+                                    wq[lane] = keep;
+                                    wqw[lane] = keepw;
+                                }
                                 qn = rest;
                             }
                         }
                         key = key_n;
+                        kw = kw_n;
                         act = act_n;
                         g = g_n;
                         a0 = b0;
@@ -1698,20 +1768,27 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
 #pragma unroll
                             for (int j = 0; j < W; j++) eq = eq && lkeys[(size_t)j * a.lcap + sl] == key[j];
                             found = want && eq;
-                            if (found) atomicAdd(&lcnt[sl], 1u);
+                            if (found) atomicAdd(&lcnt[sl], wcur);
                         }
                     }
                     const bool pend = want && !found;
                     const u64 pb = __ballot(pend);
                     if (pb) {
-                        if (pend)
-                            wq[qn + (u32)__popcll(pb & lane_lt)] = W == 1 ? key[0] : (((wrec0 + (u64)o) << 6) | ki);
+                        if (pend) {
+                            const u32 at = qn + (u32)__popcll(pb & lane_lt);
+                            wq[at] = W == 1 ? key[0] : (((wrec0 + (u64)o) << 6) | ki);
+                            wqw[at] = wcur;
+                        }
                         qn += (u32)__popcll(pb);
                         if (qn >= 64) {
-                            skm_drain<W>(a, tab, wq, 64, lo, last, limit);
+                            skm_drain<W>(a, tab, wq, wqw, 64, brecs, bstride, lo, last, limit);
                             const u32 rest = qn - 64;
                             const u64 keep = lane < (int)rest ? wq[64 + lane] : 0ull;
-                            if (lane < (int)rest) wq[lane] = keep;
+                            const u32 keepw = lane < (int)rest ? wqw[64 + lane] : 0u;
+                            if (lane < (int)rest) {
+                                wq[lane] = keep;
+                                wqw[lane] = keepw;
+                            }
                             qn = rest;
                         }
                     }
@@ -1723,7 +1800,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
             // check and the emission (unless another pass of this bucket follows)
             if (sub + 1 >= m && b + gridDim.x < a.nbuckets) prefetch_pass(b + gridDim.x);
             if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-                skm_drain<W>(a, tab, wq, qn, lo, last, limit);
+                skm_drain<W>(a, tab, wq, wqw, qn, brecs, bstride, lo, last, limit);
             __syncthreads();
             const bool aborted = *labort != 0u;
             if (aborted && my_keys) atomicAdd(lkscan, my_keys);
@@ -1820,8 +1897,14 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
 hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride, const uint64_t* starts,
                             uint32_t b0, uint32_t b1, bool count_keys, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
-                            uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s) {
+                            uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s,
+                            const SkmDedup* dd) {
     SkmBucketArgs a;
+    a.drecs = dd ? dd->recs : nullptr;
+    a.dstride = dd ? dd->stride : 0;
+    a.dcnt = dd ? dd->cnt : nullptr;
+    a.dstart = dd ? dd->start : nullptr;
+    a.dlen = dd ? dd->len : nullptr;
     {
         const char* e = getenv("KC_P5_SKIP");
         a.skip = e ? atoi(e) : 0;
@@ -1853,6 +1936,197 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
     case 3: hipLaunchKernelGGL(count_skm_k<3>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// P5a: count_rec_k (W = 1). At genome coverage most super-k-mer records of a
+// bucket are copies of one another: every read that covers a run of windows
+// sharing one minimizer cuts the same record (only runs cut by a read end or a
+// bad base differ). Each workgroup takes buckets like P5; the bucket's records
+// go into an LDS table of whole records (both words; the bucket bits replaced
+// by a non-zero marker, the bucket is known) with a count per entry. Equal
+// records meet in one entry; a record whose claim races with a writer may
+// take a second entry, which only costs dedup, never a count. The distinct
+// records and their multiplicities are written as the bucket's list
+// (dstart[b], dlen[b]); P5 then walks each distinct record's keys once,
+// adding the multiplicity. A bucket whose table fills, or whose list does not
+// fit the output, is marked kRawList and P5 walks its own records.
+// ---------------------------------------------------------------------------
+
+constexpr int kRecProbe = 8;  // P5a: groups probed per record
+
+struct RecDedupArgs {
+    const u64* recs;  // 2 x stride (SoA), grouped by bucket
+    u64 stride;
+    const u64* starts;
+    u32 b0, nbuckets;
+    u32 ngrp;         // LDS groups of 2 entries
+    u64* out;         // distinct records: 2 x ostride (SoA)
+    u64 ostride;
+    u32* ocnt;
+    u64 ocap;
+    u64* ocursor;
+    u64* dstart;
+    u32* dlen;
+};
+
+__device__ __forceinline__ u32 rec_hash(u64 k0, u64 k1) {
+    const u32 x = (u32)k0 ^ ((u32)(k0 >> 32) * 0x9e3779b1u);
+    const u32 y = (u32)k1 ^ ((u32)(k1 >> 32) * 0x85ebca6bu);
+    return fmix32(x ^ (y * 0xcc9e2d51u));
+}
+
+static size_t rec_dedup_lds(u32 ngrp) { return (size_t)ngrp * 40 + 64 * 4 + 16; }
+
+u32 rec_dedup_groups() {
+    u32 g = (u32)((160 * 1024 - 64 * 4 - 16 - 64) / 40);
+    return g & ~15u;
+}
+
+__global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* tab = (u64*)smem;                         // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
+    u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);   // 2 ngrp
+    u32* misc = cnt + 2 * (size_t)a.ngrp;          // [0] overflow, [1..16] wave totals, [18..19] base
+    const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
+    const u32 nent = 2 * a.ngrp;
+    const u64 lt = lanemask_lt();
+    for (u32 i = tid; i < nent; i += kBucketBlock) {
+        tab[2 * (size_t)i] = 0ull;
+        tab[2 * (size_t)i + 1] = 0ull;
+        cnt[i] = 0;
+    }
+    if (tid == 0) misc[0] = 0;
+    __syncthreads();
+    constexpr u64 kMark = 0x8000ull << 48;  // replaces the bucket bits: a non-zero word 0
+    constexpr u64 kLow48 = (1ull << 48) - 1ull;
+    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        const u64 lo = a.starts[b], hi = a.starts[b + 1];
+        const u64 nr = hi - lo, per_w = (nr + kBucketWaves - 1) / kBucketWaves;
+        const u64 wlo = lo + min(nr, (u64)wave * per_w), whi = lo + min(nr, (u64)(wave + 1) * per_w);
+        // one record per lane, the next batch in flight
+        u64 n0 = 0, n1 = 0;
+        if (wlo + lane < whi) {
+            n0 = a.recs[wlo + lane];
+            n1 = a.recs[a.stride + wlo + lane];
+        }
+        bool over = false;
+        for (u64 base = wlo; base < whi; base += 64) {
+            const bool act = base + lane < whi;
+            const u64 k0 = (n0 & kLow48) | kMark, k1 = n1;
+            {
+                const u64 i = base + 64 + lane;
+                n0 = i < whi ? a.recs[i] : 0ull;
+                n1 = i < whi ? a.recs[a.stride + i] : 0ull;
+            }
+            u32 g = __umulhi(rec_hash(k0, k1), a.ngrp);
+            bool done = !act;
+            for (int pr = 0; pr < kRecProbe; pr++) {
+                if (!__ballot(!done)) break;
+                if (!done) {
+                    const v2u64 e0 = ((const lds_v2u64*)(tab + 4 * (size_t)g))[0];
+                    const v2u64 e1 = ((const lds_v2u64*)(tab + 4 * (size_t)g))[1];
+                    if (e0.x == k0 && e0.y == k1) {
+                        atomicAdd(&cnt[2 * g], 1u);
+                        done = true;
+                    } else if (e1.x == k0 && e1.y == k1) {
+                        atomicAdd(&cnt[2 * g + 1], 1u);
+                        done = true;
+                    } else if (e0.x == 0ull || e1.x == 0ull) {
+                        const u32 e = e0.x == 0ull ? 2 * g : 2 * g + 1;
+                        const u64 old = atomicCAS((unsigned long long*)&tab[2 * (size_t)e], 0ull, (unsigned long long)k0);
+                        if (old == 0ull) {
+                            tab[2 * (size_t)e + 1] = k1;
+                            atomicAdd(&cnt[e], 1u);
+                            done = true;
+                        }
+                        // lost the entry: the group is read again
+                    } else {
+                        g = g + 1 == a.ngrp ? 0 : g + 1;
+                    }
+                }
+            }
+            over |= !done;
+        }
+        if (__ballot(over) && lane == 0) atomicOr(&misc[0], 1u);
+        __syncthreads();
+        const bool raw = misc[0] != 0u;
+        // emission: distinct records of the bucket, contiguous from one base
+        const u32 spw = (nent + kBucketWaves - 1) / kBucketWaves;
+        const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
+        u32 wc = 0;
+        if (!raw)
+            for (u32 c0 = s0; c0 < s1; c0 += 64) {
+                const u32 i = c0 + (u32)lane;
+                wc += (u32)__popcll(__ballot(i < s1 && tab[2 * (size_t)i] != 0ull));
+            }
+        if (lane == 0) misc[1 + wave] = wc;
+        __syncthreads();
+        u32 total = 0, before = 0;
+        for (int w = 0; w < kBucketWaves; w++) {
+            const u32 v = misc[1 + w];
+            before += w < wave ? v : 0u;
+            total += v;
+        }
+        if (tid == 0) {
+            u64 rb = 0;
+            bool fits = !raw;
+            if (fits && total) {
+                rb = atomicAdd((unsigned long long*)a.ocursor, (unsigned long long)total);
+                fits = rb + total <= a.ocap;
+            }
+            *(u64*)(misc + 18) = rb;
+            misc[0] = fits ? 0u : 1u;
+            a.dstart[b] = rb;
+            a.dlen[b] = fits ? total : kRawList;
+        }
+        __syncthreads();
+        const bool write = misc[0] == 0u;
+        u64 pos = *(u64*)(misc + 18) + before;
+        for (u32 c0 = s0; c0 < s1; c0 += 64) {
+            const u32 i = c0 + (u32)lane;
+            const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
+            const u64 bm = __ballot(occ);
+            if (occ) {
+                if (write) {
+                    const u64 q = pos + (u64)__popcll(bm & lt);
+                    a.out[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
+                    a.out[a.ostride + q] = tab[2 * (size_t)i + 1];
+                    a.ocnt[q] = cnt[i];
+                }
+                tab[2 * (size_t)i] = 0ull;
+                tab[2 * (size_t)i + 1] = 0ull;
+                cnt[i] = 0;
+            }
+            pos += (u64)__popcll(bm);
+        }
+        if (tid == 0) misc[0] = 0;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_count_rec(const uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
+                            uint64_t* out, uint64_t ostride, uint32_t* ocnt, uint64_t ocap, uint64_t* ocursor,
+                            uint64_t* dstart, uint32_t* dlen, int grid, hipStream_t s) {
+    if (b1 <= b0) return hipSuccess;
+    RecDedupArgs a;
+    a.recs = recs;
+    a.stride = stride;
+    a.starts = starts;
+    a.b0 = b0;
+    a.nbuckets = b1;
+    a.ngrp = rec_dedup_groups();
+    a.out = out;
+    a.ostride = ostride;
+    a.ocnt = ocnt;
+    a.ocap = ocap;
+    a.ocursor = ocursor;
+    a.dstart = dstart;
+    a.dlen = dlen;
+    const size_t lds = (rec_dedup_lds(a.ngrp) + 15) & ~(size_t)15;
+    hipLaunchKernelGGL(count_rec_k, dim3(grid), dim3(kBucketBlock), lds, s, a);
     return hipGetLastError();
 }
 
