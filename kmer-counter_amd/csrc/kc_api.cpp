@@ -742,6 +742,10 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 HIPCHK(c, hipMemsetAsync(dstart + nb, 0, 8, c->stream));  // list cursor
                 dcap = pool_cap - np;
                 if (dcap > c->digs_bytes / 4) dcap = c->digs_bytes / 4;
+                if (const char* e = getenv("KC_P5A_CAP")) {  // tests: lists past this many records are walked raw
+                    const uint64_t v = strtoull(e, nullptr, 10);
+                    if (v < dcap) dcap = v;
+                }
                 dd.recs = c->keys_a + np;
                 dd.stride = pool_cap;
                 dd.cnt = (const uint32_t*)c->digs;

@@ -2118,6 +2118,10 @@ hipError_t launch_count_rec(const uint64_t* recs, uint64_t stride, const uint64_
     a.b0 = b0;
     a.nbuckets = b1;
     a.ngrp = rec_dedup_groups();
+    if (const char* e = getenv("KC_P5A_GROUPS")) {  // tests: force full tables (raw buckets)
+        const long v = atol(e);
+        if (v > 0 && (u32)v < a.ngrp) a.ngrp = (u32)v;
+    }
     a.out = out;
     a.ostride = ostride;
     a.ocnt = ocnt;

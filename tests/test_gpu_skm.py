@@ -202,3 +202,50 @@ def test_skm_front2_read_lengths(kca, orc, monkeypatch, k, L):
             outs.append(ctx.records())
     assert outs[0] == outs[1]
     assert outs[0] == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("groups", [None, "64", "3"])
+def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
+    """P5a: genome reads at ~20x, where most records repeat; with a small
+    record table (KC_P5A_GROUPS) buckets overflow it and P5 walks their own
+    records (kRawList); KC_NO_DEDUP walks every bucket's own records."""
+    if groups:
+        monkeypatch.setenv("KC_P5A_GROUPS", groups)
+    fq = kca.synth_fastq(60000, 150, seed=33, genome_length=400_000, n_rate=0.0005)
+    with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    monkeypatch.setenv("KC_NO_DEDUP", "1")
+    with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        raw = ctx.records()
+    assert got == raw
+    assert got == orc.count_fastq(fq, 31)
+    assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
+
+
+def test_skm_dedup_list_overflow(kca, orc, monkeypatch):
+    """The distinct lists capped below the batch's distinct records
+    (KC_P5A_CAP): the buckets whose list does not fit are walked raw."""
+    monkeypatch.setenv("KC_P5A_CAP", "50000")
+    fq = kca.synth_fastq(60000, 150, seed=34, genome_length=300_000)
+    with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, 31)
+
+
+@pytest.mark.parametrize("k", [21, 31])
+def test_skm_dedup_weighted_spill(kca, orc, tmp_path, k):
+    """Deduplicated records with multiplicities > 1 through the last-resort
+    paths: a 1-slot LDS table and a 1 MiB working set send keys to the global
+    table and the spill runs, where a key is written once per unit of its
+    multiplicity."""
+    fq = kca.synth_fastq(20000, 150, seed=35, genome_length=60_000)
+    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=1 << 20, engine="skm", lds_slots=1) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.output_bytes(str(tmp_path))
+        st = ctx.stats()
+    assert st["spilled_kmers"] > 0
+    assert got == orc.count_fastq(fq, k)
