@@ -172,6 +172,7 @@ def main():
     finish_ms = 0.0
     decode_ms = 0.0
     part_ms = [0.0] * 5
+    dedup_ms = 0.0
     n_rec = 0
     for _ in range(args.steps):
         n_rec = step()
@@ -181,6 +182,7 @@ def main():
         finish_ms += st["finish_ms"]
         decode_ms += st["decode_ms"]
         part_ms = [a + b for a, b in zip(part_ms, st["part_ms"])]
+        dedup_ms += st.get("dedup_ms", 0.0)
     barrier_sync()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
@@ -218,14 +220,30 @@ def main():
         # the records, priced per batch)
         rec_step = st["keys"] or 1  # records handed out by F per step
         rb = 8 * (W + 1)
+        # F2 (skm_front2_k<1, k>) covers W = 1, 18 <= k <= 32 with at most 64
+        # 8-window chunks per read; the generic F otherwise
+        f2 = W == 1 and 18 <= k <= 32 and (L - k + 1 + 7) // 8 <= 64
+        fname = f"skm_front2_k<1,{k}>" if f2 else f"skm_front_k<{W}>"
+        dd_step = st.get("dedup_records", 0)  # ctx stats are per step
         specs = [
-            ("F", f"skm_front_k<{W}>", part_ms[1], launches, windows_step, "k-mers",
+            ("F", fname, part_ms[1], launches, windows_step, "k-mers",
              (G * 6) / max(1, L - k + 1) + rb * rec_step / windows_step),
             ("S", f"rp_scatter_k<{W + 1},false>", part_ms[2], 2 * steps * st["batches"], 2 * rec_step, "records",
              2 * rb + 1),
-            ("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], rec_step, "records",
-             rb + (8 * W + 4) * recs_step / rec_step),
         ]
+        if dedup_ms > 0:
+            # P5a reads every record and writes each distinct one with its
+            # multiplicity; P5 then reads the distinct records and writes the
+            # distinct (key, count) records
+            specs += [
+                ("P5a", "count_rec_k", dedup_ms, steps * st["batches"], rec_step, "records",
+                 rb + (rb + 4) * dd_step / rec_step),
+                ("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], max(1, dd_step), "distinct records",
+                 (rb + 4) + (8 * W + 4) * recs_step / max(1, dd_step)),
+            ]
+        else:
+            specs.append(("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], rec_step, "records",
+                          rb + (8 * W + 4) * recs_step / rec_step))
     elif used & 2:
         p5_per_step = max(1, st["p5_launches"])
         specs = [
@@ -293,7 +311,8 @@ def main():
             "breakdown_ms_per_step": {"p2_scatter": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
                                       "finish": finish_ms / args.steps,
                                       "exchange_rank0": xch_ms[0] / args.steps,
-                                      "partition_passes": [round(x / args.steps, 3) for x in part_ms]},
+                                      "partition_passes": [round(x / args.steps, 3) for x in part_ms],
+                                      "p5a_dedup": round(dedup_ms / args.steps, 3)},
             "engine": args.engine, "engines_used": {1: "skm", 2: "key-prefix partition", 3: "skm + key-prefix",
                                                     4: "table"}.get(st.get("engines_used", 0), str(st.get("engines_used"))),
             "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"],

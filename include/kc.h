@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define KC_ABI_VERSION 1
+#define KC_ABI_VERSION 2 /* 2: kc_stats.dedup_ms / dedup_records */
 #define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
 
 typedef enum kc_status {
@@ -137,6 +137,10 @@ typedef struct kc_stats {
     uint32_t engines_used;     /* bit 0: super-k-mer, bit 1: key-prefix partition,
                                   bit 2: global table (batches since the last reset) */
     uint32_t reserved1;
+    double dedup_ms;           /* super-k-mer engine, W = 1: summed device time of
+                                  P5a (identical records of a bucket counted once);
+                                  part_ms[4] is then the weighted P5 walk alone */
+    uint64_t dedup_records;    /* distinct records P5a listed since the last reset */
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". */

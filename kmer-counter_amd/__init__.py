@@ -77,6 +77,8 @@ class Stats(ctypes.Structure):
         ("p5_launches", ctypes.c_uint64),
         ("engines_used", ctypes.c_uint32),
         ("reserved1", ctypes.c_uint32),
+        ("dedup_ms", ctypes.c_double),
+        ("dedup_records", ctypes.c_uint64),
     ]
 
     def as_dict(self):

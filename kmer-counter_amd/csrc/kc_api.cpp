@@ -84,6 +84,8 @@ struct kc_ctx {
     uint64_t batches = 0;
     int n_cu = 256;
     double part_ms[5] = {0, 0, 0, 0, 0};  // E+P1, P2, P3 scatter, P3 hist + P4, P5
+    double dedup_ms = 0;                  // skm P5a
+    uint64_t dedup_records = 0;
     uint64_t part_keys = 0;               // keys partitioned since the last reset
     uint64_t p5_launches = 0;
 
@@ -782,7 +784,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                     HIPCHK(c, hipEventSynchronize(c->ev1));
                     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-                    c->part_ms[4] += t;
+                    c->dedup_ms += t;
                     if (getenv("KC_DEBUG")) {
                         uint64_t dn = 0;
                         HIPCHK(c, hipMemcpy(&dn, dstart + nb, 8, hipMemcpyDeviceToHost));
@@ -854,6 +856,11 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 }
             }
             if ((s = p5_range(bs, nbk, false))) return s;
+            if (dedup) {
+                uint64_t dn = 0;
+                HIPCHK(c, hipMemcpy(&dn, (uint64_t*)c->part_dedup.p + nb, 8, hipMemcpyDeviceToHost));
+                c->dedup_records += dn < dcap ? dn : dcap;
+            }
             c->skm_used = true;
             c->engines_used |= 1u;
             if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
@@ -1122,6 +1129,8 @@ kc_status kc_reset(kc_ctx* c) {
     c->rec_n = 0;
     c->batches = 0;
     for (double& x : c->part_ms) x = 0;
+    c->dedup_ms = 0;
+    c->dedup_records = 0;
     c->part_keys = 0;
     c->p5_launches = 0;
     c->skm_used = false;
@@ -1624,6 +1633,8 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     out->valid_kmers = c->stats_h[ST_VALID];
     out->spill_runs = c->runs.size();
     out->engines_used = c->engines_used;
+    out->dedup_ms = c->dedup_ms;
+    out->dedup_records = c->dedup_records;
     return KC_OK;
 }
 
