@@ -731,41 +731,15 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             c->part_ms[3] += t;
             const uint64_t kbound = nr * nw;
             const uint64_t rec_batch0 = c->rec_n;
-            // P5a (W = 1): each bucket's distinct records and multiplicities,
-            // written to the free tail of the pool arrays (counts into the
-            // digit bytes, free after S2); P5 walks those lists
+            // P5a (W = 1): each bucket's distinct records written back over
+            // the front of its range, multiplicities into the digit bytes
+            // (free after S2, read as u32 indexed like the pool); P5 walks them
             SkmDedup dd = {};
-            const bool dedup = W == 1 && !getenv("KC_NO_DEDUP") && pool_cap > np;
-            uint64_t dcap = 0;
+            const bool dedup = W == 1 && !getenv("KC_NO_DEDUP") && np <= c->digs_bytes / 4;
             if (dedup) {
-                if ((s = ensure(c, c->part_dedup, ((size_t)nb + 1) * 12 + 64))) return s;
-                uint64_t* dstart = (uint64_t*)c->part_dedup.p;
-                uint32_t* dlen = (uint32_t*)(dstart + nb + 1);
-                HIPCHK(c, hipMemsetAsync(dstart + nb, 0, 8, c->stream));  // list cursor
-                dcap = pool_cap - np;
-                if (dcap > c->digs_bytes / 4) dcap = c->digs_bytes / 4;
-                if (const char* e = getenv("KC_P5A_CAP")) {  // tests: lists past this many records are walked raw
-                    const uint64_t v = strtoull(e, nullptr, 10);
-                    if (v < dcap) dcap = v;
-                }
-                dd.recs = c->keys_a + np;
-                dd.stride = pool_cap;
+                if ((s = ensure(c, c->part_dedup, ((size_t)nb + 1) * 4 + 64))) return s;
                 dd.cnt = (const uint32_t*)c->digs;
-                dd.start = dstart;
-                dd.len = dlen;
-            }
-            if (getenv("KC_DEBUG")) {
-                std::vector<uint64_t> st((size_t)nb + 1);
-                HIPCHK(c, hipMemcpy(st.data(), c->part_starts.p, st.size() * 8, hipMemcpyDeviceToHost));
-                uint64_t mx = 0, mb = 0;
-                for (uint32_t b = 0; b + 1 < nb; b++)
-                    if (st[b + 1] - st[b] > mx) {
-                        mx = st[b + 1] - st[b];
-                        mb = b;
-                    }
-                fprintf(stderr, "kc: skm buckets: mean %.0f records, max %llu (bucket %llu), padding %llu\n",
-                        (double)st[nb - 1] / (nb - 1), (unsigned long long)mx, (unsigned long long)mb,
-                        (unsigned long long)(st[nb] - st[nb - 1]));
+                dd.len = (const uint32_t*)c->part_dedup.p;
             }
             // P5 over buckets [b0, b1); reruns with a bigger record buffer on
             // overflow (safe while nothing went to the global table or spill)
@@ -776,21 +750,13 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
                 kc_status s2;
                 if (dedup) {
-                    uint64_t* dstart = (uint64_t*)c->part_dedup.p;
                     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                     HIPCHK(c, launch_count_rec(c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, b0, b1,
-                                               c->keys_a + np, pool_cap, (uint32_t*)c->digs, dcap, dstart + nb,
-                                               dstart, (uint32_t*)(dstart + nb + 1), c->n_cu, c->stream));
+                                               (uint32_t*)c->digs, (uint32_t*)c->part_dedup.p, c->n_cu, c->stream));
                     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                     HIPCHK(c, hipEventSynchronize(c->ev1));
                     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
                     c->dedup_ms += t;
-                    if (getenv("KC_DEBUG")) {
-                        uint64_t dn = 0;
-                        HIPCHK(c, hipMemcpy(&dn, dstart + nb, 8, hipMemcpyDeviceToHost));
-                        fprintf(stderr, "kc: skm P5a[%u,%u) distinct records so far %llu of %llu, %.3f ms\n", b0, b1,
-                                (unsigned long long)dn, (unsigned long long)np, t);
-                    }
                 }
                 for (;;) {
                     if ((s2 = grow_records(c, rec0 + bound))) return s2;
@@ -857,9 +823,9 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             }
             if ((s = p5_range(bs, nbk, false))) return s;
             if (dedup) {
-                uint64_t dn = 0;
-                HIPCHK(c, hipMemcpy(&dn, (uint64_t*)c->part_dedup.p + nb, 8, hipMemcpyDeviceToHost));
-                c->dedup_records += dn < dcap ? dn : dcap;
+                HIPCHK(c, launch_dedup_total((const uint32_t*)c->part_dedup.p, (const uint64_t*)c->part_starts.p, nbk,
+                                             c->stats, c->stream));
+                if ((s = sync_stats(c))) return s;
             }
             c->skm_used = true;
             c->engines_used |= 1u;
@@ -1634,7 +1600,7 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     out->spill_runs = c->runs.size();
     out->engines_used = c->engines_used;
     out->dedup_ms = c->dedup_ms;
-    out->dedup_records = c->dedup_records;
+    out->dedup_records = c->stats_h[ST_DEDUP];
     return KC_OK;
 }
 

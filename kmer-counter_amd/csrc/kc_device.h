@@ -21,6 +21,7 @@ enum Stat : int {
     ST_P5_MAXM = 10,     // largest sub-range split m used (diagnostic)
     ST_DESC_FILL = 11,   // P5 segment descriptors written (may exceed capacity)
     ST_P5_KEYS = 12,     // skm P5 sample launch: keys of the sampled buckets
+    ST_DEDUP = 13,       // skm P5a: distinct records listed (raw buckets: their records)
     ST_N = 16
 };
 
@@ -228,17 +229,17 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
                              uint8_t* emit, int eshift, int grid, hipStream_t s);
 int skm_lds_slots(int W);
 int seg_sort_cap(int W);  // longest segment seg_sort_k takes
-// P5a (W = 1): per bucket of [b0, b1), its distinct records (2 x ostride SoA
-// at a cursor position, at most ocap in all) with their multiplicities:
-// dstart[b], dlen[b] (kRawList 0xffffffff: not deduplicated)
-hipError_t launch_count_rec(const uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
-                            uint64_t* out, uint64_t ostride, uint32_t* ocnt, uint64_t ocap, uint64_t* ocursor,
-                            uint64_t* dstart, uint32_t* dlen, int grid, hipStream_t s);
+// P5a (W = 1): per bucket b of [b0, b1), its distinct records written back in
+// place at the front of its range of recs (2 x stride SoA), their
+// multiplicities at the same indices of cnt; dlen[b] = their number
+// (kRawList 0xffffffff: the table filled, records left as they were)
+hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
+                            uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s);
+// stats[ST_DEDUP] += sum over buckets [0, nb) of dlen[b] (raw: the bucket's records)
+hipError_t launch_dedup_total(const uint32_t* dlen, const uint64_t* starts, uint32_t nb, uint64_t* stats,
+                              hipStream_t s);
 struct SkmDedup {
-    const uint64_t* recs;  // P5a output
-    uint64_t stride;
-    const uint32_t* cnt;
-    const uint64_t* start;
+    const uint32_t* cnt;  // P5a output
     const uint32_t* len;
 };
 // buckets [b0, b1); count_keys: add the buckets' key counts to stats[ST_P5_KEYS];

@@ -1330,13 +1330,10 @@ struct SkmBucketArgs {
     u32 probe_limit;
     int skip;
     // deduplicated records (P5a, count_rec_k): bucket b's dlen[b] distinct
-    // records from index dstart[b] of drecs (RW x dstride SoA) with their
-    // multiplicities dcnt; drecs == nullptr or dlen[b] == kRawList: the
-    // bucket's own records from recs (multiplicity 1)
-    const u64* drecs;
-    u64 dstride;
+    // records at the front of its own range with their multiplicities dcnt
+    // (indexed like recs); dlen == nullptr or dlen[b] == kRawList: the
+    // bucket's own records (multiplicity 1)
     const u32* dcnt;
-    const u64* dstart;
     const u32* dlen;
 };
 
@@ -1544,12 +1541,12 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     u32 pfb = ~0u;
     // bucket bb's record source: deduplicated list or its own records
     auto source = [&](u32 bb, const u64** rp, u64* st, const u32** cp, u64* l0, u64* h0) {
-        const u32 dl = a.drecs ? a.dlen[bb] : kRawList;
+        const u32 dl = a.dlen ? a.dlen[bb] : kRawList;
         if (dl != kRawList) {
-            *rp = a.drecs;
-            *st = a.dstride;
+            *rp = a.recs;
+            *st = a.stride;
             *cp = a.dcnt;
-            *l0 = a.dstart[bb];
+            *l0 = a.starts[bb];
             *h0 = *l0 + dl;
         } else {
             *rp = a.recs;
@@ -1900,10 +1897,7 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
                             uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s,
                             const SkmDedup* dd) {
     SkmBucketArgs a;
-    a.drecs = dd ? dd->recs : nullptr;
-    a.dstride = dd ? dd->stride : 0;
     a.dcnt = dd ? dd->cnt : nullptr;
-    a.dstart = dd ? dd->start : nullptr;
     a.dlen = dd ? dd->len : nullptr;
     {
         const char* e = getenv("KC_P5_SKIP");
@@ -1948,27 +1942,27 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
 // go into an LDS table of whole records (both words; the bucket bits replaced
 // by a non-zero marker, the bucket is known) with a count per entry. Equal
 // records meet in one entry; a record whose claim races with a writer may
-// take a second entry, which only costs dedup, never a count. The distinct
-// records and their multiplicities are written as the bucket's list
-// (dstart[b], dlen[b]); P5 then walks each distinct record's keys once,
-// adding the multiplicity. A bucket whose table fills, or whose list does not
-// fit the output, is marked kRawList and P5 walks its own records.
+// take a second entry, which only costs dedup, never a count. Once every
+// record of the bucket is in the table, the distinct records overwrite the
+// front of the bucket's own range (in place, no allocation) and their
+// multiplicities go to cnt[] at the same indices; dlen[b] = their number. A
+// bucket whose table fills keeps its records (dlen[b] = kRawList) and P5
+// walks them with multiplicity 1.
 // ---------------------------------------------------------------------------
 
 constexpr int kRecProbe = 8;  // P5a: groups probed per record
+#ifndef KC_P5A_PD
+#define KC_P5A_PD 4
+#endif
+constexpr int kRecPd = KC_P5A_PD;  // P5a: record batches in flight per wave
 
 struct RecDedupArgs {
-    const u64* recs;  // 2 x stride (SoA), grouped by bucket
+    u64* recs;  // 2 x stride (SoA), grouped by bucket; distinct records written back in place
     u64 stride;
     const u64* starts;
     u32 b0, nbuckets;
-    u32 ngrp;         // LDS groups of 2 entries
-    u64* out;         // distinct records: 2 x ostride (SoA)
-    u64 ostride;
-    u32* ocnt;
-    u64 ocap;
-    u64* ocursor;
-    u64* dstart;
+    u32 ngrp;  // LDS groups of 2 entries
+    u32* cnt;  // multiplicities, indexed like recs
     u32* dlen;
 };
 
@@ -1987,9 +1981,9 @@ u32 rec_dedup_groups() {
 
 __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    u64* tab = (u64*)smem;                         // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
-    u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);   // 2 ngrp
-    u32* misc = cnt + 2 * (size_t)a.ngrp;          // [0] overflow, [1..16] wave totals, [18..19] base
+    u64* tab = (u64*)smem;                        // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
+    u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);  // 2 ngrp
+    u32* misc = cnt + 2 * (size_t)a.ngrp;         // [0] overflow, [1..16] wave totals
     const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
     const u32 nent = 2 * a.ngrp;
     const u64 lt = lanemask_lt();
@@ -2002,24 +1996,42 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
     __syncthreads();
     constexpr u64 kMark = 0x8000ull << 48;  // replaces the bucket bits: a non-zero word 0
     constexpr u64 kLow48 = (1ull << 48) - 1ull;
-    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
-        const u64 lo = a.starts[b], hi = a.starts[b + 1];
+    // one record per lane, kRecPd batches in flight; a bucket's first batches
+    // are loaded while the previous bucket is written out
+    u64 n0[kRecPd], n1[kRecPd];
+    auto share = [&](u32 bb, u64* wlo, u64* whi) {
+        const u64 lo = a.starts[bb], hi = a.starts[bb + 1];
         const u64 nr = hi - lo, per_w = (nr + kBucketWaves - 1) / kBucketWaves;
-        const u64 wlo = lo + min(nr, (u64)wave * per_w), whi = lo + min(nr, (u64)(wave + 1) * per_w);
-        // one record per lane, the next batch in flight
-        u64 n0 = 0, n1 = 0;
-        if (wlo + lane < whi) {
-            n0 = a.recs[wlo + lane];
-            n1 = a.recs[a.stride + wlo + lane];
+        *wlo = lo + min(nr, (u64)wave * per_w);
+        *whi = lo + min(nr, (u64)(wave + 1) * per_w);
+    };
+    auto prefetch = [&](u32 bb) {
+        u64 wlo = 0, whi = 0;
+        if (bb < a.nbuckets) share(bb, &wlo, &whi);
+#pragma unroll
+        for (int d = 0; d < kRecPd; d++) {
+            const u64 i = wlo + (u64)d * 64 + lane;
+            n0[d] = i < whi ? __builtin_nontemporal_load(a.recs + i) : 0ull;
+            n1[d] = i < whi ? __builtin_nontemporal_load(a.recs + a.stride + i) : 0ull;
         }
+    };
+    prefetch(a.b0 + blockIdx.x);
+    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        u64 wlo, whi;
+        share(b, &wlo, &whi);
         bool over = false;
         for (u64 base = wlo; base < whi; base += 64) {
             const bool act = base + lane < whi;
-            const u64 k0 = (n0 & kLow48) | kMark, k1 = n1;
+            const u64 k0 = (n0[0] & kLow48) | kMark, k1 = n1[0];
+#pragma unroll
+            for (int d = 0; d + 1 < kRecPd; d++) {
+                n0[d] = n0[d + 1];
+                n1[d] = n1[d + 1];
+            }
             {
-                const u64 i = base + 64 + lane;
-                n0 = i < whi ? a.recs[i] : 0ull;
-                n1 = i < whi ? a.recs[a.stride + i] : 0ull;
+                const u64 i = base + (u64)kRecPd * 64 + lane;
+                n0[kRecPd - 1] = i < whi ? __builtin_nontemporal_load(a.recs + i) : 0ull;
+                n1[kRecPd - 1] = i < whi ? __builtin_nontemporal_load(a.recs + a.stride + i) : 0ull;
             }
             u32 g = __umulhi(rec_hash(k0, k1), a.ngrp);
             bool done = !act;
@@ -2052,8 +2064,10 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
         }
         if (__ballot(over) && lane == 0) atomicOr(&misc[0], 1u);
         __syncthreads();
+        // every record of the bucket is in the table: the next bucket's first
+        // batches go in flight, then the distinct records are written back
+        prefetch(b + gridDim.x);
         const bool raw = misc[0] != 0u;
-        // emission: distinct records of the bucket, contiguous from one base
         const u32 spw = (nent + kBucketWaves - 1) / kBucketWaves;
         const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
         u32 wc = 0;
@@ -2070,31 +2084,18 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
             before += w < wave ? v : 0u;
             total += v;
         }
-        if (tid == 0) {
-            u64 rb = 0;
-            bool fits = !raw;
-            if (fits && total) {
-                rb = atomicAdd((unsigned long long*)a.ocursor, (unsigned long long)total);
-                fits = rb + total <= a.ocap;
-            }
-            *(u64*)(misc + 18) = rb;
-            misc[0] = fits ? 0u : 1u;
-            a.dstart[b] = rb;
-            a.dlen[b] = fits ? total : kRawList;
-        }
-        __syncthreads();
-        const bool write = misc[0] == 0u;
-        u64 pos = *(u64*)(misc + 18) + before;
+        if (tid == 0) a.dlen[b] = raw ? kRawList : total;
+        u64 pos = a.starts[b] + before;
         for (u32 c0 = s0; c0 < s1; c0 += 64) {
             const u32 i = c0 + (u32)lane;
             const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
             const u64 bm = __ballot(occ);
             if (occ) {
-                if (write) {
+                if (!raw) {
                     const u64 q = pos + (u64)__popcll(bm & lt);
-                    a.out[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
-                    a.out[a.ostride + q] = tab[2 * (size_t)i + 1];
-                    a.ocnt[q] = cnt[i];
+                    a.recs[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
+                    a.recs[a.stride + q] = tab[2 * (size_t)i + 1];
+                    a.cnt[q] = cnt[i];
                 }
                 tab[2 * (size_t)i] = 0ull;
                 tab[2 * (size_t)i + 1] = 0ull;
@@ -2107,9 +2108,22 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
     }
 }
 
-hipError_t launch_count_rec(const uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
-                            uint64_t* out, uint64_t ostride, uint32_t* ocnt, uint64_t ocap, uint64_t* ocursor,
-                            uint64_t* dstart, uint32_t* dlen, int grid, hipStream_t s) {
+__global__ __launch_bounds__(kBlock) void dedup_total_k(const u32* __restrict__ dlen, const u64* __restrict__ starts,
+                                                       u32 nb, u64* stats) {
+    u64 v = 0;
+    for (u32 b = blockIdx.x * kBlock + threadIdx.x; b < nb; b += gridDim.x * kBlock)
+        v += dlen[b] == kRawList ? starts[b + 1] - starts[b] : (u64)dlen[b];
+    wave_add(&stats[ST_DEDUP], v);
+}
+
+hipError_t launch_dedup_total(const uint32_t* dlen, const uint64_t* starts, uint32_t nb, uint64_t* stats,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(dedup_total_k, dim3(64), dim3(kBlock), 0, s, dlen, starts, nb, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
+                            uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s) {
     if (b1 <= b0) return hipSuccess;
     RecDedupArgs a;
     a.recs = recs;
@@ -2122,12 +2136,7 @@ hipError_t launch_count_rec(const uint64_t* recs, uint64_t stride, const uint64_
         const long v = atol(e);
         if (v > 0 && (u32)v < a.ngrp) a.ngrp = (u32)v;
     }
-    a.out = out;
-    a.ostride = ostride;
-    a.ocnt = ocnt;
-    a.ocap = ocap;
-    a.ocursor = ocursor;
-    a.dstart = dstart;
+    a.cnt = cnt;
     a.dlen = dlen;
     const size_t lds = (rec_dedup_lds(a.ngrp) + 15) & ~(size_t)15;
     hipLaunchKernelGGL(count_rec_k, dim3(grid), dim3(kBucketBlock), lds, s, a);
