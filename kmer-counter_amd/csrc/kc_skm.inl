@@ -1461,11 +1461,12 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
             }
         }
     }
+    // lfill counts the pass's claimed slots (= its records at the emission)
     const u64 lm = __ballot(lclaim);
     const u64 fm = __ballot(full);
-    if (!last && (lm || fm) && lane == 0) {
+    if ((lm || fm) && lane == 0) {
         u32 f = atomicAdd(t.lfill, (u32)__popcll(lm)) + (u32)__popcll(lm);
-        if (fm || f > limit) atomicOr(t.labort, 1u);
+        if (!last && (fm || f > limit)) atomicOr(t.labort, 1u);
     }
     if (last) {
         u64 cm = __ballot(claimed);
@@ -1493,8 +1494,12 @@ __device__ __forceinline__ void skm_drain(const SkmBucketArgs& a, SkmLdsTable t,
     }
 }
 
+// starts_r / dlen_r: a.starts / a.dlen as read-only kernel arguments, so the
+// per-bucket ranges are scalar loads (lgkmcnt), which never wait behind the
+// vector loads of records in flight (in-order vmcnt)
 template <int W>
-__global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
+__global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, const u64* __restrict__ starts_r,
+                                                           const u32* __restrict__ dlen_r) {
     constexpr int RW = W + 1;
     constexpr int PD = 2;  // record batches in flight
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1541,19 +1546,19 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
     u32 pfb = ~0u;
     // bucket bb's record source: deduplicated list or its own records
     auto source = [&](u32 bb, const u64** rp, u64* st, const u32** cp, u64* l0, u64* h0) {
-        const u32 dl = a.dlen ? a.dlen[bb] : kRawList;
+        const u32 dl = dlen_r ? dlen_r[bb] : kRawList;
         if (dl != kRawList) {
             *rp = a.recs;
             *st = a.stride;
             *cp = a.dcnt;
-            *l0 = a.starts[bb];
+            *l0 = starts_r[bb];
             *h0 = *l0 + dl;
         } else {
             *rp = a.recs;
             *st = a.stride;
             *cp = nullptr;
-            *l0 = a.starts[bb];
-            *h0 = a.starts[bb + 1];
+            *l0 = starts_r[bb];
+            *h0 = starts_r[bb + 1];
         }
     };
     auto prefetch_pass = [&](u32 bb) {
@@ -1572,15 +1577,26 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
         }
         pfb = bb;
     };
-    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
-        if (tid == 0)
-            *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) &
-                           ERR_REC_OVERFLOW);
-        __syncthreads();
-        const bool stop = *lnext != 0u;
-        __syncthreads();
-        if (stop) return;
+    // the record-overflow flag, read one bucket ahead (its latency hidden by
+    // the bucket's work; a late stop only costs records the host rewrites)
+    if (a.skip & 8) return;  // timing experiments: launch only
+    // A global load waits for every older load of its wave (in-order vmcnt),
+    // so nothing here waits on a global value while the next bucket's records
+    // are in flight: the record-overflow flag (an early stop only saves work;
+    // records past rec_cap are never written and the host reruns) is read
+    // every 64 buckets, and the output range is reserved before the prefetch.
+    u32 nb_done = 0;
+    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x, nb_done++) {
+        if ((nb_done & 63u) == 0u) {
+            if (tid == 0)
+                *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) &
+                               ERR_REC_OVERFLOW);
+            __syncthreads();
+            const bool stop = *lnext != 0u;
+            __syncthreads();
+            if (stop) return;
+        }
         const u64* brecs;
         u64 bstride, lo, hi;
         const u32* bcnt;
@@ -1793,9 +1809,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 }
                 }
             }
-            // next bucket's first batches in flight during the drain, the abort
-            // check and the emission (unless another pass of this bucket follows)
-            if (sub + 1 >= m && b + gridDim.x < a.nbuckets) prefetch_pass(b + gridDim.x);
+            // the next bucket's first batches go in flight during the emission
+            // (unless another pass of this bucket follows)
+            const bool pf_next = sub + 1 >= m && b + gridDim.x < a.nbuckets;
             if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 skm_drain<W>(a, tab, wq, wqw, qn, brecs, bstride, lo, last, limit);
             __syncthreads();
@@ -1841,6 +1857,19 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                 const u32 spw = (a.lcap + kBucketWaves - 1) / kBucketWaves;
                 const u32 s0 = (u32)wave * spw;
                 const u32 s1 = min(a.lcap, s0 + spw);
+                // the pass's records = its claimed slots: the output range is
+                // reserved now, its latency hidden by the waves' slot counts
+                if (a.skip & 16) {  // timing experiments: no emission
+                    if (pf_next) prefetch_pass(b + gridDim.x);
+                    __syncthreads();
+                    ++sub;
+                    continue;
+                }
+                u64 rbase = 0;
+                const u32 nclaimed = *lfill;
+                if (tid == 0 && nclaimed)
+                    rbase = atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)nclaimed);
+                if (pf_next) prefetch_pass(b + gridDim.x);
                 u32 wc = 0;
                 for (u32 c0 = s0; c0 < s1; c0 += 64) {
                     const u32 i = c0 + (u32)lane;
@@ -1856,9 +1885,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a) {
                     total += v;
                 }
                 if (tid == 0) {
-                    u64 rbase = total ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)total) : 0ull;
                     *(u64*)(misc + 16) = rbase;
-                    if (rbase + total > a.rec_cap)
+                    if (rbase + total > a.rec_cap || total != nclaimed)
                         atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
                     *lfill = 0;
                     atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
@@ -1925,9 +1953,9 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
     a.probe_limit = probe_limit;
     const size_t lds = (skm_bucket_lds_bytes(W) + 15) & ~(size_t)15;
     switch (W) {
-    case 1: hipLaunchKernelGGL(count_skm_k<1>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
-    case 2: hipLaunchKernelGGL(count_skm_k<2>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
-    case 3: hipLaunchKernelGGL(count_skm_k<3>, dim3(grid), dim3(kBucketBlock), lds, s, a); break;
+    case 1: hipLaunchKernelGGL(count_skm_k<1>, dim3(grid), dim3(kBucketBlock), lds, s, a, a.starts, a.dlen); break;
+    case 2: hipLaunchKernelGGL(count_skm_k<2>, dim3(grid), dim3(kBucketBlock), lds, s, a, a.starts, a.dlen); break;
+    case 3: hipLaunchKernelGGL(count_skm_k<3>, dim3(grid), dim3(kBucketBlock), lds, s, a, a.starts, a.dlen); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
