@@ -528,13 +528,14 @@ struct F2Args {
     const unsigned short* inval;  //   not-ACGT masks, G u16 per read
     u64 n_reads, ntiles;
     int G, nw, nchr, R, NG, NI, HSK;
-    u32 o_inval, o_hm, o_rflag, o_sa, o_ea, wbytes;  // a wave's LDS region (bytes)
+    u32 o_inval, o_hm, o_rflag, o_sa, o_ea, o_bk, wbytes;  // a wave's LDS region (bytes)
     u64 chunk;  // pool records per wave allocation (>= records of one tile)
     u64* pool;
     u64 pool_cap;
     u64* pool_cursor;
     unsigned char* dig1;
     u64* stats;
+    int skip;  // timing experiments only (KC_F_SKIP): 1 record stores, 2 runs + records, 4 window minima, 8 hashes
 };
 
 constexpr int kF2Pf = 2;  // F2: code words prefetched per lane
@@ -593,8 +594,9 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
     u32* inval = (u32*)(wb + a.o_inval);
     u32* hm = (u32*)(wb + a.o_hm);
     u32* rflag = (u32*)(wb + a.o_rflag);
-    u32* sa = (u32*)(wb + a.o_sa);
-    unsigned short* ea = (unsigned short*)(wb + a.o_ea);
+    unsigned short* sa = (unsigned short*)(wb + a.o_sa);  // run starts (tile window index)
+    unsigned short* ea = (unsigned short*)(wb + a.o_ea);  // run ends
+    unsigned short* wbk = (unsigned short*)(wb + a.o_bk);  // window buckets, 8 per lane (chunk)
     const int G = a.G, NG = a.NG, R = a.R, nw = a.nw, nchr = a.nchr, NI = a.NI, HSK = a.HSK;
     const int RG = R * G;
     const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
@@ -612,9 +614,20 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         pr[j] = (int)div_g.div((u32)it);
         pg[j] = it - pr[j] * G;
     }
+    int po[kF2Pf];  // LDS word of each prefetched code word
+#pragma unroll
+    for (int j = 0; j < kF2Pf; j++) po[j] = pr[j] * NG + pg[j];
     const int hr0 = (int)div_ni.div((u32)lane), hq0 = lane - hr0 * NI;  // first hash item
     const int cr_ = lane / nchr, cc = lane - (lane / nchr) * nchr;     // chunk: read, chunk of the read
     const int p0 = 8 * cc;
+    // per-lane constants of the chunk: its hash row, code rows, windows
+    const u32* hbase = hm + (cr_ < R ? cr_ : 0) * HSK + 9 * cc;
+    const u32* crw0 = codes + (cr_ < R ? cr_ : 0) * NG;
+    const u32* irw0 = inval + (cr_ < R ? cr_ : 0) * NG;
+    const u32 act = (u32)max(0, min(8, nw - p0));
+    const u32 actm = (1u << act) - 1u;  // the chunk's windows inside the read
+    const u32 q0 = (u32)(cr_ * nw + p0);
+    const bool first_chunk = cc == 0, last_chunk = cc == nchr - 1;
     u32 pfc[kF2Pf], pfi[kF2Pf];
     auto prefetch = [&](u64 tile) {
         const u64 r0 = tile * (u64)R;
@@ -651,8 +664,8 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
 #pragma unroll
         for (int j = 0; j < kF2Pf; j++)
             if (pr[j] < nr) {
-                codes[pr[j] * NG + pg[j]] = pfc[j];
-                inval[pr[j] * NG + pg[j]] = pfi[j];
+                codes[po[j]] = pfc[j];
+                inval[po[j]] = pfi[j];
                 const u32 f = flag_of(pfc[j], pfi[j], pg[j]);
                 if (f) atomicOr(&rflag[pr[j]], f);
             }
@@ -668,7 +681,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         wave_sync();
         prefetch(tile + nwaves);
         // 2. m-mer hashes, 16 positions per item
-        for (int it2 = lane; it2 < nr * NI; it2 += 64) {
+        for (int it2 = lane; it2 < ((a.skip & 8) ? 0 : nr * NI); it2 += 64) {
             int hr = hr0, hq = hq0;
             if (it2 != lane) {
                 hr = (int)div_ni.div((u32)it2);
@@ -691,13 +704,14 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         const bool live_lane = lane < nr * nchr;
         u32 bk[8];
         {
-            const u32* hb = hm + (live_lane ? cr_ : 0) * HSK + 9 * cc;
+            const u32* hb = hbase;
             u32 h[WM + 7];
 #pragma unroll
             for (int j = 0; j < WM + 7; j++) h[j] = hb[j + (j >> 3)];
             u32 core = h[7];
+            if (!(a.skip & 4))
 #pragma unroll
-            for (int j = 8; j < WM; j++) core = min(core, h[j]);
+                for (int j = 8; j < WM; j++) core = min(core, h[j]);
             u32 lf[8];
             lf[7] = ~0u;
 #pragma unroll
@@ -710,18 +724,17 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
                 bk[i] = min(b, kNoKey - 1u);
             }
         }
-        u32 act = 0;
+        u32 livem = live_lane ? actm : 0u;  // windows that keep their bucket
         if (live_lane) {
             const u32 fl = rflag[cr_];
-            act = (u32)min(8, nw - p0);
             if (fl == 0u) {
                 my_valid += act;
             } else {
                 // invalid bases (flag 1): a window is dead when one of its K
                 // bases is not ACGT (not-ACGT bits of bases p0 .. p0 + 55 in
                 // one 64-bit word); a possible key 0^W (flag 2): rolling keys
-                const u32* crw = codes + cr_ * NG;
-                const u32* ir = inval + cr_ * NG;
+                const u32* crw = crw0;
+                const u32* ir = irw0;
                 u32 badm = 0;
                 if (fl & 1u) {
                     const int g0 = p0 >> 4;
@@ -750,14 +763,11 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
                         tl <<= 2;
                     }
                 }
-                const u32 actm = (1u << act) - 1u;
                 const u32 validm = actm & ~badm;
                 const u32 zeros = (u32)__popc(validm & zm);
                 my_hole |= (actm & badm) != 0u;
                 my_valid += (u32)__popc(validm);
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-                    if ((((validm & ~zm) >> i) & 1u) == 0u) bk[i] = kNoKey;
+                livem = validm & ~zm;
                 if (zeros) {
                     atomicAdd((unsigned long long*)&a.stats[ST_KEY0], (unsigned long long)zeros);
                     atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
@@ -766,12 +776,21 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         }
 #pragma unroll
         for (int i = 0; i < 8; i++)
-            if (!live_lane || i >= (int)act) bk[i] = kNoKey;
+            if (!((livem >> i) & 1u)) bk[i] = kNoKey;
+        // the chunk's buckets for the record stage (one 16-byte store)
+        {
+            v4u pk;
+            pk.x = bk[0] | (bk[1] << 16);
+            pk.y = bk[2] | (bk[3] << 16);
+            pk.z = bk[4] | (bk[5] << 16);
+            pk.w = bk[6] | (bk[7] << 16);
+            *(v4u*)(wbk + 8 * lane) = pk;
+        }
         // 4. run starts / ends; neighbouring chunks from the neighbouring lanes
         u32 prev = (u32)__shfl_up((int)bk[7], 1);
         u32 nxt = (u32)__shfl_down((int)bk[0], 1);
-        if (cc == 0) prev = kNoKey;
-        if (cc == nchr - 1) nxt = kNoKey;
+        if (first_chunk) prev = kNoKey;
+        if (last_chunk) nxt = kNoKey;
         u32 smask = 0, emask = 0;
         {
             u32 pv = prev;
@@ -790,23 +809,20 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         u32 T;
         const u32 ex = f2_scan16((u32)__popc(smask), &T);
         {
-            const u32 q0 = (u32)(cr_ * nw + p0);
+            // set bits only (a lane holds one or two starts and ends)
             u32 sp = ex, ep = ex - open;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                if ((smask >> i) & 1u) sa[sp++] = (q0 + (u32)i) | (bk[i] << 16);
-                if ((emask >> i) & 1u) ea[ep++] = (unsigned short)(q0 + (u32)i);
-            }
+            for (u32 mm = smask; mm; mm &= mm - 1u) sa[sp++] = (unsigned short)(q0 + (u32)__builtin_ctz(mm));
+            for (u32 mm = emask; mm; mm &= mm - 1u) ea[ep++] = (unsigned short)(q0 + (u32)__builtin_ctz(mm));
         }
         wave_sync();
+        if (a.skip & 2) continue;
         // 5. runs -> pieces of <= nmax windows -> records at consecutive
         // positions of the wave's pool chunk (one global atomic per chunk)
         for (u32 i0 = 0; i0 < T; i0 += 64) {
             const u32 i = i0 + (u32)lane;
-            u32 qs = 0, n = 0, sv = 0;
+            u32 qs = 0, n = 0;
             if (i < T) {
-                sv = sa[i];
-                qs = sv & 0xffffu;
+                qs = sa[i];
                 n = (u32)ea[i] - qs + 1u;
             }
             const u32 pieces = n <= NMAX ? (n ? 1u : 0u) : (n + NMAX - 1u) / NMAX;
@@ -834,16 +850,28 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
             if (n == 0) continue;
             const int r = (int)div_nw.div(qs);
             const int ps0 = (int)qs - r * nw;
-            const u64 bkt = sv >> 16;
+            const u64 bkt = wbk[r * 8 * nchr + ps0];
             const u32* crw = codes + r * NG;
             u32 g = pb;
             for (u32 off = 0; off < n; off += NMAX, g++) {
                 const u32 nn = min(NMAX, n - off);
                 const int ps = ps0 + (int)off;
                 u64 rec[RW];
-                rec[0] = (bkt << 48) | (f2_code_word(crw, ps) >> 16);
+                {
+                    // words g .. g + 2 RW of the row hold bases ps .. ps + 32 RW - 8 + 31
+                    const int g = ps >> 4, o = ps & 15;
+                    u32 cw[2 * RW + 1];
 #pragma unroll
-                for (int j = 1; j < RW; j++) rec[j] = f2_code_word(crw, ps + 32 * j - 8);
+                    for (int x = 0; x < 2 * RW + 1; x++) cw[x] = crw[g + x];
+                    u32 sw[2 * RW];  // the row shifted to base ps
+#pragma unroll
+                    for (int x = 0; x < 2 * RW; x++) sw[x] = o ? __builtin_amdgcn_alignbit(cw[x], cw[x + 1], 32 - 2 * o) : cw[x];
+                    // word 0: bucket, then bases ps ..; word j >= 1: bases ps + 32 j - 8 ..
+                    rec[0] = (bkt << 48) | ((((u64)sw[0] << 32) | sw[1]) >> 16);
+#pragma unroll
+                    for (int j = 1; j < RW; j++)
+                        rec[j] = ((((u64)sw[2 * j - 1] << 32) | sw[2 * j]) << 16) | (sw[2 * j + 1] >> 16);
+                }
                 const int vb = 16 + 2 * (C::KP + (int)nn - 1);
 #pragma unroll
                 for (int j = 0; j < RW; j++) {
@@ -853,7 +881,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
                 }
                 rec[RW - 1] |= (u64)nn;
                 const u64 dst = (u64)g < room ? oc + g : nbase + ((u64)g - room);
-                if (dst < a.pool_cap) {
+                if (dst < a.pool_cap && !(a.skip & 1)) {
 #pragma unroll
                     for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + dst] = rec[j];
                     if (a.dig1) a.dig1[dst] = (unsigned char)bkt;
@@ -890,7 +918,7 @@ static bool f2_args(const CountLaunch& l, const SkmGeom& g, F2Args* a, size_t* l
     a->NI = (8 * nchr + wm + 7 + 15) / 16;
     a->HSK = 18 * a->NI + 1;
     // code words: records read 3 words from (ps + 32 j - 8) / 16, hashes NI + 1
-    int ng = (8 * nchr + 32 * RW) / 16 + 4;
+    int ng = (8 * nchr + 32 * RW) / 16 + 2 * RW + 3;
     if (ng < a->NI + 2) ng = a->NI + 2;
     if (ng < a->G + 1) ng = a->G + 1;
     a->NG = ng;
@@ -902,10 +930,12 @@ static bool f2_args(const CountLaunch& l, const SkmGeom& g, F2Args* a, size_t* l
     a->o_rflag = (u32)p;
     p += 64 * 4;
     a->o_sa = (u32)p;
-    p += (size_t)a->R * nchr * 8 * 4;
+    p += (size_t)a->R * nchr * 8 * 2;
     a->o_ea = (u32)p;
     p += (size_t)a->R * nchr * 8 * 2;
     p = (p + 15) & ~(size_t)15;
+    a->o_bk = (u32)p;
+    p += 64 * 8 * 2;
     a->wbytes = (u32)p;
     *lds = p * (kSkmBlock / 64);
     if (*lds > 64 * 1024) return false;
@@ -997,6 +1027,10 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
             f2.pool_cursor = pool_cursor;
             f2.dig1 = dig1;
             f2.stats = l.stats;
+            {
+                const char* e = getenv("KC_F_SKIP");
+                f2.skip = e ? atoi(e) : 0;
+            }
             int per_cu = 0, n_cu = 0, dev = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
