@@ -35,3 +35,18 @@ def orc():
     import oracle
     oracle.lib()
     return oracle
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_gpu_first(request):
+    """PyTorch ships its own HIP runtime (libamdhip64 under torch/lib) next to
+    the system one libkc_hip.so links; in one process the GPU must be opened by
+    PyTorch first, or its later torch.cuda init fails. GPU sessions that will
+    mix the two (the key-space exchange tests) therefore open it up front."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+        except ImportError:
+            return
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda:0")
