@@ -220,10 +220,16 @@ def main():
         # the records, priced per batch)
         rec_step = st["keys"] or 1  # records handed out by F per step
         rb = 8 * (W + 1)
-        # F2 (skm_front2_k<1, k>) covers W = 1, 18 <= k <= 32 with at most 64
-        # 8-window chunks per read; the generic F otherwise
-        f2 = W == 1 and 18 <= k <= 32 and (L - k + 1 + 7) // 8 <= 64
-        fname = f"skm_front2_k<1,{k}>" if f2 else f"skm_front_k<{W}>"
+        # F3 (skm_front3_k<k>, a lane per read) covers W = 1, 19 <= k <= 32
+        # with rows of <= 40 KiB per wave; F2 (skm_front2_k<1, k>) W = 1,
+        # 18 <= k <= 32 with at most 64 8-window chunks per read; the generic F
+        # otherwise
+        nw = L - k + 1
+        ng = max((L + 15) // 16 + 1, (nw - 1) // 16 + 5) | 1
+        f3 = (W == 1 and 19 <= k <= 32 and (320 + 64) * 8 + 256 + 256 * ng <= 40 * 1024
+              and not os.environ.get("KC_NO_F3"))
+        f2 = W == 1 and 18 <= k <= 32 and (nw + 7) // 8 <= 64 and not os.environ.get("KC_NO_F2")
+        fname = f"skm_front3_k<{k}>" if f3 else (f"skm_front2_k<1,{k}>" if f2 else f"skm_front_k<{W}>")
         dd_step = st.get("dedup_records", 0)  # ctx stats are per step
         specs = [
             ("F", fname, part_ms[1], launches, windows_step, "k-mers",

@@ -83,7 +83,7 @@ __device__ __forceinline__ u64 hash_key(const u64 (&key)[W]) {
 // Block-wide exclusive scan of one u32 per thread (256 threads). `lds` holds
 // >= 4 u32. Returns the exclusive prefix; *total receives the block sum.
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* lds, u32* total) {
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     u32 x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1617,7 +1617,7 @@ constexpr int kBucketWaves = kBucketBlock / 64;
 template <int NT>
 __device__ __forceinline__ u32 block_excl_scan_n(u32 v, u32* lds, u32* total) {
     constexpr int NW = NT / 64;
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     u32 x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -3116,7 +3116,7 @@ __device__ __forceinline__ uint4 fq_load16(uintptr_t addr) {
 __global__ __launch_bounds__(kBlock) void fq_count_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                      u64* __restrict__ counts) {
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (u64 c = (u64)blockIdx.x * kFqWaves + wave; c < nchunks; c += (u64)gridDim.x * kFqWaves) {
         u32 cnt = 0;
 #pragma unroll 4
@@ -3148,7 +3148,7 @@ __global__ __launch_bounds__(kBlock) void fq_emit_k(const uint8_t* __restrict__ 
                                                     const u64* __restrict__ line_base, u64* __restrict__ seq_off,
                                                     u64* __restrict__ seq_end, u64 max_rec, u64* stats) {
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     u64 err = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (n == 0 || base[0] != '@') err |= ERR_FQ_NOT_AT;
@@ -3275,7 +3275,7 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                                                       unsigned short* __restrict__ inval, u64* stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const u64 lt = lanemask_lt();
     const size_t wbytes = (size_t)kFqStage + (((size_t)lcap * 2 + 15) & ~(size_t)15);
     unsigned char* txt = smem + (size_t)wave * wbytes;

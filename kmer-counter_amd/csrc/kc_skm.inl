@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
     const int HSK = skm_hsk(hch * hq);  // hash items cover hch * hq positions
     const FastDivU div_nchr((u32)nchr), div_hch((u32)hch), div_nw((u32)nw), div_g((u32)G);
     const SkmLds lay = skm_lds_layout(R, NG, hch * hq, nw);
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     unsigned char* wb = smem + (size_t)wave * lay.total;
     u32* codes = (u32*)(wb + lay.codes);
     u32* inval = (u32*)(wb + lay.inval);
@@ -227,8 +227,10 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         }
     };
     auto flag_of = [&](u32 cw, u32 iv, int g) -> u32 {
-        // aligned all-A halves of the read's groups (padding past L counts)
-        const bool za = g < G && ((cw & 0xffffu) == 0u || (cw >> 16) == 0u);
+        // aligned all-A halves inside the read (a key 0^W has >= k >= 18 A
+        // bases of the read in a row, so it holds one; halves with padding
+        // past L would flag every read whose L is not a multiple of 8)
+        const bool za = g < G && (((cw >> 16) == 0u && 16 * g + 8 <= a.L) || ((cw & 0xffffu) == 0u && 16 * g + 16 <= a.L));
         return (iv ? 1u : 0u) | (za ? 2u : 0u);
     };
     prefetch(wid);
@@ -588,7 +590,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
     constexpr int WM = C::WM;
     constexpr u32 NMAX = (u32)C::NMAX;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     unsigned char* wb = smem + (size_t)wave * a.wbytes;
     u32* codes = (u32*)wb;
     u32* inval = (u32*)(wb + a.o_inval);
@@ -598,6 +600,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
     unsigned short* ea = (unsigned short*)(wb + a.o_ea);  // run ends
     unsigned short* wbk = (unsigned short*)(wb + a.o_bk);  // window buckets, 8 per lane (chunk)
     const int G = a.G, NG = a.NG, R = a.R, nw = a.nw, nchr = a.nchr, NI = a.NI, HSK = a.HSK;
+    const int L = nw + K - 1;
     const int RG = R * G;
     const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
     const u64 nwaves = (u64)gridDim.x * (kSkmBlock / 64);
@@ -645,9 +648,10 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
         }
     };
     auto flag_of = [&](u32 cw, u32 iv, int g) -> u32 {
-        // non-ACGT bases; aligned all-A halves of the read's groups (padding
-        // past L counts): only such reads can hold a key 0^W
-        const bool za = g < G && ((cw & 0xffffu) == 0u || (cw >> 16) == 0u);
+        // non-ACGT bases; aligned all-A halves inside the read (a key 0^W
+        // has >= k A bases of the read in a row): only such reads can hold
+        // a key 0^W
+        const bool za = g < G && (((cw >> 16) == 0u && 16 * g + 8 <= L) || ((cw & 0xffffu) == 0u && 16 * g + 16 <= L));
         return (iv ? 1u : 0u) | (za ? 2u : 0u);
     };
     prefetch(wid);
@@ -901,6 +905,361 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F_
     if (__ballot(my_hole) && lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
 }
 
+// ---------------------------------------------------------------------------
+// F3: skm_front3_k<K> (W = 1, m = 11, 19 <= k <= 32). One lane per read: a
+// wave takes 64 reads (a tile) and all lanes walk their reads' m-mer
+// positions in lock-step, so a position, its window and every shift are
+// wave-uniform and the per-window work is a handful of VALU operations with
+// no cross-lane traffic:
+//   - positions come in blocks of B (16 for k - 10 >= 17, else 8) inside a
+//     code word pair: the B m-mer hashes, their prefix minima (one running
+//     register) and suffix minima (kept for the next two blocks)
+//   - a window of k - 10 m-mers ends in block b and starts in block b - 1 or
+//     b - 2 (B < k - 10 < 2B), so its minimum is min(suffix, prefix) or
+//     min3(suffix, whole block b - 1, prefix) (van Herk / Gil-Werman)
+//   - a lane whose bucket changes pushes the run that ended (start, end,
+//     bucket, read) to the wave's descriptor ring (ballot + mbcnt)
+//   - every 64 descriptors become records: one descriptor per lane, pieces of
+//     <= nmax windows, record words from the read's row of code words in LDS,
+//     consecutive lanes at consecutive pool slots (coalesced stores)
+// Reads with not-ACGT bases or aligned all-A halves (possible key 0) make the
+// tile take the per-window liveness checks of F2's slow path.
+// Same records as F2 (same runs, same pieces) up to their order in the pool.
+// ---------------------------------------------------------------------------
+template <int V>
+struct F3Tag {
+    static constexpr int value = V;
+};
+
+// f(F3Tag<I>{}) for I in [I0, N), unrolled by construction
+template <int I0, int N, typename F>
+__device__ __forceinline__ void f3_static_for(F&& f) {
+    if constexpr (I0 < N) {
+        f(F3Tag<I0>{});
+        f3_static_for<I0 + 1, N>(f);
+    }
+}
+
+template <int K>
+struct F3Cfg {
+    static constexpr int WM = K - 10;            // m-mers per window (m = 11)
+    static constexpr int B = WM >= 17 ? 16 : 8;  // positions per block
+    static constexpr int E = WM - 1;             // window span - 1
+    static constexpr int D = E - B;              // a block's windows that start two blocks back
+    static_assert(D >= 0 && D < B, "block geometry: B < k - 10 <= 2B");
+};
+
+constexpr int kF3Ring = 320;  // descriptors per wave (u64); a drain check every 4 windows keeps < 64 + 4 x 64
+
+struct F3Args {
+    const u32* codes;             // kernel E output, G u32 per read
+    const unsigned short* inval;  //   not-ACGT masks, G u16 per read
+    u64 n_reads, ntiles;
+    int G, nw, np, NG;  // np = L - 10 m-mer positions; NG: LDS row stride (words, odd)
+    u32 wbytes;         // a wave's LDS: ring, read flags, 64 rows
+    u64 chunk;
+    u64* pool;
+    u64 pool_cap;
+    u64* pool_cursor;
+    unsigned char* dig1;
+    u64* stats;
+    int skip;  // timing experiments only (KC_F_SKIP): 1 record stores, 2 runs + records
+};
+
+// 22-bit m-mer at base I of the 32 bases {c0, c1} (I constant after unrolling)
+__device__ __forceinline__ u32 f3_mmer(u32 c0, u32 c1, int I) {
+    return (I <= 5 ? (c0 >> (10 - 2 * I)) : __builtin_amdgcn_alignbit(c0, c1, 42 - 2 * I)) & 0x3fffffu;
+}
+
+// 64 not-ACGT bits from base b of a read (MSB = base b; bases < 0 none)
+__device__ __forceinline__ u64 f3_inv64(const unsigned short* __restrict__ iv, int G, int b) {
+    const int b0 = b < 0 ? 0 : b;
+    const int g = b0 >> 4, sh = b0 & 15;
+    u32 w[5];
+#pragma unroll
+    for (int t = 0; t < 5; t++) w[t] = g + t < G ? (u32)iv[g + t] : 0u;
+    u64 x = ((u64)w[0] << 48) | ((u64)w[1] << 32) | ((u64)w[2] << 16) | (u64)w[3];
+    if (sh) x = (x << sh) | ((u64)w[4] >> (16 - sh));
+    return b < 0 ? x >> (-b) : x;
+}
+
+template <int K>
+__global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
+    using C = F3Cfg<K>;
+    using C2 = F2Cfg<1, K>;
+    constexpr int B = C::B, E = C::E, D = C::D;
+    constexpr int RW = 2;
+    constexpr u32 NMAX = (u32)C2::NMAX;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    unsigned char* wb = smem + (size_t)wave * a.wbytes;
+    u64* ring = (u64*)wb;
+    u32* rflag = (u32*)(wb + kF3Ring * 8);
+    u32* codes = rflag + 64;
+    const int G = a.G, NG = a.NG, nw = a.nw, np = a.np;
+    const int L = np + 10;
+    const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
+    const u64 nwaves = (u64)gridDim.x * (kSkmBlock / 64);
+    for (int i = lane; i < 64 * NG; i += 64) codes[i] = 0;
+    const FastDivU div_g((u32)G);
+    const u32* crow = codes + lane * NG;
+    const u32 ltag = (u32)lane << 16;
+    u64 my_valid = 0, my_zero = 0;
+    bool my_hole = false;
+    u64 ccur = 0, cend = 0;  // the wave's pool chunk (wave-uniform)
+    u32 qn = 0;              // descriptors in the ring (wave-uniform)
+    // records of the first cnt descriptors (one per lane); the rest move down
+    auto drain = [&](u32 cnt) {
+        wave_sync();
+        const bool has = (u32)lane < cnt;
+        const u64 d = has ? ring[lane] : 0ull;
+        for (u32 i = cnt + (u32)lane; i < qn; i += 64) ring[i - cnt] = ring[i];
+        qn -= cnt;
+        if (a.skip & 8) return;  // timing experiments: descriptors only
+        const u32 lo = (u32)d, hi = (u32)(d >> 32);
+        const u32 s0 = lo >> 16;
+        const u64 bkt = lo & 0xffffu;
+        const u32 n = has ? (hi & 0xffffu) - s0 + 1u : 0u;
+        // pool slots: one piece per run unless a run is longer than nmax
+        u32 ptot, pb;
+        const bool multi = __builtin_amdgcn_ballot_w64(n > NMAX) != 0ull;
+        u32 pieces = has ? 1u : 0u;
+        if (!multi) {
+            pb = (u32)lane;  // the descriptors sit in lanes 0 .. cnt - 1
+            ptot = cnt;
+        } else {
+            pieces = (n + NMAX - 1u) / NMAX;
+            const u32 inc = wave_incl_scan(pieces);
+            pb = inc - pieces;
+            ptot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+        const u64 room = cend - ccur;
+        u64 b0 = ccur, b1 = 0;  // slot g: b0 + g below room, else b1 + g
+        if ((u64)ptot > room) {
+            u64 nb = 0;
+            if (lane == 0) nb = atomicAdd((unsigned long long*)a.pool_cursor, (unsigned long long)a.chunk);
+            nb = readlane64(nb, 0);
+            b1 = nb - room;
+            ccur = nb + ((u64)ptot - room);
+            cend = nb + a.chunk;
+        } else {
+            ccur += ptot;
+        }
+        const u32* crw = codes + (hi >> 16) * NG;
+        for (u32 p = 0; p < pieces; p++) {
+            const u32 off = p * NMAX;
+            const u32 nn = min(NMAX, n - off);
+            const int ps = (int)(s0 + off);
+            const int g = ps >> 4, o = ps & 15;
+            u32 cw[2 * RW + 1];
+#pragma unroll
+            for (int x = 0; x < 2 * RW + 1; x++) cw[x] = crw[g + x];
+            u32 sw[2 * RW];
+#pragma unroll
+            for (int x = 0; x < 2 * RW; x++) sw[x] = o ? __builtin_amdgcn_alignbit(cw[x], cw[x + 1], 32 - 2 * o) : cw[x];
+            u64 rec[RW];
+            rec[0] = (bkt << 48) | ((((u64)sw[0] << 32) | sw[1]) >> 16);
+#pragma unroll
+            for (int j = 1; j < RW; j++) rec[j] = ((((u64)sw[2 * j - 1] << 32) | sw[2 * j]) << 16) | (sw[2 * j + 1] >> 16);
+            // keep the 16 + 2 (K' + nn - 1) bits of the record
+            const int vb = 16 + 2 * (C2::KP + (int)nn - 1);
+#pragma unroll
+            for (int j = 0; j < RW; j++) {
+                const int bits = vb - 64 * j;
+                if (bits < 64) rec[j] &= bits <= 0 ? 0ull : (~0ull << (64 - bits));
+            }
+            rec[RW - 1] |= (u64)nn;
+            const u32 gq = pb + p;
+            const u64 dst = ((u64)gq < room ? b0 : b1) + gq;
+            if (dst < a.pool_cap && !(a.skip & 1)) {
+#pragma unroll
+                for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + dst] = rec[j];
+                if (a.dig1) a.dig1[dst] = (unsigned char)bkt;
+            }
+        }
+    };
+    // a run ended at window w - 1 in the lanes of `ended` (prev: its bucket,
+    // s: its first window); descriptor = read lane | last window, first
+    // window | bucket
+    auto push = [&](bool ended, u64 pm, int wlast, u32 s, u32 prev) {
+        if (ended) {
+            const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0u));
+            ring[qn + rank] = ((u64)(ltag | (u32)wlast) << 32) | ((s << 16) | prev);
+        }
+        qn += (u32)__popcll(pm);
+    };
+    wave_sync();
+    for (u64 tile = wid; tile < a.ntiles; tile += nwaves) {
+        const u64 r0 = tile * 64;
+        const int nr = (int)min((u64)64, a.n_reads - r0);
+        const u64 livem = nr >= 64 ? ~0ull : ((1ull << nr) - 1ull);
+        // 1. the tile's code words into the rows; read flags (not-ACGT bases,
+        // aligned all-A halves inside the read)
+        rflag[lane] = 0;
+        wave_sync();
+        {
+            const u64 base = r0 * (u64)G;
+            const int nwords = nr * G;
+            for (int it0 = 0; it0 < nwords; it0 += 4 * 64) {
+                u32 cw[4], iv[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int it = it0 + 64 * j + lane;
+                    cw[j] = 0;
+                    iv[j] = 0;
+                    if (it < nwords) {
+                        cw[j] = __builtin_nontemporal_load(a.codes + base + (u64)it);
+                        iv[j] = __builtin_nontemporal_load(a.inval + base + (u64)it);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int it = it0 + 64 * j + lane;
+                    if (it < nwords) {
+                        const int r = (int)div_g.div((u32)it), g = it - r * G;
+                        codes[r * NG + g] = cw[j];
+                        const bool za = ((cw[j] >> 16) == 0u && 16 * g + 8 <= L) || ((cw[j] & 0xffffu) == 0u && 16 * g + 16 <= L);
+                        const u32 f = (iv[j] ? 1u : 0u) | (za ? 2u : 0u);
+                        if (f) atomicOr(&rflag[r], f);
+                    }
+                }
+            }
+        }
+        wave_sync();
+        const u32 fl = lane < nr ? rflag[lane] : 0u;
+        const int slow = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(fl != 0u) != 0ull ? 1 : 0);  // uniform
+        const unsigned short* ivg = a.inval + (r0 + (u64)(lane < nr ? lane : 0)) * (u64)G;
+        // 2. lock-step walk over the positions
+        u32 Sp[B];                 // suffix minima of the previous block
+        u32 St[D > 0 ? D : 1];     // ... of the block before it, last D
+        u32 prev = kNoKey, s = 0;  // the open run: bucket, first window
+        u32 xcnt = 0;
+#pragma unroll
+        for (int i = 0; i < B; i++) Sp[i] = ~0u;
+#pragma unroll
+        for (int i = 0; i < (D > 0 ? D : 1); i++) St[i] = ~0u;
+        u32 c0 = crow[0];
+        for (int g = 0; 16 * g < ((a.skip & 4) ? 0 : np); g++) {
+            const u32 c1 = crow[g + 1];
+            auto block = [&](auto tag) {
+                constexpr int OFF = decltype(tag)::value;
+                const int p0 = 16 * g + OFF;
+                if (p0 >= np) return;
+                u32 h[B];
+#pragma unroll
+                for (int i = 0; i < B; i++) h[i] = mul_u24(f3_mmer(c0, c1, OFF + i) ^ 0xd1e995u, 0x9e3779u);
+                u32 deadm = 0;
+                if (slow && (fl & 1u)) {
+                    const u64 X = f3_inv64(ivg, G, p0 - E);
+                    constexpr u64 KM = ~0ull << (64 - K);  // a window's K bases
+#pragma unroll
+                    for (int j = 0; j < B; j++) deadm |= ((X & (KM >> j)) ? 1u : 0u) << j;
+                }
+                u32 P = h[0];
+                f3_static_for<0, B>([&](auto jt) {
+                    constexpr int j = decltype(jt)::value;
+                    if constexpr (j > 0) P = min(P, h[j]);
+                    const int w = p0 + j - E;
+                    if (w >= 0 && w < nw) {  // wave-uniform
+                        u32 v;
+                        if constexpr (j < D)
+                            v = min(min(St[j], Sp[0]), P);
+                        else
+                            v = min(Sp[j - D], P);
+                        u32 u = min(v & 0xffffu, kNoKey - 1u);
+                        if (slow) {
+                            const bool dead = (deadm >> j) & 1u;
+                            bool zero = false;
+                            if ((fl & 2u) && !dead) zero = (f2_code_word(crow, w) & C2::LAST_MASK) == 0ull;
+                            if (lane < nr) {
+                                my_valid += dead ? 0u : 1u;
+                                my_zero += zero ? 1u : 0u;
+                                my_hole |= dead;
+                            }
+                            if (dead || zero) u = kNoKey;
+                        }
+                        if (w == 0) {
+                            s = 0;
+                        } else if (!(a.skip & 2)) {
+                            if (!slow && (a.skip & 16)) {
+                                // timing experiment: a per-lane append instead of the wave ring
+                                const bool bnd = u != prev;
+                                ring[lane * 4 + (xcnt & 3u)] = ((u64)(ltag | (u32)(w - 1)) << 32) | ((s << 16) | prev);
+                                xcnt += (bnd && lane < nr) ? 1u : 0u;
+                                if (bnd) s = (u32)w;
+                            } else if (!slow) {
+                                const bool bnd = u != prev;
+                                push(bnd && lane < nr, __builtin_amdgcn_ballot_w64(bnd) & livem, w - 1, s, prev);
+                                if (bnd) s = (u32)w;
+                            } else {
+                                const bool ended = u != prev && lane < nr && prev != kNoKey;
+                                const u64 pm = __builtin_amdgcn_ballot_w64(ended);
+                                push(ended, pm, w - 1, s, prev);
+                                if (u != prev) s = (u32)w;
+                            }
+                        }
+                        prev = u;
+                    }
+                    if constexpr ((j & 3) == 3)
+                        while (qn >= 64u) drain(64u);
+                });
+#pragma unroll
+                for (int x = 0; x < D; x++) St[x] = Sp[B - D + x];
+                Sp[B - 1] = h[B - 1];
+#pragma unroll
+                for (int i = B - 2; i >= 0; i--) Sp[i] = min(h[i], Sp[i + 1]);
+            };
+            block(F3Tag<0>{});
+            if constexpr (B == 8) block(F3Tag<8>{});
+            c0 = c1;
+        }
+        // the open runs end at the last window
+        {
+            const bool ended = prev != kNoKey && lane < nr && !(a.skip & 2);
+            push(ended, __builtin_amdgcn_ballot_w64(ended), nw - 1, s, prev);
+        }
+        while (qn) drain(min(64u, qn));
+        if (!slow && lane < nr) my_valid += (u64)nw + (xcnt & 0x80000000u);
+        wave_sync();
+    }
+    // pad the rest of the wave's chunk with n = 0 records in bucket kNoKey
+    for (u64 i = ccur + (u64)lane; i < cend; i += 64)
+        if (i < a.pool_cap) {
+#pragma unroll
+            for (int j = 0; j < RW; j++) a.pool[(u64)j * a.pool_cap + i] = j == 0 ? ((u64)kNoKey << 48) : 0ull;
+            if (a.dig1) a.dig1[i] = (unsigned char)kNoKey;
+        }
+    wave_add(&a.stats[ST_VALID], my_valid);
+    const u64 zsum = my_zero;
+    if (__builtin_amdgcn_ballot_w64(zsum != 0ull)) {
+        wave_add(&a.stats[ST_KEY0], zsum);
+        if (lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+    }
+    if (__builtin_amdgcn_ballot_w64(my_hole) && lane == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
+}
+
+// F3 geometry: false when F3 does not apply
+static bool f3_args(const CountLaunch& l, const SkmGeom& g, F3Args* a, size_t* lds) {
+    const int W = (l.k + 31) / 32;
+    if (W != 1 || g.m != 11 || l.k < 19 || l.k > 32 || getenv("KC_NO_F3")) return false;
+    const int nw = l.L - l.k + 1;
+    if (nw <= 0 || nw > 65535) return false;
+    a->G = groups_per_read(l.L);
+    a->nw = nw;
+    a->np = l.L - 10;
+    // rows: hash pairs read words g, g + 1 (g <= (np - 1) / 16), records
+    // words (ps >> 4) .. + 2 RW (ps < nw), zero tests + 2
+    int ng = a->G + 1;
+    if (ng < (nw - 1) / 16 + 5) ng = (nw - 1) / 16 + 5;
+    ng |= 1;  // odd stride: a lane per row, no bank conflicts
+    a->NG = ng;
+    const size_t wbytes = (size_t)kF3Ring * 8 + 64 * 4 + (size_t)64 * ng * 4;
+    if (wbytes > 40 * 1024) return false;
+    a->wbytes = (u32)wbytes;
+    *lds = (size_t)(kSkmBlock / 64) * wbytes;
+    return true;
+}
+
 // F2 geometry for (L, k) (W = 1, m = 11): false when F2 does not apply
 static bool f2_args(const CountLaunch& l, const SkmGeom& g, F2Args* a, size_t* lds) {
     const int W = (l.k + 31) / 32;
@@ -1013,6 +1372,48 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
         a.skip = e ? atoi(e) : 0;
     }
     {
+        F3Args f3;
+        size_t f3lds = 0;
+        if (f3_args(l, g, &f3, &f3lds)) {
+            f3.codes = l.codes;
+            f3.inval = (const unsigned short*)l.inval;
+            f3.n_reads = l.n_reads;
+            f3.ntiles = (l.n_reads + 63) / 64;
+            // a drain's pieces: 64 runs of <= nw windows, nmax per piece
+            f3.chunk = 64 * (u64)((f3.nw + g.nmax - 1) / g.nmax);
+            if (f3.chunk < 1024) f3.chunk = 1024;
+            f3.pool = pool;
+            f3.pool_cap = pool_cap;
+            f3.pool_cursor = pool_cursor;
+            f3.dig1 = dig1;
+            f3.stats = l.stats;
+            {
+                const char* e = getenv("KC_F_SKIP");
+                f3.skip = e ? atoi(e) : 0;
+            }
+            int per_cu = 0, n_cu = 0, dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+            const u64 nwg = (f3.ntiles + kSkmBlock / 64 - 1) / (kSkmBlock / 64);
+#define KC_F3(KK)                                                                                               \
+    case KK:                                                                                                    \
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, skm_front3_k<KK>, kSkmBlock, f3lds);       \
+        {                                                                                                       \
+            u64 cap = (per_cu > 0 && n_cu > 0) ? (u64)per_cu * (u64)n_cu : (u64)grid_cap;                      \
+            if (cap > (u64)grid_cap) cap = (u64)grid_cap;                                                       \
+            hipLaunchKernelGGL((skm_front3_k<KK>), dim3((int)hmin(nwg, cap)), dim3(kSkmBlock), f3lds, s, f3);    \
+        }                                                                                                       \
+        break;
+            switch (l.k) {
+                KC_F3(19) KC_F3(20) KC_F3(21) KC_F3(22) KC_F3(23) KC_F3(24) KC_F3(25) KC_F3(26)
+                KC_F3(27) KC_F3(28) KC_F3(29) KC_F3(30) KC_F3(31) KC_F3(32)
+            default: return hipErrorInvalidValue;
+            }
+#undef KC_F3
+            return hipGetLastError();
+        }
+    }
+    {
         F2Args f2;
         size_t f2lds = 0;
         if (f2_args(l, g, &f2, &f2lds)) {
@@ -1085,17 +1486,25 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
 // needed (records, and the keys of one group are distinct or summed later).
 // ---------------------------------------------------------------------------
 
+// radix-scatter LDS budget per workgroup (items) and workgroups per CU
+#ifndef KC_RP_LDS
+#define KC_RP_LDS 143808
+#endif
+#ifndef KC_RP_WPC
+#define KC_RP_WPC 1
+#endif
+
 template <int NW, bool PAY>
 struct RpCfg {
     static constexpr int BYTES = 8 * NW + (PAY ? 4 : 0);
-    static constexpr int K0 = 143808 / (BYTES * kP3Block);
+    static constexpr int K0 = KC_RP_LDS / (BYTES * kP3Block);
     static constexpr int KPT = K0 > 16 ? 16 : K0;
     static constexpr int TILE = kP3Block * KPT;
 };
 
 int rp_tile(int NW, bool pay) {
     const int bytes = 8 * NW + (pay ? 4 : 0);
-    int kpt = 143808 / (bytes * kP3Block);
+    int kpt = KC_RP_LDS / (bytes * kP3Block);
     if (kpt > 16) kpt = 16;
     return kP3Block * kpt;
 }
@@ -1307,7 +1716,7 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
     // one persistent workgroup per CU (the LDS tile allows no second one): a
     // larger grid would run as two rounds of workgroups, each restarting its
     // prefetch pipeline
-    const int g = (int)hmin(ntiles, (u64)(grid / 2 > 0 ? grid / 2 : 1));
+    const int g = (int)hmin(ntiles, (u64)(grid / 2 > 0 ? KC_RP_WPC * grid / 2 : 1));
     const size_t lds = (rp_scatter_lds(NW, pay) + 15) & ~(size_t)15;
 #define KC_RPS(NWV, PAYV)                                                                                          \
     hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kP3Block), lds, s, kin, istride, kout, ostride, pin, \
