@@ -949,7 +949,10 @@ struct F3Cfg {
     static_assert(D >= 0 && D < B, "block geometry: B < k - 10 <= 2B");
 };
 
-constexpr int kF3Ring = 320;  // descriptors per wave (u64); a drain check every 4 windows keeps < 64 + 4 x 64
+#ifndef KC_F3_WPE
+#define KC_F3_WPE 4  // F3: waves per SIMD the register budget is sized for
+#endif
+constexpr int kF3Ring = 384;  // per wave (u64): < 64 + 4 x 64 descriptors between drain checks, then a spare slot per lane
 
 struct F3Args {
     const u32* codes;             // kernel E output, G u32 per read
@@ -984,7 +987,7 @@ __device__ __forceinline__ u64 f3_inv64(const unsigned short* __restrict__ iv, i
 }
 
 template <int K>
-__global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
+__global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3_WPE, 8))) void skm_front3_k(F3Args a) {
     using C = F3Cfg<K>;
     using C2 = F2Cfg<1, K>;
     constexpr int B = C::B, E = C::E, D = C::D;
@@ -995,7 +998,8 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
     unsigned char* wb = smem + (size_t)wave * a.wbytes;
     u64* ring = (u64*)wb;
     u32* rflag = (u32*)(wb + kF3Ring * 8);
-    u32* codes = rflag + 64;
+    u32* codes = rflag + 64;                 // 64 rows x NG words
+    u32* stage = codes + 64 * a.NG;          // next tile: 64 G code words, then 32 G mask dwords (u16 pairs)
     const int G = a.G, NG = a.NG, nw = a.nw, np = a.np;
     const int L = np + 10;
     const u64 wid = (u64)blockIdx.x * (kSkmBlock / 64) + wave;
@@ -1088,44 +1092,48 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
         }
         qn += (u32)__popcll(pm);
     };
+    // a tile's code words and masks into the staging area by LDS DMA (no
+    // registers held while in flight); lanes past the tile load its first word
+    const int ngw = 64 * G, nmw = 32 * G;  // staged dwords: codes, masks
+    auto prefetch = [&](u64 t) {
+        if (t >= a.ntiles) return;
+        const int nwords = (int)min((u64)64, a.n_reads - t * 64) * G;
+        const u32* cg = a.codes + t * 64 * (u64)G;
+        for (int j = 0; j < ngw; j += 64) {
+            const int it = j + lane < nwords ? j + lane : 0;
+            __builtin_amdgcn_global_load_lds((const void*)(cg + it), (__attribute__((address_space(3))) void*)(stage + j), 4, 0, 0);
+        }
+        const u32* mg = (const u32*)(a.inval + t * 64 * (u64)G);  // 4-byte aligned (launch checks a.inval)
+        for (int j = 0; j < nmw; j += 64) {
+            const int it = 2 * (j + lane) < nwords ? j + lane : 0;
+            __builtin_amdgcn_global_load_lds((const void*)(mg + it), (__attribute__((address_space(3))) void*)(stage + ngw + j), 4, 0, 0);
+        }
+    };
+    prefetch(wid);
     wave_sync();
     for (u64 tile = wid; tile < a.ntiles; tile += nwaves) {
         const u64 r0 = tile * 64;
         const int nr = (int)min((u64)64, a.n_reads - r0);
         const u64 livem = nr >= 64 ? ~0ull : ((1ull << nr) - 1ull);
-        // 1. the tile's code words into the rows; read flags (not-ACGT bases,
-        // aligned all-A halves inside the read)
+        // 1. the tile's staged code words into the rows; read flags (not-ACGT
+        // bases, aligned all-A halves inside the read)
         rflag[lane] = 0;
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the staging DMA has landed
         wave_sync();
         {
-            const u64 base = r0 * (u64)G;
             const int nwords = nr * G;
-            for (int it0 = 0; it0 < nwords; it0 += 4 * 64) {
-                u32 cw[4], iv[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int it = it0 + 64 * j + lane;
-                    cw[j] = 0;
-                    iv[j] = 0;
-                    if (it < nwords) {
-                        cw[j] = __builtin_nontemporal_load(a.codes + base + (u64)it);
-                        iv[j] = __builtin_nontemporal_load(a.inval + base + (u64)it);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int it = it0 + 64 * j + lane;
-                    if (it < nwords) {
-                        const int r = (int)div_g.div((u32)it), g = it - r * G;
-                        codes[r * NG + g] = cw[j];
-                        const bool za = ((cw[j] >> 16) == 0u && 16 * g + 8 <= L) || ((cw[j] & 0xffffu) == 0u && 16 * g + 16 <= L);
-                        const u32 f = (iv[j] ? 1u : 0u) | (za ? 2u : 0u);
-                        if (f) atomicOr(&rflag[r], f);
-                    }
-                }
+            for (int it = lane; it < nwords; it += 64) {
+                const u32 cw = stage[it];
+                const u32 iv = (stage[ngw + (it >> 1)] >> (16 * (it & 1))) & 0xffffu;
+                const int r = (int)div_g.div((u32)it), g = it - r * G;
+                codes[r * NG + g] = cw;
+                const bool za = ((cw >> 16) == 0u && 16 * g + 8 <= L) || ((cw & 0xffffu) == 0u && 16 * g + 16 <= L);
+                const u32 f = (iv ? 1u : 0u) | (za ? 2u : 0u);
+                if (f) atomicOr(&rflag[r], f);
             }
         }
         wave_sync();
+        prefetch(tile + nwaves);
         const u32 fl = lane < nr ? rflag[lane] : 0u;
         const int slow = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(fl != 0u) != 0ull ? 1 : 0);  // uniform
         const unsigned short* ivg = a.inval + (r0 + (u64)(lane < nr ? lane : 0)) * (u64)G;
@@ -1133,14 +1141,55 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
         u32 Sp[B];                 // suffix minima of the previous block
         u32 St[D > 0 ? D : 1];     // ... of the block before it, last D
         u32 prev = kNoKey, s = 0;  // the open run: bucket, first window
-        u32 xcnt = 0;
 #pragma unroll
         for (int i = 0; i < B; i++) Sp[i] = ~0u;
 #pragma unroll
         for (int i = 0; i < (D > 0 ? D : 1); i++) St[i] = ~0u;
+        const bool fast = !slow && !(a.skip & 2);
+        const bool live = lane < nr;
+        const int g_lo = (E + 1 + 15) / 16;                  // first block whose windows are all >= 1
+        const int g_hi = np >= 16 ? (np - 16) / 16 + 1 : 0;  // blocks ending before np
         u32 c0 = crow[0];
         for (int g = 0; 16 * g < ((a.skip & 4) ? 0 : np); g++) {
             const u32 c1 = crow[g + 1];
+            // interior block of a tile without flagged reads: every window
+            // exists (w >= 1) and is live, no per-window branch; lanes without a
+            // run to push write their spare ring slot
+            auto fast_block = [&](auto tag) {
+                constexpr int OFF = decltype(tag)::value;
+                const int p0 = 16 * g + OFF;
+                u32 h[B];
+#pragma unroll
+                for (int i = 0; i < B; i++) h[i] = mul_u24(f3_mmer(c0, c1, OFF + i) ^ 0xd1e995u, 0x9e3779u);
+                u32 P = h[0];
+                const u32 wv0 = (u32)(p0 - E) + (u32)lane * 0u;  // window of j = 0, in a VGPR
+                f3_static_for<0, B>([&](auto jt) {
+                    constexpr int j = decltype(jt)::value;
+                    if constexpr (j > 0) P = min(P, h[j]);
+                    u32 v;
+                    if constexpr (j < D)
+                        v = min(min(St[j], Sp[0]), P);
+                    else
+                        v = min(Sp[j - D], P);
+                    const u32 u = min(v & 0xffffu, kNoKey - 1u);
+                    const u32 w = wv0 + (u32)j;
+                    const bool bnd = u != prev;
+                    const u64 pm = __builtin_amdgcn_ballot_w64(bnd) & livem;
+                    const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0u)) + qn;
+                    const u32 slot = (bnd && live) ? rank : (u32)(kF3Ring - 64 + lane);
+                    ring[slot] = ((u64)(ltag | (w - 1u)) << 32) | ((s << 16) | prev);
+                    qn += (u32)__popcll(pm);
+                    if (bnd) s = w;
+                    prev = u;
+                    if constexpr ((j & 3) == 3)
+                        while (qn >= 64u) drain(64u);
+                });
+#pragma unroll
+                for (int x = 0; x < D; x++) St[x] = Sp[B - D + x];
+                Sp[B - 1] = h[B - 1];
+#pragma unroll
+                for (int i = B - 2; i >= 0; i--) Sp[i] = min(h[i], Sp[i + 1]);
+            };
             auto block = [&](auto tag) {
                 constexpr int OFF = decltype(tag)::value;
                 const int p0 = 16 * g + OFF;
@@ -1181,13 +1230,7 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
                         if (w == 0) {
                             s = 0;
                         } else if (!(a.skip & 2)) {
-                            if (!slow && (a.skip & 16)) {
-                                // timing experiment: a per-lane append instead of the wave ring
-                                const bool bnd = u != prev;
-                                ring[lane * 4 + (xcnt & 3u)] = ((u64)(ltag | (u32)(w - 1)) << 32) | ((s << 16) | prev);
-                                xcnt += (bnd && lane < nr) ? 1u : 0u;
-                                if (bnd) s = (u32)w;
-                            } else if (!slow) {
+                            if (!slow) {
                                 const bool bnd = u != prev;
                                 push(bnd && lane < nr, __builtin_amdgcn_ballot_w64(bnd) & livem, w - 1, s, prev);
                                 if (bnd) s = (u32)w;
@@ -1209,8 +1252,13 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
 #pragma unroll
                 for (int i = B - 2; i >= 0; i--) Sp[i] = min(h[i], Sp[i + 1]);
             };
-            block(F3Tag<0>{});
-            if constexpr (B == 8) block(F3Tag<8>{});
+            if (fast && g >= g_lo && g < g_hi) {
+                fast_block(F3Tag<0>{});
+                if constexpr (B == 8) fast_block(F3Tag<8>{});
+            } else {
+                block(F3Tag<0>{});
+                if constexpr (B == 8) block(F3Tag<8>{});
+            }
             c0 = c1;
         }
         // the open runs end at the last window
@@ -1219,7 +1267,7 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
             push(ended, __builtin_amdgcn_ballot_w64(ended), nw - 1, s, prev);
         }
         while (qn) drain(min(64u, qn));
-        if (!slow && lane < nr) my_valid += (u64)nw + (xcnt & 0x80000000u);
+        if (!slow && lane < nr) my_valid += (u64)nw;
         wave_sync();
     }
     // pad the rest of the wave's chunk with n = 0 records in bucket kNoKey
@@ -1242,6 +1290,7 @@ __global__ __launch_bounds__(kSkmBlock) void skm_front3_k(F3Args a) {
 static bool f3_args(const CountLaunch& l, const SkmGeom& g, F3Args* a, size_t* lds) {
     const int W = (l.k + 31) / 32;
     if (W != 1 || g.m != 11 || l.k < 19 || l.k > 32 || getenv("KC_NO_F3")) return false;
+    if (((uintptr_t)l.inval & 3) || ((uintptr_t)l.codes & 3)) return false;  // dword DMA of the masks
     const int nw = l.L - l.k + 1;
     if (nw <= 0 || nw > 65535) return false;
     a->G = groups_per_read(l.L);
@@ -1253,7 +1302,8 @@ static bool f3_args(const CountLaunch& l, const SkmGeom& g, F3Args* a, size_t* l
     if (ng < (nw - 1) / 16 + 5) ng = (nw - 1) / 16 + 5;
     ng |= 1;  // odd stride: a lane per row, no bank conflicts
     a->NG = ng;
-    const size_t wbytes = (size_t)kF3Ring * 8 + 64 * 4 + (size_t)64 * ng * 4;
+    // ring, read flags, rows, staging (codes + masks of the next tile)
+    const size_t wbytes = (size_t)kF3Ring * 8 + 64 * 4 + (size_t)64 * ng * 4 + (size_t)96 * a->G * 4;
     if (wbytes > 40 * 1024) return false;
     a->wbytes = (u32)wbytes;
     *lds = (size_t)(kSkmBlock / 64) * wbytes;
