@@ -2524,7 +2524,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
                                                         u64* __restrict__ okeys, u32* __restrict__ ocnts,
                                                         u64 ostride, u32* __restrict__ packed,
                                                         u64* __restrict__ stats, u32* __restrict__ fb,
-                                                        u64* __restrict__ fb_n) {
+                                                        u64* __restrict__ fb_n, int skip) {
     constexpr int CAP = SegCfg<W>::CAP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* skey = (u64*)smem;                      // W x CAP
@@ -2640,7 +2640,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         // insertion sort of this thread's 4 bins [bs, bs + sum)
         const u32 ends[4] = {bs + c0, bs + c0 + c1, bs + c0 + c1 + c2, bs + sum};
         u32 s0 = bs;
-        for (int qb = 0; qb < 4; qb++) {
+        for (int qb = 0; qb < ((skip & 2) ? 0 : 4); qb++) {
             const u32 e0 = ends[qb];
             for (u32 x = s0 + 1; x < e0; x++) {
                 u64 kx[W];
@@ -2671,7 +2671,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             s0 = e0;
         }
         __syncthreads();
-        for (u32 p = tid; p < len; p += kSegBlock) {
+        for (u32 p = tid; p < ((skip & 1) ? 0u : len); p += kSegBlock) {
             u64 kk[W];
 #pragma unroll
             for (int jj = 0; jj < W; jj++) kk[jj] = skey[(size_t)jj * CAP + p];
@@ -2868,9 +2868,11 @@ hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, 
     if (e != hipSuccess) return e;
     const size_t lds_msd = (seg_sort_msd_lds(W) + 15) & ~(size_t)15;
     const size_t lds = (seg_sort_lds(W) + 15) & ~(size_t)15;
+    const char* se = getenv("KC_SEG_SKIP");  // timing experiments: 1 output stores, 2 insertion sort
+    const int skip = se ? atoi(se) : 0;
 #define KC_SEG(WW)                                                                                                  \
     hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds_msd, s, rkeys, rcnts, rstride, order,       \
-                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, fb, fb_n);       \
+                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, fb, fb_n, skip); \
     hipLaunchKernelGGL(seg_sort_lsd_k<WW>, dim3(grid), dim3(kSegBlock), lds, s, rkeys, rcnts, rstride, order,       \
                        dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, (const u32*)fb,   \
                        (const u64*)fb_n)
