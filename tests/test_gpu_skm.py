@@ -174,11 +174,15 @@ def _special_reads(L, n, seed):
     return out
 
 
+@pytest.mark.parametrize("front", ["f3", "f2"])
 @pytest.mark.parametrize("k", list(range(18, 33)))
-def test_skm_front2_every_k(kca, orc, k):
-    """F2 (skm_front2_k<1, k>, every k of W = 1) against the oracle and
-    against the generic F (KC_NO_F2) on reads that take its slow path, plus
-    genome reads that take its fast path."""
+def test_skm_front_every_k(kca, orc, monkeypatch, k, front):
+    """The W = 1 front ends for every k: F3 (skm_front3_k<k>, k >= 19; k = 18
+    falls to F2) and F2 (skm_front2_k<1, k>, under KC_NO_F3) against the
+    oracle, on reads that take their slow paths (not-ACGT bases, all-A
+    stretches, poly-T) plus genome reads that take the fast paths."""
+    if front == "f2":
+        monkeypatch.setenv("KC_NO_F3", "1")
     L = 150
     reads = _special_reads(L, 3000, k)
     fq = _fq(reads) + kca.synth_fastq(20000, L, seed=k, genome_length=200_000, first_read=3000)
@@ -188,20 +192,35 @@ def test_skm_front2_every_k(kca, orc, k):
     assert got == orc.count_fastq(fq, k)
 
 
-@pytest.mark.parametrize("k,L", [(31, 40), (31, 63), (21, 200), (32, 300), (25, 530), (31, 600)])
-def test_skm_front2_read_lengths(kca, orc, monkeypatch, k, L):
-    """Read lengths from one chunk per read to 64 chunks (the F2 limit) and
-    past it (L = 600: the generic F); F2 and the generic F give the same bytes."""
+@pytest.mark.parametrize("k,L", [(31, 40), (31, 63), (21, 200), (32, 300), (25, 530), (31, 600), (19, 1000)])
+def test_skm_front_read_lengths(kca, orc, monkeypatch, k, L):
+    """Read lengths from one 8-window chunk per read to past F2's 64 chunks;
+    F3, F2 (KC_NO_F3) and the generic F (KC_NO_F3 + KC_NO_F2) give the same
+    bytes where each applies."""
     fq = _fq(_special_reads(L, 400, L)) + kca.synth_fastq(3000, L, seed=L, genome_length=100_000, first_read=400)
     outs = []
-    for no_f2 in (False, True):
-        if no_f2:
-            monkeypatch.setenv("KC_NO_F2", "1")
+    for env in ((), ("KC_NO_F3",), ("KC_NO_F3", "KC_NO_F2")):
+        for v in env:
+            monkeypatch.setenv(v, "1")
         with kca.Context(kmer_length=k, line_length=L, engine="skm") as ctx:
             ctx.count_fastq(fq)
             outs.append(ctx.records())
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
     assert outs[0] == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("L", [27, 32, 48, 150])
+def test_skm_front3_lengths_multiple_of_16(kca, orc, L):
+    """F3 at read lengths around and at multiples of 16 (k = 27: the last
+    window's key ends at the read end; all-A halves at the read end are real
+    bases when L is a multiple of 8)."""
+    k = 27
+    reads = _special_reads(L, 600, L + 1) + ["A" * L, "T" * L, "A" * (L - 8) + "C" * 8]
+    fq = _fq(reads) + kca.synth_fastq(2000, L, seed=L, genome_length=50_000, first_read=len(reads))
+    with kca.Context(kmer_length=k, line_length=L, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, k)
 
 
 @pytest.mark.parametrize("groups", [None, "64", "3"])
