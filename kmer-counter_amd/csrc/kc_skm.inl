@@ -1635,9 +1635,19 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     u64 nk[KPT][NW];
     u32 np[KPT];
+    // tiles: with a grid of 8k workgroups, XCD x (blocks b = x mod 8) walks
+    // the x-th eighth of the tiles, 8k/8 consecutive tiles at a time, so the
+    // digit runs that land next to each other in the output are written
+    // through the same L2 (partial lines merge there); else block b walks
+    // b, b + grid, ...
+    const bool xcd_map = (gridDim.x & 7u) == 0u && ntiles >= 8;
+    const u64 step = xcd_map ? (u64)(gridDim.x >> 3) : (u64)gridDim.x;
+    const u64 tx = (ntiles + 7) >> 3;
+    const u64 t_first = xcd_map ? (u64)(blockIdx.x & 7u) * tx + (blockIdx.x >> 3) : (u64)blockIdx.x;
+    const u64 t_end = xcd_map ? min(ntiles, (u64)((blockIdx.x & 7u) + 1) * tx) : ntiles;
     auto load = [&](u64 t) {
         u64 lo = 0, hi = 0;
-        if (t < ntiles) rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+        if (t < t_end) rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
             const u64 q = lo + (u64)i * kP3Block + tid;
@@ -1647,10 +1657,10 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
             if constexpr (PAY) np[i] = q < hi ? __builtin_nontemporal_load(pin + q) : 0u;
         }
     };
-    load(blockIdx.x);
+    load(t_first);
     // this tile's 256 global run starts, loaded one tile ahead like the items
-    u64 npos = (tid < 256 && blockIdx.x < ntiles) ? pos[(u64)blockIdx.x * 256 + tid] : 0ull;
-    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    u64 npos = (tid < 256 && t_first < t_end) ? pos[t_first * 256 + tid] : 0ull;
+    for (u64 t = t_first; t < t_end; t += step) {
         u64 lo, hi;
         rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
         const u32 len = (u32)(hi - lo);
@@ -1665,8 +1675,8 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
         for (int i = tid; i < 16 * 128; i += kP3Block) wc[i] = 0;
         if (tid < 256) gpos[tid] = npos;
         __syncthreads();
-        load(t + gridDim.x);
-        if (tid < 256 && t + gridDim.x < ntiles) npos = pos[(t + gridDim.x) * 256 + tid];
+        load(t + step);
+        if (tid < 256 && t + step < t_end) npos = pos[(t + step) * 256 + tid];
         u32 rank[KPT];
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
