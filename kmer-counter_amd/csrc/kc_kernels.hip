@@ -2637,6 +2637,26 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             scnt[q] = rcnts[st + p];
         }
         __syncthreads();
+        if constexpr (W == 1) {
+            // one-word keys: every record's rank inside its bin (bin d spans
+            // [end of bin d - 1, end of bin d) after the scatter; equal keys,
+            // which batches that are summed later can hold, by LDS position)
+            // is its place: written straight there
+            for (u32 p = tid; p < ((skip & 1) ? 0u : len); p += kSegBlock) {
+                const u64 kp = skey[p];
+                const u32 d = (u32)(kp >> sh) & 4095u;
+                const u32 b0 = d ? bcnt[d - 1] : 0u, b1 = bcnt[d];
+                u32 r = 0;
+                for (u32 q = b0; q < ((skip & 2) ? b0 : b1); q++) {
+                    const u64 kq = skey[q];
+                    r += (kq < kp || (kq == kp && q < p)) ? 1u : 0u;
+                }
+                const u64 kk[1] = {kp};
+                seg_put<1>(okeys, ocnts, ostride, packed, obase + b0 + r, kk, scnt[p]);
+            }
+            __syncthreads();
+            continue;
+        }
         // insertion sort of this thread's 4 bins [bs, bs + sum)
         const u32 ends[4] = {bs + c0, bs + c0 + c1, bs + c0 + c1 + c2, bs + sum};
         u32 s0 = bs;
