@@ -1862,6 +1862,9 @@ __device__ __forceinline__ void skm_key(const u64 (&rw)[W + 1], u32 i, u64 last_
 }
 
 constexpr int kSkmGroup = 4;    // P5 LDS table: slots per group (two 16-byte loads per key)
+#ifndef KC_P5_CLAIM
+#define KC_P5_CLAIM 1  // P5 (W = 1): new keys claim an empty home-group slot in the walk, not the slow path
+#endif
 constexpr u32 kSkmQueue = 128;  // P5 per-wave slow-path queue entries (u64: key at W = 1, else record << 6 | key index)
 
 // P5 LDS: table (lcap slots) + misc (48 u32) + per-wave slow-path queues +
@@ -2211,6 +2214,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                     }
                 };
                 if (W == 1 && grouped) {
+                    u32 fclaim = 0;  // slots this lane claimed in this batch
                     // software pipeline: the home group of key t + 1 is loaded
                     // while key t is resolved (a group read before a claim of
                     // the slow path only sends that key to the slow path again)
@@ -2237,7 +2241,23 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                         const int hit = e0 ? 0 : (e1 ? 1 : (e2 ? 2 : 3));
                         const bool found = want && (e0 || e1 || e2 || e3);
                         if (found) atomicAdd(&lcnt[kSkmGroup * g + hit], kw);
-                        const bool pend = want && !found;
+                        bool pend = want && !found;
+                        if constexpr (KC_P5_CLAIM) {
+                            // a new key takes the first empty slot of its home
+                            // group here (slots fill in order and never empty
+                            // within a pass, so a key still sits in one slot);
+                            // a lost race goes to the slow path
+                            const bool z0 = a0.x == 0ull, z1 = a0.y == 0ull, z2 = a1.x == 0ull, z3 = a1.y == 0ull;
+                            if (pend && (z0 || z1 || z2 || z3)) {
+                                const u32 sl = kSkmGroup * g + (z0 ? 0u : (z1 ? 1u : (z2 ? 2u : 3u)));
+                                const u64 old = atomicCAS((unsigned long long*)&lkeys[sl], 0ull, (unsigned long long)key);
+                                if (old == 0ull || old == key) {
+                                    atomicAdd(&lcnt[sl], kw);
+                                    fclaim += old == 0ull ? 1u : 0u;
+                                    pend = false;
+                                }
+                            }
+                        }
                         const u64 pb = __ballot(pend);
                         if (pb) {
                             if (pend) {
@@ -2264,6 +2284,17 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                         g = g_n;
                         a0 = b0;
                         a1 = b1;
+                    }
+                    if constexpr (KC_P5_CLAIM) {
+                        // this batch's claims into the pass's fill count (exact
+                        // before the emission; the abort check follows it)
+                        u32 fc = fclaim;
+                        for (int o2 = 32; o2 >= 1; o2 >>= 1) fc += (u32)__shfl_xor((int)fc, o2);
+                        if (fc && lane == 0) {
+                            const u32 f = atomicAdd(lfill, fc) + fc;
+                            if (!last && f > limit) atomicOr(labort, 1u);
+                        }
+                        fclaim = 0;
                     }
                 } else {
                 for (u32 t = 0; t < per; t++) {
