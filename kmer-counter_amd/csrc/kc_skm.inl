@@ -2541,7 +2541,10 @@ u32 rec_dedup_groups() {
     return g & ~15u;
 }
 
-__global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
+// starts_r: a.starts as a read-only kernel argument, so a bucket's range is a
+// scalar load that never waits behind the record loads and write-back stores
+// in flight (in-order vmcnt)
+__global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, const u64* __restrict__ starts_r) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* tab = (u64*)smem;                        // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
     u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);  // 2 ngrp
@@ -2562,7 +2565,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
     // are loaded while the previous bucket is written out
     u64 n0[kRecPd], n1[kRecPd];
     auto share = [&](u32 bb, u64* wlo, u64* whi) {
-        const u64 lo = a.starts[bb], hi = a.starts[bb + 1];
+        const u64 lo = starts_r[bb], hi = starts_r[bb + 1];
         const u64 nr = hi - lo, per_w = (nr + kBucketWaves - 1) / kBucketWaves;
         *wlo = lo + min(nr, (u64)wave * per_w);
         *whi = lo + min(nr, (u64)(wave + 1) * per_w);
@@ -2647,7 +2650,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a) {
             total += v;
         }
         if (tid == 0) a.dlen[b] = raw ? kRawList : total;
-        u64 pos = a.starts[b] + before;
+        u64 pos = starts_r[b] + before;
         for (u32 c0 = s0; c0 < s1; c0 += 64) {
             const u32 i = c0 + (u32)lane;
             const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
@@ -2701,7 +2704,7 @@ hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* sta
     a.cnt = cnt;
     a.dlen = dlen;
     const size_t lds = (rec_dedup_lds(a.ngrp) + 15) & ~(size_t)15;
-    hipLaunchKernelGGL(count_rec_k, dim3(grid), dim3(kBucketBlock), lds, s, a);
+    hipLaunchKernelGGL(count_rec_k, dim3(grid), dim3(kBucketBlock), lds, s, a, a.starts);
     return hipGetLastError();
 }
 
