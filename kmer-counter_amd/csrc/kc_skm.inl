@@ -2548,7 +2548,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* tab = (u64*)smem;                        // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
     u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);  // 2 ngrp
-    u32* misc = cnt + 2 * (size_t)a.ngrp;         // [0] overflow, [1..16] wave totals
+    u32* misc = cnt + 2 * (size_t)a.ngrp;         // [0] overflow, [1..16] wave totals, [17] write-back cursor
     const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
     const u32 nent = 2 * a.ngrp;
     const u64 lt = lanemask_lt();
@@ -2557,7 +2557,10 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
         tab[2 * (size_t)i + 1] = 0ull;
         cnt[i] = 0;
     }
-    if (tid == 0) misc[0] = 0;
+    if (tid == 0) {
+        misc[0] = 0;
+        misc[17] = 0;
+    }
     __syncthreads();
     constexpr u64 kMark = 0x8000ull << 48;  // replaces the bucket bits: a non-zero word 0
     constexpr u64 kLow48 = (1ull << 48) - 1ull;
@@ -2585,6 +2588,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
         u64 wlo, whi;
         share(b, &wlo, &whi);
         bool over = false;
+        u32 claims = 0;  // entries this lane took
         for (u64 base = wlo; base < whi; base += 64) {
             const bool act = base + lane < whi;
             const u64 k0 = (n0[0] & kLow48) | kMark, k1 = n1[0];
@@ -2618,6 +2622,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
                             tab[2 * (size_t)e + 1] = k1;
                             atomicAdd(&cnt[e], 1u);
                             done = true;
+                            ++claims;
                         }
                         // lost the entry: the group is read again
                     } else {
@@ -2633,42 +2638,44 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
         // batches go in flight, then the distinct records are written back
         prefetch(b + gridDim.x);
         const bool raw = misc[0] != 0u;
+        // the distinct records = the entries taken (every taken entry holds a
+        // record); one pass over the table writes them back, each wave's
+        // occupied entries at positions from an LDS counter
+        for (int o2 = 32; o2 >= 1; o2 >>= 1) claims += (u32)__shfl_xor((int)claims, o2);
+        if (lane == 0) misc[1 + wave] = claims;
+        __syncthreads();
+        u32 total = 0;
+        for (int w = 0; w < kBucketWaves; w++) total += misc[1 + w];
+        if (tid == 0) a.dlen[b] = raw ? kRawList : total;
         const u32 spw = (nent + kBucketWaves - 1) / kBucketWaves;
         const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
-        u32 wc = 0;
-        if (!raw)
-            for (u32 c0 = s0; c0 < s1; c0 += 64) {
-                const u32 i = c0 + (u32)lane;
-                wc += (u32)__popcll(__ballot(i < s1 && tab[2 * (size_t)i] != 0ull));
-            }
-        if (lane == 0) misc[1 + wave] = wc;
-        __syncthreads();
-        u32 total = 0, before = 0;
-        for (int w = 0; w < kBucketWaves; w++) {
-            const u32 v = misc[1 + w];
-            before += w < wave ? v : 0u;
-            total += v;
-        }
-        if (tid == 0) a.dlen[b] = raw ? kRawList : total;
-        u64 pos = starts_r[b] + before;
+        const u64 pos0 = starts_r[b];
         for (u32 c0 = s0; c0 < s1; c0 += 64) {
             const u32 i = c0 + (u32)lane;
             const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
             const u64 bm = __ballot(occ);
-            if (occ) {
-                if (!raw) {
-                    const u64 q = pos + (u64)__popcll(bm & lt);
-                    a.recs[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
-                    a.recs[a.stride + q] = tab[2 * (size_t)i + 1];
-                    a.cnt[q] = cnt[i];
+            if (bm) {
+                u32 wb = 0;
+                if (lane == 0 && !raw) wb = atomicAdd(&misc[17], (u32)__popcll(bm));
+                wb = (u32)__builtin_amdgcn_readfirstlane((int)wb);
+                if (occ) {
+                    if (!raw) {
+                        const u64 q = pos0 + wb + (u64)__popcll(bm & lt);
+                        a.recs[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
+                        a.recs[a.stride + q] = tab[2 * (size_t)i + 1];
+                        a.cnt[q] = cnt[i];
+                    }
+                    tab[2 * (size_t)i] = 0ull;
+                    tab[2 * (size_t)i + 1] = 0ull;
+                    cnt[i] = 0;
                 }
-                tab[2 * (size_t)i] = 0ull;
-                tab[2 * (size_t)i + 1] = 0ull;
-                cnt[i] = 0;
             }
-            pos += (u64)__popcll(bm);
         }
-        if (tid == 0) misc[0] = 0;
+        __syncthreads();
+        if (tid == 0) {
+            misc[0] = 0;
+            misc[17] = 0;
+        }
         __syncthreads();
     }
 }
