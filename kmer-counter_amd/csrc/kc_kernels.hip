@@ -3268,6 +3268,25 @@ __device__ __forceinline__ u32 nl_nib(u32 w) {
     return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | (z >> 28);
 }
 
+// '\n' bytes of 16 bytes (4 dwords, first byte lowest) as a 16-bit mask, bit
+// i = byte i: the per-byte flags (0x80 per byte) of the 4 dwords are merged as
+// y = z0 >> 7 | z1 >> 6 | z2 >> 5 | z3 >> 4 (byte b, bit q = byte 4q + b),
+// packed to 16 bits and the 4 x 4 bit block transposed
+__device__ __forceinline__ u32 nl_mask16w(u32 w0, u32 w1, u32 w2, u32 w3) {
+    auto z = [](u32 w) {
+        const u32 t = w ^ 0x0a0a0a0au;
+        return ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
+    };
+    const u32 y = (z(w0) >> 7) | (z(w1) >> 6) | (z(w2) >> 5) | (z(w3) >> 4);
+    const u32 v1 = (y | (y >> 4)) & 0x00ff00ffu;
+    u32 p = (v1 & 0xffu) | ((v1 >> 8) & 0xff00u);
+    u32 t = (p ^ (p >> 3)) & 0x0a0au;
+    p ^= t ^ (t << 3);
+    t = (p ^ (p >> 6)) & 0x00ccu;
+    p ^= t ^ (t << 6);
+    return p & 0xffffu;
+}
+
 // newline bytes among the first nv bytes of a dword (any)
 __device__ __forceinline__ bool has_nl(u32 x, int nv) {
     if (nv <= 0) return false;
@@ -3359,11 +3378,8 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
             for (int rd = 0; rd < 2; rd++) {
                 u64 m = 0;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const u32 q4 = nl_nib(v[rd][i].x) | (nl_nib(v[rd][i].y) << 4) | (nl_nib(v[rd][i].z) << 8) |
-                                   (nl_nib(v[rd][i].w) << 12);
-                    m |= (u64)q4 << (16 * i);
-                }
+                for (int i = 0; i < 4; i++)
+                    m |= (u64)nl_mask16w(v[rd][i].x, v[rd][i].y, v[rd][i].z, v[rd][i].w) << (16 * i);
                 const long long rel0 = hrel + rd * 4096 + lane * 64;
                 if (rel0 < 0) m = (rel0 <= -64) ? 0ull : (m & (~0ull << (u32)(-rel0)));
                 if (rel0 + 64 > (long long)n) m = (rel0 >= (long long)n) ? 0ull : (m & (~0ull >> (u32)(rel0 + 64 - (long long)n)));
