@@ -3310,6 +3310,37 @@ __device__ __forceinline__ u32 swar_codes(u32 x, int nv, u32* bad4) {
     return ((t << 6) | (t >> 4) | (t >> 14) | (t >> 24)) & 255u;
 }
 
+// 16 bytes (x0 first, lowest byte first; nb of them valid) -> the group's code
+// word (base 0 in bits 31-30) and not-ACGT mask (base 0 in bit 15), as
+// swar_codes per dword, with the four code bytes packed by one 24-bit multiply
+// each (c0, c1, c2 at bits 0, 8, 16 times 2^22 + 2^12 + 2^2 land at bits 22,
+// 20, 18 with no carries) and the 16 byte flags transposed as in nl_mask16w
+__device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb, u32* bad16) {
+    const u32 xs[4] = {x0, x1, x2, x3};
+    u32 bf[4], code = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int nv = nb - 4 * k;
+        const u32 vm = nv >= 4 ? ~0u : (nv <= 0 ? 0u : (~0u >> (8 * (4 - nv))));
+        u32 t = ((xs[k] >> 1) ^ (xs[k] >> 2)) & 0x03030303u;
+        const u32 y = __builtin_amdgcn_perm(0u, 0x54474341u, t) ^ xs[k];
+        const u32 bad = (((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u & vm;
+        t = (t & vm) | (bad >> 7) | (bad >> 6);
+        bf[k] = bad;
+        const u32 c4 = ((__umul24(t, 0x401004u) >> 16) & 0xfcu) | (t >> 24);
+        code |= c4 << (24 - 8 * k);
+    }
+    const u32 yb = (bf[0] >> 7) | (bf[1] >> 6) | (bf[2] >> 5) | (bf[3] >> 4);
+    const u32 v1 = (yb | (yb >> 4)) & 0x00ff00ffu;
+    u32 p = (v1 & 0xffu) | ((v1 >> 8) & 0xff00u);
+    u32 tt = (p ^ (p >> 3)) & 0x0a0au;
+    p ^= tt ^ (tt << 3);
+    tt = (p ^ (p >> 6)) & 0x00ccu;
+    p ^= tt ^ (tt << 6);
+    *bad16 = __builtin_bitreverse32(p) >> 16;
+    return code;
+}
+
 __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                       const u64* __restrict__ line_base, u64 max_rec, int L, int G,
                                                       int lcap, u32* __restrict__ codes,
@@ -3458,12 +3489,8 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 const u32 x1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
                 const u32 x2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
                 const u32 x3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
-                u32 b0, b1, b2, b3;
-                const u32 c0 = swar_codes(x0, nb, &b0);
-                const u32 c1 = swar_codes(x1, nb - 4, &b1);
-                const u32 c2 = swar_codes(x2, nb - 8, &b2);
-                const u32 c3 = swar_codes(x3, nb - 12, &b3);
-                const u32 bad = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
+                u32 bad;
+                const u32 cw = swar_group(x0, x1, x2, x3, nb, &bad);
                 // a newline is a non-ACGT byte: the exact test only for such groups
                 bool wrong = bad != 0u &&
                              (has_nl(x0, nb) || has_nl(x1, nb - 4) || has_nl(x2, nb - 8) || has_nl(x3, nb - 12));
@@ -3474,7 +3501,7 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 }
                 if (wrong) err |= ERR_FQ_SEQ_LEN;
                 const u64 at = (rec0 + r) * (u64)G + (u64)g;
-                codes[at] = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+                codes[at] = cw;
                 inval[at] = (unsigned short)bad;
             }
             sync();
