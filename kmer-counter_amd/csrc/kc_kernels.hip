@@ -3363,26 +3363,41 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     };
-    for (u64 c = (u64)blockIdx.x * kFqWaves + wave; c < nchunks; c += (u64)gridDim.x * kFqWaves) {
-        u64 run = line_base[c];
-        for (int h = 0; h < 2; h++) {
+    // the wave's halves in order: (c, 0), (c, 1), (c + stride, 0), ...; the
+    // next half's text is loaded into registers while this one is walked and
+    // encoded from LDS
+    const u64 cstride = (u64)gridDim.x * kFqWaves;
+    uint4 v[2][4], x;
+    auto issue = [&](u64 cc, int hh) {
+        const uintptr_t hb = A + cc * kFqChunk + (u64)hh * kFqHalf;
+        const long long hrel = (long long)(hb - (uintptr_t)base);
+#pragma unroll
+        for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int o = rd * 4096 + lane * 64 + i * 16;
+                const long long rel = hrel + o;
+                v[rd][i] = (rel + 16 <= 0 || rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+            }
+        const int o = kFqHalf + lane * 16;
+        const long long rel = hrel + o;
+        x = (rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+    };
+    u64 c = (u64)blockIdx.x * kFqWaves + wave;
+    int h = 0;
+    u64 run = 0;
+    if (c < nchunks) issue(c, 0);
+    while (c < nchunks) {
+        {
             const uintptr_t hb = A + c * kFqChunk + (u64)h * kFqHalf;
             const long long hrel = (long long)(hb - (uintptr_t)base);
-            if (hrel >= (long long)n) break;
-            // rounds 0, 1: lane l holds bytes [4096 rd + 64 l, + 64); x: the next KiB
-            uint4 v[2][4], x;
-#pragma unroll
-            for (int rd = 0; rd < 2; rd++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int o = rd * 4096 + lane * 64 + i * 16;
-                    const long long rel = hrel + o;
-                    v[rd][i] = (rel + 16 <= 0 || rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
-                }
-            {
-                const int o = kFqHalf + lane * 16;
-                const long long rel = hrel + o;
-                x = (rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+            if (h == 0) run = line_base[c];
+            // the next half: (c, 1) unless it starts past the block
+            u64 cn = c;
+            int hn = 1;
+            if (h == 1 || (long long)(hrel + kFqHalf) >= (long long)n) {
+                cn = c + cstride;
+                hn = 0;
             }
 #pragma unroll
             for (int rd = 0; rd < 2; rd++)
@@ -3403,14 +3418,21 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 w.w = x.w;
                 *(v4u*)(txt + kFqHalf + lane * 16) = w;
             }
-            sync();
-            const u64 rec0 = (run + 3) >> 2;  // first record whose header may end in this half
+            u64 mk[2];
 #pragma unroll
             for (int rd = 0; rd < 2; rd++) {
                 u64 m = 0;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
                     m |= (u64)nl_mask16w(v[rd][i].x, v[rd][i].y, v[rd][i].z, v[rd][i].w) << (16 * i);
+                mk[rd] = m;
+            }
+            if (cn < nchunks) issue(cn, hn);
+            sync();
+            const u64 rec0 = (run + 3) >> 2;  // first record whose header may end in this half
+#pragma unroll
+            for (int rd = 0; rd < 2; rd++) {
+                u64 m = mk[rd];
                 const long long rel0 = hrel + rd * 4096 + lane * 64;
                 if (rel0 < 0) m = (rel0 <= -64) ? 0ull : (m & (~0ull << (u32)(-rel0)));
                 if (rel0 + 64 > (long long)n) m = (rel0 >= (long long)n) ? 0ull : (m & (~0ull >> (u32)(rel0 + 64 - (long long)n)));
@@ -3505,6 +3527,8 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 inval[at] = (unsigned short)bad;
             }
             sync();
+            c = cn;
+            h = hn;
         }
     }
     if (err) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)err);
