@@ -101,6 +101,21 @@ typedef struct kc_config {
                                     65536 buckets by the first 8 bases, each
                                     counted in an LDS table; sorted output needs
                                     no global sort */
+#define KC_FLAG_VARLEN 16u      /* variable-length reads (an
+                                    extension: the reference concatenates reads
+                                    without separators and cuts at multiples of
+                                    the first read's length, FASTQFileReader.cpp:
+                                    57-79, so it has no defined result for them).
+                                    kc_count_fastq* then accept 4-line records
+                                    whose sequence lines hold 0..line_length
+                                    bytes; every read counts the windows of a
+                                    reference read of its own length (a read
+                                    shorter than k counts none), and key 0^W is
+                                    present iff a read of >= k bases holds a
+                                    not-ACGT base or a key-0 window was counted.
+                                    kc_stats.windows sums the reads' own
+                                    windows. Not with KC_FLAG_ENGINE_TABLE
+                                    (kc_create returns KC_ERR_ARG). */
 /* Default engine (no ENGINE flag): the super-k-mer engine. Runs of consecutive
  * windows that share a minimizer bucket move through HBM as one record of
  * bases (~1.5 B per k-mer at k=31 instead of an 8-byte key), are grouped by

@@ -187,7 +187,7 @@ class Context:
 
     def __init__(self, kmer_length: int, line_length: int = 0, device: int = 0,
                  gpu_memory_limit: int = 100000000, table_bytes: int = 0, temp_dir: Optional[str] = None,
-                 quiet: bool = True, engine: str = "auto", lds_slots: int = 0):
+                 quiet: bool = True, engine: str = "auto", lds_slots: int = 0, variable_length: bool = False):
         self._L = lib()
         self.k = kmer_length
         self.W = (kmer_length + 31) // 32
@@ -197,7 +197,7 @@ class Context:
         engine_flags = {"auto": 0, "table": 2, "skm": 4, "partition": 8}
         if engine not in engine_flags:
             raise ValueError("engine must be 'auto', 'skm', 'partition' or 'table'")
-        flags = (1 if quiet else 0) | engine_flags[engine]
+        flags = (1 if quiet else 0) | engine_flags[engine] | (16 if variable_length else 0)
         cfg = _Config(device, 0, kmer_length, line_length or kmer_length, int(gpu_memory_limit), int(table_bytes),
                       self._tmp, flags, int(lds_slots))
         h = ctypes.c_void_p()

@@ -876,7 +876,7 @@ static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq
 // one batch, the emit pass also encodes every read (fq_encode: the text is read
 // twice instead of three times) and *encoded is set; seq_off is then unset.
 static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out,
-                             bool* encoded = nullptr) {
+                             bool* encoded = nullptr, bool varlen = false) {
     if (encoded) *encoded = false;
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
@@ -897,7 +897,7 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
         return fail(c, KC_ERR_FORMAT, "FASTQ block has %llu lines, not a multiple of 4", (unsigned long long)lines);
     uint64_t n_rec = lines / 4;
     const uint64_t nw = (uint64_t)(L - c->k + 1);
-    const bool fuse = encoded && !getenv("KC_NO_FQ_ENCODE") && L >= c->k && engine_reads_codes(c, L) &&
+    const bool fuse = encoded && !varlen && !getenv("KC_NO_FQ_ENCODE") && L >= c->k && engine_reads_codes(c, L) &&
                       n_rec * nw <= c->key_cap;
     if (fuse) {
         const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
@@ -908,8 +908,18 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
         if ((s = ensure(c, c->seq_off, n_rec * 8 + 8)) || (s = ensure(c, c->seq_end, n_rec * 8 + 8))) return s;
         HIPCHK(c, launch_fq_emit(base, n, (uint64_t*)c->fq_base.p, (uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p,
                                  n_rec, c->stats, c->stream));
-        HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
-                                     c->stream));
+        if (varlen) {
+            // sequence lengths up to L, checked (and the reads encoded) by E-var
+            const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
+            if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
+            HIPCHK(c, hipMemsetAsync(c->stats + ST_VHOLE, 0, 16, c->stream));
+            HIPCHK(c, launch_encode_reads_var(base, (const uint64_t*)c->seq_off.p, (const uint64_t*)c->seq_end.p, n_rec,
+                                              (int)L, (int)c->k, (uint32_t*)c->part_codes.p,
+                                              (uint16_t*)c->part_inval.p, c->stats, c->stream));
+        } else {
+            HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
+                                         c->stream));
+        }
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     if ((s = sync_stats(c))) return s;
@@ -921,13 +931,13 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
         std::string why;
         if (e & ERR_FQ_NOT_AT) why += " record-does-not-start-with-@";
         if (e & ERR_FQ_NO_PLUS) why += " no-+-line-after-sequence";
-        if (e & ERR_FQ_SEQ_LEN) why += " sequence-length-differs-from-L";
+        if (e & ERR_FQ_SEQ_LEN) why += varlen ? " sequence-longer-than-L" : " sequence-length-differs-from-L";
         if (e & ERR_FQ_TOO_MANY) why += " index-overflow";
         if (e & ERR_FQ_NO_FINAL_NL) why += " block-does-not-end-with-newline";
         HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
         c->stats_h[ST_ERR] = 0;
-        return fail(c, KC_ERR_FORMAT, "FASTQ block is not 4-line records with %lld-base reads:%s", (long long)L,
-                    why.c_str());
+        return fail(c, KC_ERR_FORMAT, "FASTQ block is not 4-line records with %s%lld-base reads:%s",
+                    varlen ? "at most " : "", (long long)L, why.c_str());
     }
     *n_rec_out = n_rec;
     if (encoded) *encoded = fuse;
@@ -991,6 +1001,10 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(KC_ERR_HIP);
     uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
     if (M < (1u << 20)) M = 1u << 20;
+    if ((cfg->flags & KC_FLAG_VARLEN) && (cfg->flags & KC_FLAG_ENGINE_TABLE)) {
+        delete c;
+        return KC_ERR_ARG;  // the table engine reads the text, not encoded reads
+    }
     c->part = (cfg->flags & KC_FLAG_ENGINE_TABLE) == 0;
     c->skm = c->part && (cfg->flags & KC_FLAG_ENGINE_PREFIX) == 0;
     c->skm_force = (cfg->flags & KC_FLAG_ENGINE_SKM) != 0;
@@ -1135,6 +1149,40 @@ kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) 
     return count_reads(c, (const uint8_t*)c->in_stage.p, nullptr, (uint64_t)(size / L), L);
 }
 
+// KC_FLAG_VARLEN: reads of 0..L bases, each counted as a reference read of
+// its own length (the reference concatenates sequences
+// without separators and cuts them at multiples of the first read's length,
+// FASTQFileReader.cpp:57-79, GPUHandler.cu:13-15, so it has no defined result
+// here). The reads are encoded into L-base slots padded with not-ACGT bases,
+// so every engine that reads codes counts exactly their own windows. The
+// padding's invalid windows are no holes: key 0^W is present iff a read of
+// >= k bases holds a not-ACGT base (ST_VHOLE) or a key-0 window was counted.
+static kc_status fastq_device_var(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_reads,
+                                  bool count) {
+    kc_status s;
+    if (!c->part || !engine_reads_codes(c, L))
+        return fail(c, KC_ERR_ARG, "variable-length reads need an engine that reads encoded reads (L = %lld)",
+                    (long long)L);
+    uint64_t n_rec = 0;
+    if ((s = index_fastq(c, base, n, L, &n_rec, nullptr, true))) return s;
+    if (count && n_rec > 0) {
+        if ((s = sync_stats(c))) return s;
+        const uint64_t present0 = c->stats_h[ST_KEY0_PRESENT];
+        const uint64_t vhole = c->stats_h[ST_VHOLE], vwin = c->stats_h[ST_VWIN];
+        const uint64_t win0 = c->st.windows;
+        if ((s = count_reads(c, base, nullptr, n_rec, L, 0))) return s;
+        if ((s = sync_stats(c))) return s;
+        const uint64_t present = (present0 | vhole | (c->stats_h[ST_KEY0] != 0 ? 1u : 0u)) ? 1u : 0u;
+        c->stats_h[ST_KEY0_PRESENT] = present;
+        HIPCHK(c, hipMemcpyAsync(c->stats + ST_KEY0_PRESENT, &c->stats_h[ST_KEY0_PRESENT], 8, hipMemcpyHostToDevice,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->st.windows = win0 + vwin;  // the reads' own windows, not the padded slots'
+    }
+    if (n_reads) *n_reads = n_rec;
+    return KC_OK;
+}
+
 static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_t L, uint64_t* n_reads,
                               bool count) {
     if (!c || (!d_fastq && n > 0)) return KC_ERR_ARG;
@@ -1146,6 +1194,7 @@ static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_
     if (s) return s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     uint64_t n_rec = 0;
+    if (c->cfg.flags & KC_FLAG_VARLEN) return fastq_device_var(c, (const uint8_t*)d_fastq, n, L, n_reads, count);
     bool enc = false;
     if ((s = index_fastq(c, (const uint8_t*)d_fastq, n, L, &n_rec, count ? &enc : nullptr))) return s;
     if (count && (s = count_reads(c, (const uint8_t*)d_fastq, enc ? nullptr : (const uint64_t*)c->seq_off.p, n_rec, L,

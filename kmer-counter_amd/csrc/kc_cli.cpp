@@ -9,7 +9,8 @@
 // keys are ignored, the last occurrence wins. Additive keys (not in the
 // reference): gpus=N, exchange=none|alltoall (key-space exchange between the
 // GPUs' runs, output by concatenation; runs that spilled fall back to the
-// k-way merge), inputMode=auto|fastq|exact, tableBytes=B, quiet=1.
+// k-way merge), inputMode=auto|fastq|exact, tableBytes=B, quiet=1,
+// readLengths=fixed|variable.
 //
 // Input (InputFileHandler.cpp:22-47): every directory entry whose name does
 // not start with '.', in readdir order; L of a file = length of its line 2
@@ -21,6 +22,11 @@
 //                     KMerCounter::GetChunkSize) and sends them with
 //                     kc_count_chunk — bit-exact even on malformed input.
 //   inputMode=auto  : fastq when every block of the file validates, else exact.
+//   readLengths=variable : reads of any length up to the file's longest
+//                     sequence line, each counted as a reference read of its
+//                     own length (KC_FLAG_VARLEN; SURVEY §8f row 1 — an
+//                     extension, the reference has no defined result there).
+//                     Always the fastq mode; a malformed file is an error.
 // Output: the SortedKMerFile (sorted, deduplicated records), see include/kc.h.
 #include <dirent.h>
 #include <fcntl.h>
@@ -56,6 +62,7 @@ struct Options {
     std::string input_mode = "auto";
     uint64_t table_bytes = 0;
     bool quiet = false;
+    bool varlen = false;
 };
 
 bool starts(const char* s, const char* p) { return strncmp(s, p, strlen(p)) == 0; }
@@ -97,6 +104,7 @@ Options parse(int argc, char** argv) {
         if (starts(a, "exchange=")) o.exchange = a + 9;
         if (starts(a, "tableBytes=")) o.table_bytes = strtoull(a + 11, nullptr, 10);
         if (starts(a, "quiet=")) o.quiet = atoi(a + 6) != 0;
+        if (starts(a, "readLengths=")) o.varlen = strcmp(a + 12, "variable") == 0;
     }
     if (o.gpus < 1) o.gpus = 1;
     if (o.exchange != "none" && o.exchange != "alltoall") {
@@ -178,6 +186,20 @@ std::vector<InputFile> list_inputs(const std::string& dir) {
     }
     closedir(d);
     return v;
+}
+
+// Longest sequence line (line 2 of every 4-line record) of a FASTQ text.
+int64_t max_seq_line(const char* p, size_t n) {
+    int64_t best = 0;
+    size_t pos = 0, line = 0;
+    while (pos < n) {
+        const char* nl = (const char*)memchr(p + pos, '\n', n - pos);
+        const size_t end = nl ? (size_t)(nl - p) : n;
+        if (line % 4 == 1 && (int64_t)(end - pos) > best) best = (int64_t)(end - pos);
+        line++;
+        pos = end + 1;
+    }
+    return best;
 }
 
 struct Mapped {
@@ -335,7 +357,7 @@ int main(int argc, char** argv) {
         cfg.gpu_memory_limit = (uint64_t)o.gpu_memory_limit;
         cfg.table_bytes = o.table_bytes;
         cfg.temp_dir = o.temp_dir.c_str();
-        cfg.flags = o.quiet ? KC_FLAG_QUIET : KC_FLAG_NONE;
+        cfg.flags = (o.quiet ? KC_FLAG_QUIET : KC_FLAG_NONE) | (o.varlen ? KC_FLAG_VARLEN : KC_FLAG_NONE);
         gw[g].gpu = g;
         kc_status s = kc_create(&gw[g].ctx, &cfg);
         if (s) die(nullptr, s, "cannot create device context");
@@ -347,17 +369,22 @@ int main(int argc, char** argv) {
         int64_t L;
     };
     size_t next_block = 0;
-    for (const InputFile& f : files) {
-        if (f.L < o.kmer_length) continue;
-        bool exact = o.input_mode == "exact";
+    for (const InputFile& file : files) {
+        InputFile f = file;
+        if (!o.varlen && f.L < o.kmer_length) continue;
+        bool exact = o.input_mode == "exact" && !o.varlen;
         Mapped m;
         if (!exact) {
             if (!m.map(f.path)) die(nullptr, KC_ERR_IO, f.path.c_str());
             if (m.n == 0) continue;
         }
+        if (o.varlen) {
+            f.L = max_seq_line(m.p, m.n);  // every read fits a slot of the longest one
+            if (f.L < o.kmer_length) continue;
+        }
         std::vector<std::pair<size_t, size_t>> blocks;
         if (!exact) blocks = fastq_blocks(m.p, m.n, (size_t)1 << 30);
-        if (!exact && o.input_mode == "auto" && blocks.size() > 1) {
+        if (!exact && o.input_mode == "auto" && blocks.size() > 1 && !o.varlen) {
             // validate every block before counting anything from the file
             kc_ctx* c = gw[0].ctx;
             for (auto& b : blocks) {
@@ -391,7 +418,7 @@ int main(int argc, char** argv) {
             }
             for (auto& t : th) t.join();
             for (int g = 0; g < o.gpus; g++) {
-                if (st[g] == KC_ERR_FORMAT && o.input_mode == "auto" && blocks.size() == 1) {
+                if (st[g] == KC_ERR_FORMAT && o.input_mode == "auto" && blocks.size() == 1 && !o.varlen) {
                     fallback = true;  // a single block validates before counting
                 } else if (st[g]) {
                     die(gw[g].ctx, st[g], f.path.c_str());

@@ -22,6 +22,8 @@ enum Stat : int {
     ST_DESC_FILL = 11,   // P5 segment descriptors written (may exceed capacity)
     ST_P5_KEYS = 12,     // skm P5 sample launch: keys of the sampled buckets
     ST_DEDUP = 13,       // skm P5a: distinct records listed (raw buckets: their records)
+    ST_VHOLE = 14,       // variable-length reads: a read of >= k bases holds a not-ACGT base
+    ST_VWIN = 15,        // variable-length reads: windows of the reads' own lengths
     ST_N = 16
 };
 
@@ -62,6 +64,15 @@ struct CountLaunch {
 // r * groups_per_read(L). P1 and P2 read these instead of the FASTQ text.
 int groups_per_read(int L);
 hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s);
+// Variable-length reads (KC_FLAG_VARLEN): read r = text [seq_off[r], seq_end[r])
+// of at most L bases, encoded as a read of L bases whose positions past its
+// own end are not-ACGT with code 0 (no window reaches them; a key's bases past
+// the read end read as 0). Sets ERR_FQ_SEQ_LEN for a read longer than L,
+// stats[ST_VHOLE] when a read of >= k bases holds a not-ACGT base, adds the
+// reads' own windows to stats[ST_VWIN].
+hipError_t launch_encode_reads_var(const uint8_t* base, const uint64_t* seq_off, const uint64_t* seq_end,
+                                   uint64_t n_reads, int L, int k, uint32_t* codes, uint16_t* inval, uint64_t* stats,
+                                   hipStream_t s);
 
 // Tile geometry of count_kmers for (L, k); also used to size dynamic LDS.
 struct CountGeom {

@@ -840,6 +840,78 @@ hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* 
     return hipGetLastError();
 }
 
+// E for variable-length reads (KC_FLAG_VARLEN): one thread per (read, 16-base
+// group) of an L-base slot; the read's own bytes as in encode_reads_k, the
+// slot past its end marked not-ACGT with code 0, so the read counts exactly
+// the windows of a reference read of its own length (GPUHandler.cu:129-233 at
+// L = its length: a window needs k valid bases, key bases past the end are 0)
+__global__ __launch_bounds__(kBlock) void encode_reads_var_k(const uint8_t* __restrict__ base,
+                                                             const u64* __restrict__ seq_off,
+                                                             const u64* __restrict__ seq_end, u64 n_reads, int L,
+                                                             int G, int k, u32* __restrict__ codes,
+                                                             unsigned short* __restrict__ inval, u64* stats) {
+    const u64 total = n_reads * (u64)G;
+    bool too_long = false, hole = false;
+    u64 win = 0;
+    for (u64 it = (u64)blockIdx.x * kBlock + threadIdx.x; it < total; it += (u64)gridDim.x * kBlock) {
+        const u64 r = it / (u64)G;
+        const int g = (int)(it - r * (u64)G);
+        const u64 s0 = seq_off[r];
+        const u64 len = seq_end[r] - s0;
+        if (len > (u64)L) {
+            too_long = true;
+            codes[it] = 0u;
+            inval[it] = 0xffffu;
+            continue;
+        }
+        if (g == 0 && len >= (u64)k) win += len - (u64)k + 1;
+        const int nb = min(16, L - 16 * g);                            // bases of the slot in this group
+        const int nr = max(0, min(nb, (int)len - 16 * g));             // of them, bases of the read
+        u32 d[5] = {0u, 0u, 0u, 0u, 0u};
+        int sh = 0;
+        if (nr > 0) {
+            const uintptr_t addr = (uintptr_t)(base + s0 + 16 * (u64)g);
+            typedef __attribute__((address_space(1))) const u32 g32;
+            const g32* dw = (const g32*)(addr & ~(uintptr_t)3);
+            sh = (int)(addr & 3);
+#pragma unroll
+            for (int i = 0; i < 5; i++) d[i] = (4 * i < sh + nr) ? __builtin_nontemporal_load(dw + i) : 0u;
+        }
+        const u32 x0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+        const u32 x1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+        const u32 x2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+        const u32 x3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+        u32 b0, b1, b2, b3;
+        const u32 c0 = bytes_to_codes(x0, nr, &b0);
+        const u32 c1 = bytes_to_codes(x1, nr - 4, &b1);
+        const u32 c2 = bytes_to_codes(x2, nr - 8, &b2);
+        const u32 c3 = bytes_to_codes(x3, nr - 12, &b3);
+        const u32 bad = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
+        if (bad != 0u && len >= (u64)k) hole = true;
+        // slot positions [nr, nb) lie past the read: bits 15 - i
+        const u32 pad = ((1u << (16 - nr)) - 1u) & ~((1u << (16 - nb)) - 1u);
+        codes[it] = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+        inval[it] = (unsigned short)(bad | pad);
+    }
+    if (__ballot(too_long) && lane_id() == 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_FQ_SEQ_LEN);
+    if (__ballot(hole) && lane_id() == 0) atomicOr((unsigned long long*)&stats[ST_VHOLE], 1ull);
+    for (int o = 32; o >= 1; o >>= 1) win += __shfl_xor(win, o);
+    if (lane_id() == 0 && win) atomicAdd((unsigned long long*)&stats[ST_VWIN], (unsigned long long)win);
+}
+
+hipError_t launch_encode_reads_var(const uint8_t* base, const uint64_t* seq_off, const uint64_t* seq_end,
+                                   uint64_t n_reads, int L, int k, uint32_t* codes, uint16_t* inval, uint64_t* stats,
+                                   hipStream_t s) {
+    if (n_reads == 0) return hipSuccess;
+    if (L < 1 || k < 1) return hipErrorInvalidValue;
+    const int G = groups_per_read(L);
+    const u64 total = n_reads * (u64)G;
+    const int grid = (int)hmin((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(encode_reads_var_k, dim3(grid), dim3(kBlock), 0, s, base, (const u64*)seq_off,
+                       (const u64*)seq_end, n_reads, L, G, k, codes, (unsigned short*)inval, (u64*)stats);
+    return hipGetLastError();
+}
+
 // P2 workgroup: kP2Block threads, one per CU, most of the CU's LDS for staging
 constexpr int kP2Block = 1024;
 constexpr size_t kPartLds = 152 * 1024;  // + alignment and the sink's fixed arrays stays under 160 KiB

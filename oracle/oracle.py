@@ -93,6 +93,29 @@ def count_chunks(chunks, k: int, mode: str = "spec") -> bytes:
     return res
 
 
+def fastq_sequences(data: bytes):
+    """Sequence lines (line 2 of every 4-line record) of well-formed FASTQ."""
+    lines = data.split(b"\n")
+    return [lines[i] for i in range(1, len(lines) - 1, 4)]
+
+
+def count_fastq_varlen(data: bytes, k: int, mode: str = "spec") -> bytes:
+    """Variable-length reads (KC_FLAG_VARLEN): every read
+    counted as a reference chunk of that one read with L = its own length
+    (processKMers semantics per read, GPUHandler.cu:397-466; a read shorter
+    than k contributes nothing). Runs of equal-length reads share a chunk."""
+    chunks, run, run_len = [], [], -1
+    for s in fastq_sequences(data):
+        if len(s) != run_len and run:
+            chunks.append((b"".join(run), run_len))
+            run = []
+        run_len = len(s)
+        run.append(s)
+    if run:
+        chunks.append((b"".join(run), run_len))
+    return count_chunks([(c, ll) for c, ll in chunks if ll >= k], k, mode)
+
+
 def refcpu(data: bytes, k: int, gpu_memory_limit: int = 100000000, threads: int = 1):
     """The reference pipeline on the CPU (chunker + ref-structured encode/extract
     + adjacent reduce + sharded-lock hash + sort). Returns (bytes, windows)."""
