@@ -10,7 +10,7 @@
 // reference): gpus=N, exchange=none|alltoall (key-space exchange between the
 // GPUs' runs, output by concatenation; runs that spilled fall back to the
 // k-way merge), inputMode=auto|fastq|exact, tableBytes=B, quiet=1,
-// readLengths=fixed|variable.
+// readLengths=fixed|variable, outputFormat=sorted|dump.
 //
 // Input (InputFileHandler.cpp:22-47): every directory entry whose name does
 // not start with '.', in readdir order; L of a file = length of its line 2
@@ -28,6 +28,14 @@
 //                     extension, the reference has no defined result there).
 //                     Always the fastq mode; a malformed file is an error.
 // Output: the SortedKMerFile (sorted, deduplicated records), see include/kc.h.
+//   outputFormat=dump : the record layout of the reference's active path,
+//                     KMerCounter::DumpResults (KMerCounter.cpp:91-106): key
+//                     word 0 (8 B LE) + count (4 B LE) per distinct key, for
+//                     k > 32 truncated to word 0 as the reference does (keys
+//                     that differ only past base 32 stay separate records).
+//                     Records are in key order (the reference's TBB hash order
+//                     is not reproducible); for k <= 32 the bytes equal the
+//                     sorted output.
 #include <dirent.h>
 #include <fcntl.h>
 #include <inttypes.h>
@@ -63,6 +71,7 @@ struct Options {
     uint64_t table_bytes = 0;
     bool quiet = false;
     bool varlen = false;
+    bool dump = false;
 };
 
 bool starts(const char* s, const char* p) { return strncmp(s, p, strlen(p)) == 0; }
@@ -105,6 +114,7 @@ Options parse(int argc, char** argv) {
         if (starts(a, "tableBytes=")) o.table_bytes = strtoull(a + 11, nullptr, 10);
         if (starts(a, "quiet=")) o.quiet = atoi(a + 6) != 0;
         if (starts(a, "readLengths=")) o.varlen = strcmp(a + 12, "variable") == 0;
+        if (starts(a, "outputFormat=")) o.dump = strcmp(a + 13, "dump") == 0;
     }
     if (o.gpus < 1) o.gpus = 1;
     if (o.exchange != "none" && o.exchange != "alltoall") {
@@ -300,6 +310,36 @@ class ExactChunker {
     bool done_ = false;
 };
 
+// outputFormat=dump for k > 32: rewrites the SortedKMerFile in place as word 0
+// + count per record (DumpResults, KMerCounter.cpp:96-103).
+bool to_dump_format(const std::string& path, int W) {
+    if (W == 1) return true;  // the same bytes
+    const size_t rs = 8 * (size_t)W + 4;
+    FILE* in = fopen(path.c_str(), "rb");
+    if (!in) return false;
+    const std::string tmp = path + ".dump.tmp";
+    FILE* out = fopen(tmp.c_str(), "wb");
+    if (!out) {
+        fclose(in);
+        return false;
+    }
+    std::vector<unsigned char> ib(rs * 65536), ob(12 * 65536);
+    bool ok = true;
+    for (;;) {
+        const size_t got = fread(ib.data(), 1, ib.size(), in);
+        const size_t nrec = got / rs;
+        for (size_t r = 0; r < nrec; r++) {
+            memcpy(ob.data() + 12 * r, ib.data() + rs * r, 8);
+            memcpy(ob.data() + 12 * r + 8, ib.data() + rs * r + 8 * W, 4);
+        }
+        if (nrec && fwrite(ob.data(), 1, 12 * nrec, out) != 12 * nrec) ok = false;
+        if (got < ib.size()) break;
+    }
+    fclose(in);
+    if (fclose(out) || !ok) return false;
+    return rename(tmp.c_str(), path.c_str()) == 0;
+}
+
 void die(kc_ctx* c, kc_status s, const char* what) {
     fprintf(stderr, "kmer-counter: %s: %s%s%s\n", what, kc_strerror(s), c ? ": " : "", c ? kc_last_error(c) : "");
     exit(1);
@@ -483,6 +523,8 @@ int main(int argc, char** argv) {
         for (auto& p : all) unlink(p.c_str());
         if (s) die(nullptr, s, "merge");
     }
+    if (o.dump && !to_dump_format(o.output_file, (int)((o.kmer_length + 31) / 32)))
+        die(nullptr, KC_ERR_IO, o.output_file.c_str());
     for (auto& w : gw) {
         if (!o.quiet) {
             kc_stats st;
