@@ -16,6 +16,11 @@ step. `--exchange none` is the read-shard mode (cfg3): no collective, the
 per-GPU runs are left for the host k-way merge (not timed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--exchange alltoall|none] [--no-cpu]
+                    [--min-read-length M]
+
+--min-read-length M (0 < M < L): variable-length input (SURVEY §8f row 1,
+KC_FLAG_VARLEN): read i keeps its first M..L bases (generator in
+kc_synth.h); k-mers per step = the reads' own windows (kc_stats.windows).
 
 Prints one JSON line on rank 0 (contract in the task statement).
 """
@@ -58,6 +63,24 @@ def cpu_baseline(kca, reads, L, k, genome, seed, first, threads=None):
                       f"gpuMemoryLimit=1e8, bitEncode/extractKMers/reduceKMers restated, hash insert into a "
                       f"sharded-lock table standing in for TBB); timed up to the complete table, as the "
                       f"reference's DumpResults writes in hash order; {threads} threads, {dt:.2f} s"}
+
+
+def cpu_baseline_varlen(kca, reads, L, lmin, k, genome, seed):
+    """Variable-length input has no reference pipeline to port (the reference
+    concatenates reads without separators): the CPU baseline is the oracle's
+    per-read statement (spec form, one thread, sorted output) on a sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: timed as the CPU baseline only
+
+    fq = kca.synth_fastq(reads, L, seed, genome_length=genome, min_read_length=lmin)
+    windows = sum(max(0, len(s) - k + 1) for s in oracle.fastq_sequences(fq))
+    t0 = time.perf_counter()
+    out = oracle.count_fastq_varlen(fq, k)
+    dt = time.perf_counter() - t0
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": f"{reads} reads of {lmin}..{L} bp of the same workload ({windows} k-mers, "
+                      f"{len(out) // (8 * ((k + 31) // 32) + 4)} distinct): oracle count_fastq_varlen (each read "
+                      f"as a reference chunk of its own length, spec form, sorted output); 1 thread, {dt:.2f} s"}
 
 
 def shard_first(rank: int, reads_per_gpu: int) -> int:
@@ -105,6 +128,8 @@ def main():
     ap.add_argument("--engine", default="auto", choices=["auto", "skm", "partition", "table"])
     ap.add_argument("--cpu-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--min-read-length", type=int, default=0,
+                    help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
     ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
                     help="N>1: key-space all-to-all (cfg4) or read-shard only (cfg3); ignored at N=1")
     args = ap.parse_args()
@@ -134,9 +159,12 @@ def main():
     if world > 1:
         import torch
         device = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
-    ctx = kca.Context(kmer_length=k, line_length=L, device=device, gpu_memory_limit=args.mem, engine=args.engine)
+    varlen = 0 < args.min_read_length < L
+    ctx = kca.Context(kmer_length=k, line_length=L, device=device, gpu_memory_limit=args.mem, engine=args.engine,
+                      variable_length=varlen)
     first = shard_first(rank, args.reads)
-    ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first)
+    ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first,
+                                   args.min_read_length if varlen else 0)
 
     exchange = args.exchange if world > 1 else "none"
     xdev = None
@@ -190,7 +218,14 @@ def main():
         import torch
         dev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
         elapsed = max_over_ranks(dist, elapsed, dev)
-    windows_per_gpu = args.reads * (L - k + 1)
+    # variable-length reads: the reads' own windows (ctx stats are per step)
+    windows_per_gpu = st["windows"] if varlen else args.reads * (L - k + 1)
+    if dist is not None and varlen:
+        import torch
+        dev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
+        t = torch.tensor([float(windows_per_gpu)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        windows_per_gpu = t.item() / world
     total_kmers = windows_per_gpu * world * args.steps
     value = total_kmers / elapsed
 
@@ -287,17 +322,21 @@ def main():
                 "path_bytes_per_kmer": round(b_path, 3), "kernels": kernels}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and varlen:
+        cpu = cpu_baseline_varlen(kca, max(1, args.cpu_reads // 20), L, args.min_read_length, k, args.genome,
+                                  args.seed)
+    elif rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(kca, args.cpu_reads, L, k, args.genome, args.seed, 0)
         t1 = cpu_baseline(kca, max(1, args.cpu_reads // 10), L, k, args.genome, args.seed, 0, threads=1)
         cpu["value_t1"] = t1["value"]
         cpu["sample_t1"] = t1["sample"]
 
     src = (f"sampled from a {args.genome} bp random genome" if args.genome else "of iid uniform bases")
-    base = (f"k={k}, {args.reads} x {L} bp reads per GPU {src} (seed {args.seed}), FASTQ in HBM, "
+    lens = f"{args.min_read_length}..{L} bp (variable-length, KC_FLAG_VARLEN)" if varlen else f"{L} bp"
+    base = (f"k={k}, {args.reads} x {lens} reads per GPU {src} (seed {args.seed}), FASTQ in HBM, "
             f"in-HBM count")
     if world == 1:
-        workload, parallelism = f"cfg{args.config}: " + base, "single GPU"
+        workload, parallelism = f"cfg{args.config}{'v' if varlen else ''}: " + base, "single GPU"
     elif exchange == "alltoall":
         workload = (f"cfg4 pattern at {world} GPUs: " + base + "; key-space all-to-all of the sorted (key, count) "
                     "records + per-GPU merge inside the step (output = concatenation of the ranks' runs)")

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define KC_ABI_VERSION 2 /* 2: kc_stats.dedup_ms / dedup_records */
+#define KC_ABI_VERSION 3 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length */
 #define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
 
 typedef enum kc_status {
@@ -167,6 +167,11 @@ typedef struct kc_synth_spec {
                               random genome of this many bases */
     double n_rate;         /* probability that a base is replaced by 'N' */
     uint64_t first_read;   /* index of the first record to emit (for sharding) */
+    int64_t min_read_length; /* 0 = every read has read_length bases; in
+                              [1, read_length): read i keeps its first
+                              min + rand(i) mod (read_length - min + 1) bases
+                              and its header is padded with 'x' to keep the
+                              record size (variable-length input, KC_FLAG_VARLEN) */
 } kc_synth_spec;
 
 /* ---- lifecycle ---------------------------------------------------------- */

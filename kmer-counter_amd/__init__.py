@@ -95,6 +95,7 @@ class _Synth(ctypes.Structure):
         ("genome_length", ctypes.c_uint64),
         ("n_rate", ctypes.c_double),
         ("first_read", ctypes.c_uint64),
+        ("min_read_length", ctypes.c_int64),
     ]
 
 
@@ -157,15 +158,15 @@ def lib() -> ctypes.CDLL:
     return L
 
 
-def _spec(n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0):
-    return _Synth(n_reads, read_length, seed, genome_length, n_rate, first_read)
+def _spec(n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0, min_read_length=0):
+    return _Synth(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length)
 
 
 def synth_fastq(n_reads: int, read_length: int, seed: int, genome_length: int = 0, n_rate: float = 0.0,
-                first_read: int = 0) -> bytes:
+                first_read: int = 0, min_read_length: int = 0) -> bytes:
     """Synthetic FASTQ text (SURVEY §8d generator) produced by the library's host generator."""
     L = lib()
-    sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read)
+    sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length)
     n = L.kc_synth_fastq_bytes(ctypes.byref(sp))
     buf = ctypes.create_string_buffer(n + 1)
     st = L.kc_synth_fastq_host(ctypes.byref(sp), buf, n + 1)
@@ -251,9 +252,10 @@ class Context:
         self._chk(self._L.kc_count_fastq_device(self._h, ctypes.c_void_p(ptr), size, line_length, ctypes.byref(n)))
         return n.value
 
-    def synth_device(self, n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0):
+    def synth_device(self, n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0,
+                     min_read_length=0):
         """Generates synthetic FASTQ directly in device memory; returns (ptr, nbytes)."""
-        sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read)
+        sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length)
         p = ctypes.c_void_p()
         n = ctypes.c_uint64()
         self._chk(self._L.kc_synth_fastq_device(self._h, ctypes.byref(sp), ctypes.byref(p), ctypes.byref(n)))

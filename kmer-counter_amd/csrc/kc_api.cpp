@@ -1680,13 +1680,15 @@ static SynthArgs synth_args(const kc_synth_spec* sp) {
     a.seed = sp->seed;
     a.genome = sp->genome_length;
     a.L = sp->read_length;
+    a.Lmin = sp->min_read_length;
     double thr = sp->n_rate * 9007199254740992.0;
     a.n_threshold = sp->n_rate <= 0 ? 0 : (thr >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)thr);
     return a;
 }
 
 static bool synth_ok(const kc_synth_spec* sp) {
-    return sp && sp->read_length > 0 && (sp->genome_length == 0 || sp->genome_length >= (uint64_t)sp->read_length);
+    return sp && sp->read_length > 0 && (sp->genome_length == 0 || sp->genome_length >= (uint64_t)sp->read_length) &&
+           sp->min_read_length >= 0 && sp->min_read_length <= sp->read_length;
 }
 
 kc_status kc_synth_fastq_host(const kc_synth_spec* sp, char* dst, uint64_t dst_bytes) {

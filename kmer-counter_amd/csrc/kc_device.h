@@ -265,6 +265,7 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
 struct SynthArgs {
     uint64_t first, n, seed, genome, n_threshold;
     int64_t L;
+    int64_t Lmin = 0;  // variable read lengths in [Lmin, L] (0: fixed)
 };
 hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s);
 void synth_host(const SynthArgs& a, char* out);

@@ -3662,6 +3662,7 @@ static kc_synth_params to_params(const SynthArgs& a) {
     p.genome = a.genome;
     p.n_threshold = a.n_threshold;
     p.L = a.L;
+    p.Lmin = a.Lmin;
     return p;
 }
 

@@ -13,6 +13,10 @@
 //       rand(seed, 4, i*ceil(L/32) + j/32).
 //   N replacement: base j of read i becomes 'N' when
 //       (rand(seed, 3, i*L + j) >> 11) < n_threshold,  n_threshold = n_rate * 2^53.
+//   Variable read lengths (Lmin in [1, L)): read i keeps its first
+//       len_i = Lmin + rand(seed, 5, i) mod (L - Lmin + 1) bases (sequence and
+//       quality lines), and its header gains 2 (L - len_i) 'x' bytes, so every
+//       record keeps the fixed-length record's size and offset.
 #pragma once
 #include <stdint.h>
 
@@ -61,7 +65,13 @@ KC_SYNTH_HD uint64_t kc_synth_offset(uint64_t first, uint64_t i, int64_t L) {
 struct kc_synth_params {
     uint64_t first, n, seed, genome, n_threshold;
     int64_t L;
+    int64_t Lmin;  // 0: every read has L bases
 };
+
+KC_SYNTH_HD int64_t kc_synth_len(const kc_synth_params& p, uint64_t i) {
+    if (p.Lmin <= 0 || p.Lmin >= p.L) return p.L;
+    return p.Lmin + (int64_t)(kc_synth_rand(p.seed, 5, i) % (uint64_t)(p.L - p.Lmin + 1));
+}
 
 KC_SYNTH_HD char kc_synth_base(const kc_synth_params& p, uint64_t i, int64_t j, uint64_t pos) {
     uint32_t c;
@@ -89,13 +99,15 @@ KC_SYNTH_HD void kc_synth_record(const kc_synth_params& p, uint64_t i, char* dst
     *o++ = '@';
     *o++ = 'r';
     while (nd) *o++ = digits[--nd];
+    const int64_t len = kc_synth_len(p, i);
+    for (int64_t j = 0; j < 2 * (p.L - len); j++) *o++ = 'x';
     *o++ = '\n';
     uint64_t pos = 0;
     if (p.genome > 0) pos = kc_synth_rand(p.seed, 1, i) % (p.genome - (uint64_t)p.L + 1);
-    for (int64_t j = 0; j < p.L; j++) *o++ = kc_synth_base(p, i, j, pos);
+    for (int64_t j = 0; j < len; j++) *o++ = kc_synth_base(p, i, j, pos);
     *o++ = '\n';
     *o++ = '+';
     *o++ = '\n';
-    for (int64_t j = 0; j < p.L; j++) *o++ = 'I';
+    for (int64_t j = 0; j < len; j++) *o++ = 'I';
     *o++ = '\n';
 }

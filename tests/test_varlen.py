@@ -166,3 +166,24 @@ def test_varlen_cli(kca, orc, tmp_path):
     subprocess.run([cli, "kmerLength=25", f"inputFileLocation={d}", f"outputFile={out}", f"tempFileLocation={tmp_path}",
                     "readLengths=variable", "quiet=1"], check=True, capture_output=True, timeout=300)
     assert out.read_bytes() == orc.count_fastq_varlen(fa + fb, 25)
+
+
+def test_synth_varlen_generator(kca, orc):
+    fixed = kca.synth_fastq(300, 120, 4, genome_length=10_000)
+    var = kca.synth_fastq(300, 120, 4, genome_length=10_000, min_read_length=40)
+    assert len(var) == len(fixed)  # headers absorb the trimmed bases
+    seqs, fseqs = orc.fastq_sequences(var), orc.fastq_sequences(fixed)
+    assert all(40 <= len(s) <= 120 for s in seqs) and len({len(s) for s in seqs}) > 20
+    assert all(f.startswith(s) for s, f in zip(seqs, fseqs))  # a read keeps its first bases
+
+
+@pytest.mark.gpu
+def test_varlen_gpu_synth_device(kca, orc):
+    host = kca.synth_fastq(20000, 150, 6, genome_length=400_000, min_read_length=50)
+    with kca.Context(kmer_length=31, line_length=150, variable_length=True) as ctx:
+        ptr, n = ctx.synth_device(20000, 150, 6, 400_000, 0.0, 0, 50)
+        assert ctx.copy_to_host(ptr, n) == host
+        ctx.count_fastq_device(ptr, n, 150)
+        got = ctx.records()
+        ctx.free_device(ptr)
+    assert got == orc.count_fastq_varlen(host, 31)
