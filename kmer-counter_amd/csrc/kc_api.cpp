@@ -74,6 +74,8 @@ struct kc_ctx {
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_dedup;  // skm P5a: per-bucket list starts (u64) and lengths (u32), list cursor
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
+    DevBuf part_rlen;               // KC_FLAG_VARLEN: each read's own length (u16)
+    const uint16_t* var_rlen = nullptr;  // set while a variable-length block is counted
     // P5 segment descriptors (see finish_part_sorted) and their sort scratch
     DevBuf desc_key, desc_start, desc_len, desc_k2, desc_v, desc_v2, desc_lens, desc_offs, desc_fb;
     uint64_t* rec_keys = nullptr;  // W x rec_cap
@@ -671,6 +673,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         const uint64_t g0 = pre0 < 0 ? 0 : ((uint64_t)pre0 + done) * G;
         l.codes = (const uint32_t*)c->part_codes.p + g0;
         l.inval = (const uint16_t*)c->part_inval.p + g0;
+        l.rlen = (pre0 >= 0 && c->var_rlen) ? c->var_rlen + (uint64_t)pre0 + done : nullptr;
         if ((s = sync_stats(c))) return s;
         std::vector<uint64_t> saved(c->stats_h, c->stats_h + ST_N);
         HIPCHK(c, hipMemsetAsync(c->pool_cursor, 0, 8, c->stream));
@@ -911,11 +914,14 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
         if (varlen) {
             // sequence lengths up to L, checked (and the reads encoded) by E-var
             const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
-            if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
+            if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16)) ||
+                (s = ensure(c, c->part_rlen, n_rec * 2 + 16)))
+                return s;
             HIPCHK(c, hipMemsetAsync(c->stats + ST_VHOLE, 0, 16, c->stream));
             HIPCHK(c, launch_encode_reads_var(base, (const uint64_t*)c->seq_off.p, (const uint64_t*)c->seq_end.p, n_rec,
                                               (int)L, (int)c->k, (uint32_t*)c->part_codes.p,
-                                              (uint16_t*)c->part_inval.p, c->stats, c->stream));
+                                              (uint16_t*)c->part_inval.p, (uint16_t*)c->part_rlen.p, c->stats,
+                                              c->stream));
         } else {
             HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
                                          c->stream));
@@ -1075,6 +1081,7 @@ void kc_destroy(kc_ctx* c) {
     release(c->part_hist);
     release(c->part_codes);
     release(c->part_inval);
+    release(c->part_rlen);
     DevBuf* dbufs[] = {&c->desc_key, &c->desc_start, &c->desc_len, &c->desc_k2, &c->desc_v, &c->desc_v2,
                        &c->desc_lens, &c->desc_offs, &c->desc_fb};
     for (DevBuf* b : dbufs) release(*b);
@@ -1170,7 +1177,10 @@ static kc_status fastq_device_var(kc_ctx* c, const uint8_t* base, uint64_t n, in
         const uint64_t present0 = c->stats_h[ST_KEY0_PRESENT];
         const uint64_t vhole = c->stats_h[ST_VHOLE], vwin = c->stats_h[ST_VWIN];
         const uint64_t win0 = c->st.windows;
-        if ((s = count_reads(c, base, nullptr, n_rec, L, 0))) return s;
+        c->var_rlen = (const uint16_t*)c->part_rlen.p;
+        s = count_reads(c, base, nullptr, n_rec, L, 0);
+        c->var_rlen = nullptr;
+        if (s) return s;
         if ((s = sync_stats(c))) return s;
         const uint64_t present = (present0 | vhole | (c->stats_h[ST_KEY0] != 0 ? 1u : 0u)) ? 1u : 0u;
         c->stats_h[ST_KEY0_PRESENT] = present;

@@ -57,6 +57,7 @@ struct CountLaunch {
     uint32_t probe_limit;
     const uint32_t* codes = nullptr;   // partition engine: reads encoded by kernel E
     const uint16_t* inval = nullptr;   //   (groups_per_read(L) words per read)
+    const uint16_t* rlen = nullptr;    // KC_FLAG_VARLEN: each read's own length (<= L), read r at rlen[r]
 };
 
 // E: encode the launch's reads once into 2-bit codes (u32 per 16 bases, first
@@ -70,9 +71,10 @@ hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* 
 // the read end read as 0). Sets ERR_FQ_SEQ_LEN for a read longer than L,
 // stats[ST_VHOLE] when a read of >= k bases holds a not-ACGT base, adds the
 // reads' own windows to stats[ST_VWIN].
+// rlen (may be nullptr): each read's own length.
 hipError_t launch_encode_reads_var(const uint8_t* base, const uint64_t* seq_off, const uint64_t* seq_end,
-                                   uint64_t n_reads, int L, int k, uint32_t* codes, uint16_t* inval, uint64_t* stats,
-                                   hipStream_t s);
+                                   uint64_t n_reads, int L, int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen,
+                                   uint64_t* stats, hipStream_t s);
 
 // Tile geometry of count_kmers for (L, k); also used to size dynamic LDS.
 struct CountGeom {

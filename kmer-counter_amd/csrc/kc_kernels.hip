@@ -11,6 +11,7 @@
 
 #include "kc_device.h"
 #include <cstdlib>
+#include <type_traits>
 #include "kc_synth.h"
 
 namespace kc {
@@ -849,7 +850,8 @@ __global__ __launch_bounds__(kBlock) void encode_reads_var_k(const uint8_t* __re
                                                              const u64* __restrict__ seq_off,
                                                              const u64* __restrict__ seq_end, u64 n_reads, int L,
                                                              int G, int k, u32* __restrict__ codes,
-                                                             unsigned short* __restrict__ inval, u64* stats) {
+                                                             unsigned short* __restrict__ inval,
+                                                             unsigned short* __restrict__ rlen, u64* stats) {
     const u64 total = n_reads * (u64)G;
     bool too_long = false, hole = false;
     u64 win = 0;
@@ -862,8 +864,10 @@ __global__ __launch_bounds__(kBlock) void encode_reads_var_k(const uint8_t* __re
             too_long = true;
             codes[it] = 0u;
             inval[it] = 0xffffu;
+            if (rlen && g == 0) rlen[r] = 0;
             continue;
         }
+        if (rlen && g == 0) rlen[r] = (unsigned short)len;
         if (g == 0 && len >= (u64)k) win += len - (u64)k + 1;
         const int nb = min(16, L - 16 * g);                            // bases of the slot in this group
         const int nr = max(0, min(nb, (int)len - 16 * g));             // of them, bases of the read
@@ -900,15 +904,16 @@ __global__ __launch_bounds__(kBlock) void encode_reads_var_k(const uint8_t* __re
 }
 
 hipError_t launch_encode_reads_var(const uint8_t* base, const uint64_t* seq_off, const uint64_t* seq_end,
-                                   uint64_t n_reads, int L, int k, uint32_t* codes, uint16_t* inval, uint64_t* stats,
-                                   hipStream_t s) {
+                                   uint64_t n_reads, int L, int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen,
+                                   uint64_t* stats, hipStream_t s) {
     if (n_reads == 0) return hipSuccess;
     if (L < 1 || k < 1) return hipErrorInvalidValue;
     const int G = groups_per_read(L);
     const u64 total = n_reads * (u64)G;
     const int grid = (int)hmin((total + kBlock - 1) / kBlock, 65536);
     hipLaunchKernelGGL(encode_reads_var_k, dim3(grid), dim3(kBlock), 0, s, base, (const u64*)seq_off,
-                       (const u64*)seq_end, n_reads, L, G, k, codes, (unsigned short*)inval, (u64*)stats);
+                       (const u64*)seq_end, n_reads, L, G, k, codes, (unsigned short*)inval, (unsigned short*)rlen,
+                       (u64*)stats);
     return hipGetLastError();
 }
 

@@ -967,6 +967,9 @@ struct F3Args {
     unsigned char* dig1;
     u64* stats;
     int skip;  // timing experiments only (KC_F_SKIP): 1 record stores, 2 runs + records
+    // KC_FLAG_VARLEN: read r's own length (slot positions past it are
+    // not-ACGT padding in inval); nullptr: every read has L bases
+    const unsigned short* rlen;
 };
 
 // 22-bit m-mer at base I of the 32 bases {c0, c1} (I constant after unrolling)
@@ -1127,8 +1130,17 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                 const u32 iv = (stage[ngw + (it >> 1)] >> (16 * (it & 1))) & 0xffffu;
                 const int r = (int)div_g.div((u32)it), g = it - r * G;
                 codes[r * NG + g] = cw;
-                const bool za = ((cw >> 16) == 0u && 16 * g + 8 <= L) || ((cw & 0xffffu) == 0u && 16 * g + 16 <= L);
-                const u32 f = (iv ? 1u : 0u) | (za ? 2u : 0u);
+                int lr = L;  // the read's own length
+                u32 ivr = iv;
+                if (a.rlen) {
+                    // a variable-length read: the padding past its end is no
+                    // bad base (its windows end with the read, below)
+                    lr = (int)a.rlen[r0 + (u64)r];
+                    const int o = lr - 16 * g;
+                    ivr = o >= 16 ? iv : (o <= 0 ? 0u : iv & ~((1u << (16 - o)) - 1u));
+                }
+                const bool za = ((cw >> 16) == 0u && 16 * g + 8 <= lr) || ((cw & 0xffffu) == 0u && 16 * g + 16 <= lr);
+                const u32 f = (ivr ? 1u : 0u) | (za ? 2u : 0u);
                 if (f) atomicOr(&rflag[r], f);
             }
         }
@@ -1147,6 +1159,12 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
         for (int i = 0; i < (D > 0 ? D : 1); i++) St[i] = ~0u;
         const bool fast = !slow && !(a.skip & 2);
         const bool live = lane < nr;
+        // windows of the lane's read (variable-length reads: its own; windows
+        // from nwr on are not windows, their bucket is kNoKey); vt: a read of
+        // the tile is shorter than the slot (wave-uniform)
+        int nwr = nw;
+        if (a.rlen && live) nwr = max(0, (int)a.rlen[r0 + (u64)lane] - K + 1);
+        const bool vt = a.rlen != nullptr && __builtin_amdgcn_ballot_w64(live && nwr < nw) != 0ull;
         const int g_lo = (E + 1 + 15) / 16;                  // first block whose windows are all >= 1
         const int g_hi = np >= 16 ? (np - 16) / 16 + 1 : 0;  // blocks ending before np
         u32 c0 = crow[0];
@@ -1155,8 +1173,9 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
             // interior block of a tile without flagged reads: every window
             // exists (w >= 1) and is live, no per-window branch; lanes without a
             // run to push write their spare ring slot
-            auto fast_block = [&](auto tag) {
+            auto fast_block = [&](auto tag, auto vtag) {
                 constexpr int OFF = decltype(tag)::value;
+                constexpr bool VT = decltype(vtag)::value;
                 const int p0 = 16 * g + OFF;
                 u32 h[B];
 #pragma unroll
@@ -1171,8 +1190,9 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                         v = min(min(St[j], Sp[0]), P);
                     else
                         v = min(Sp[j - D], P);
-                    const u32 u = min(v & 0xffffu, kNoKey - 1u);
+                    u32 u = min(v & 0xffffu, kNoKey - 1u);
                     const u32 w = wv0 + (u32)j;
+                    if constexpr (VT) u = (int)w < nwr ? u : kNoKey;
                     const bool bnd = u != prev;
                     const u64 pm = __builtin_amdgcn_ballot_w64(bnd) & livem;
                     const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0u)) + qn;
@@ -1216,17 +1236,19 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                         else
                             v = min(Sp[j - D], P);
                         u32 u = min(v & 0xffffu, kNoKey - 1u);
+                        const bool beyond = vt && w >= nwr;  // past a variable-length read's windows
                         if (slow) {
                             const bool dead = (deadm >> j) & 1u;
                             bool zero = false;
-                            if ((fl & 2u) && !dead) zero = (f2_code_word(crow, w) & C2::LAST_MASK) == 0ull;
+                            if ((fl & 2u) && !dead && !beyond) zero = (f2_code_word(crow, w) & C2::LAST_MASK) == 0ull;
                             if (lane < nr) {
-                                my_valid += dead ? 0u : 1u;
+                                my_valid += (dead || beyond) ? 0u : 1u;
                                 my_zero += zero ? 1u : 0u;
-                                my_hole |= dead;
+                                my_hole |= dead && !beyond;
                             }
                             if (dead || zero) u = kNoKey;
                         }
+                        if (beyond) u = kNoKey;
                         if (w == 0) {
                             s = 0;
                         } else if (!(a.skip & 2)) {
@@ -1253,8 +1275,13 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                 for (int i = B - 2; i >= 0; i--) Sp[i] = min(h[i], Sp[i + 1]);
             };
             if (fast && g >= g_lo && g < g_hi) {
-                fast_block(F3Tag<0>{});
-                if constexpr (B == 8) fast_block(F3Tag<8>{});
+                if (vt) {
+                    fast_block(F3Tag<0>{}, std::true_type{});
+                    if constexpr (B == 8) fast_block(F3Tag<8>{}, std::true_type{});
+                } else {
+                    fast_block(F3Tag<0>{}, std::false_type{});
+                    if constexpr (B == 8) fast_block(F3Tag<8>{}, std::false_type{});
+                }
             } else {
                 block(F3Tag<0>{});
                 if constexpr (B == 8) block(F3Tag<8>{});
@@ -1267,7 +1294,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
             push(ended, __builtin_amdgcn_ballot_w64(ended), nw - 1, s, prev);
         }
         while (qn) drain(min(64u, qn));
-        if (!slow && lane < nr) my_valid += (u64)nw;
+        if (!slow && lane < nr) my_valid += (u64)nwr;
         wave_sync();
     }
     // pad the rest of the wave's chunk with n = 0 records in bucket kNoKey
@@ -1437,6 +1464,7 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
             f3.pool_cursor = pool_cursor;
             f3.dig1 = dig1;
             f3.stats = l.stats;
+            f3.rlen = (const unsigned short*)l.rlen;
             {
                 const char* e = getenv("KC_F_SKIP");
                 f3.skip = e ? atoi(e) : 0;
