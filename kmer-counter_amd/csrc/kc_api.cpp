@@ -879,7 +879,7 @@ static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq
 // one batch, the emit pass also encodes every read (fq_encode: the text is read
 // twice instead of three times) and *encoded is set; seq_off is then unset.
 static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out,
-                             bool* encoded = nullptr, bool varlen = false) {
+                             bool* encoded = nullptr, bool varlen = false, bool two_pass_var = false) {
     if (encoded) *encoded = false;
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
@@ -902,11 +902,23 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
     const uint64_t nw = (uint64_t)(L - c->k + 1);
     const bool fuse = encoded && !varlen && !getenv("KC_NO_FQ_ENCODE") && L >= c->k && engine_reads_codes(c, L) &&
                       n_rec * nw <= c->key_cap;
+    // variable-length reads: the fused index + encode unless a half held more
+    // records than its list (then again with the two-pass index)
+    const bool fuse_var = varlen && !two_pass_var && !getenv("KC_NO_FQ_ENCODE");
     if (fuse) {
         const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
         if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
         HIPCHK(c, launch_fq_encode(base, n, (uint64_t*)c->fq_base.p, n_rec, (int)L, (uint32_t*)c->part_codes.p,
                                    (uint16_t*)c->part_inval.p, c->stats, c->stream));
+    } else if (fuse_var) {
+        const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
+        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16)) ||
+            (s = ensure(c, c->part_rlen, n_rec * 2 + 16)))
+            return s;
+        HIPCHK(c, hipMemsetAsync(c->stats + ST_VHOLE, 0, 16, c->stream));
+        HIPCHK(c, launch_fq_encode_var(base, n, (uint64_t*)c->fq_base.p, n_rec, (int)L, (int)c->k,
+                                       (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p,
+                                       (uint16_t*)c->part_rlen.p, c->stats, c->stream));
     } else {
         if ((s = ensure(c, c->seq_off, n_rec * 8 + 8)) || (s = ensure(c, c->seq_end, n_rec * 8 + 8))) return s;
         HIPCHK(c, launch_fq_emit(base, n, (uint64_t*)c->fq_base.p, (uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p,
@@ -933,6 +945,12 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
     c->st.decode_ms += t;
     uint64_t e = c->stats_h[ST_ERR];
+    if (fuse_var && (e & ERR_FQ_LIST)) {
+        HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->stats_h[ST_ERR] = 0;
+        return index_fastq(c, base, n, L, n_rec_out, encoded, varlen, true);
+    }
     if (e) {
         std::string why;
         if (e & ERR_FQ_NOT_AT) why += " record-does-not-start-with-@";

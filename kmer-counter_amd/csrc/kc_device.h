@@ -35,7 +35,9 @@ enum ErrBits : uint64_t {
     ERR_FQ_TOO_MANY = 16,   // more records than the index buffer holds
     ERR_FQ_NO_FINAL_NL = 32, // block does not end with '\n'
     ERR_REC_OVERFLOW = 64,   // partition engine: record buffer too small
-    ERR_SEG_TOO_LONG = 128   // seg_sort: a segment longer than its LDS capacity
+    ERR_SEG_TOO_LONG = 128,  // seg_sort: a segment longer than its LDS capacity
+    ERR_FQ_LIST = 256        // fused variable-length index: a half held more records than its list (not a
+                             // format error: the block is indexed again by the two-pass path)
 };
 
 // Slot stride (uint64 words) of the open-addressed table for W key words:
@@ -210,6 +212,13 @@ hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, 
 // checks as fq_emit + fq_validate; seq_off / seq_end are not written.
 hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
                             uint32_t* codes, uint16_t* inval, uint64_t* stats, hipStream_t s);
+// The same for variable-length reads (KC_FLAG_VARLEN): sequences of 0..L
+// bases encoded as launch_encode_reads_var does (slot padding, rlen, ST_VHOLE,
+// ST_VWIN); ERR_FQ_LIST when a half holds more records than its list (then
+// index the block with the two-pass path).
+hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
+                                int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen, uint64_t* stats,
+                                hipStream_t s);
 
 // ---- super-k-mer engine (kc_skm.inl) ----
 struct SkmGeom {

@@ -3418,17 +3418,28 @@ __device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb
     return code;
 }
 
+// VAR (KC_FLAG_VARLEN): sequences of 0..L bases. After the newline walk one
+// lane per listed record finds its sequence's newline (staged dwords, global
+// past the staging) and keeps its length; the encode then reads only the
+// read's own bytes and marks the rest of the L-base slot not-ACGT (as
+// encode_reads_var_k). The list holds lcap records per half (records of >= 32
+// bytes); a denser half sets ERR_FQ_LIST.
+template <bool VAR>
 __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                       const u64* __restrict__ line_base, u64 max_rec, int L, int G,
                                                       int lcap, u32* __restrict__ codes,
-                                                      unsigned short* __restrict__ inval, u64* stats) {
+                                                      unsigned short* __restrict__ inval, u64* stats,
+                                                      unsigned short* __restrict__ rlen, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
     const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const u64 lt = lanemask_lt();
-    const size_t wbytes = (size_t)kFqStage + (((size_t)lcap * 2 + 15) & ~(size_t)15);
+    const size_t wbytes = (size_t)kFqStage + (((size_t)lcap * (VAR ? 4 : 2) + 15) & ~(size_t)15);
     unsigned char* txt = smem + (size_t)wave * wbytes;
     unsigned short* lst = (unsigned short*)(txt + kFqStage);
+    unsigned short* lenl = lst + lcap;  // VAR: the listed records' sequence lengths
+    bool vhole = false;
+    u64 vwin = 0;
     const FastDivU divg((u32)G);
     u64 err = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -3504,6 +3515,14 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                     m |= (u64)nl_mask16w(v[rd][i].x, v[rd][i].y, v[rd][i].z, v[rd][i].w) << (16 * i);
                 mk[rd] = m;
             }
+            // VAR: newlines of the staged KiB past the half (the sequence end
+            // of a record that straddles the half end is its first one); the
+            // walk writes each listed record's sequence-end position
+            u32 mx = 0;
+            if constexpr (VAR) {
+                mx = nl_mask16w(x.x, x.y, x.z, x.w);
+                for (int i = lane; i < lcap; i += 64) lenl[i] = 0xffffu;
+            }
             if (cn < nchunks) issue(cn, hn);
             sync();
             const u64 rec0 = (run + 3) >> 2;  // first record whose header may end in this half
@@ -3545,8 +3564,12 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                         const u64 li = (j >> 2) - rec0;
                         if ((j >> 2) >= max_rec) err |= ERR_FQ_TOO_MANY;
                         else if (li < (u64)lcap) lst[li] = (unsigned short)(o + 1);
-                        else err |= ERR_FQ_SEQ_LEN;  // more records than L-base sequences allow
+                        else err |= VAR ? ERR_FQ_LIST : ERR_FQ_SEQ_LEN;  // more records than the list holds
                     } else if (jc != 2u) {
+                        if (VAR && jc == 1u) {
+                            const u64 li = (j >> 2) - rec0;  // wraps for records listed by the previous half
+                            if (li < (u64)lcap) lenl[li] = (unsigned short)o;
+                        }
                         // after the sequence: '+'; after the quality line: '@' (or the block end)
                         const u32 nx = q + 1 < n ? (u32)txt[o + 1] : 0u;
                         if (jc == 1u ? nx != (u32)'+' : (q + 1 < n && nx != (u32)'@'))
@@ -3560,13 +3583,53 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
             u64 rec1 = (run + 3) >> 2;
             if (rec1 > max_rec) rec1 = max_rec;
             const u32 nrec = rec1 > rec0 ? (u32)min(rec1 - rec0, (u64)lcap) : 0u;
+            if constexpr (VAR) {
+                // each listed record's sequence length: the walk saw its
+                // sequence end, or (at most one record, the one straddling the
+                // half end) it is the first newline of the staged KiB past the
+                // half, or (reads past that KiB) found by a dword scan
+                const u64 bx = __ballot(mx != 0u);
+                int ex = -1;
+                if (bx) {
+                    const int fl = __ffsll((long long)bx) - 1;
+                    ex = kFqHalf + 16 * fl + __builtin_ctz((u32)__builtin_amdgcn_readlane((int)mx, fl));
+                }
+                for (u32 li = (u32)lane; li < nrec; li += 64) {
+                    const int s = (int)lst[li];
+                    const u32 se = lenl[li];
+                    int pos = s & ~3, e = se != 0xffffu ? (int)se : (s <= kFqHalf ? ex : -1);
+                    while (e < 0 && pos - s <= L) {
+                        u32 w;
+                        if (pos + 4 <= kFqStage) {
+                            w = *(const u32*)(txt + pos);
+                        } else {
+                            const long long q = hrel + pos;  // block offset of the dword (4-aligned address)
+                            typedef __attribute__((address_space(1))) const u32 g32;
+                            w = q < (long long)n ? *(const g32*)(hb + (u64)pos) : 0x0a0a0a0au;
+                        }
+                        u32 m = nl_nib(w);
+                        if (pos < s) m &= 0xfu << (s - pos);
+                        if (m) e = pos + __builtin_ctz(m);
+                        pos += 4;
+                    }
+                    const int len = e < 0 ? L + 1 : e - s;
+                    if (len > L) err |= ERR_FQ_SEQ_LEN;
+                    const int lc = min(len, L);
+                    lenl[li] = (unsigned short)lc;
+                    if (rlen) rlen[rec0 + li] = (unsigned short)lc;
+                    if (lc >= k) vwin += (u64)(lc - k + 1);
+                }
+                sync();
+            }
             for (u32 item = (u32)lane; item < nrec * (u32)G; item += 64) {
                 const u32 r = divg.div(item);
                 const int g = (int)(item - r * (u32)G);
                 const int s0 = (int)lst[r] + 16 * g;  // staged offset of the group's first base
-                const int nb = min(16, L - 16 * g);
+                const int nb0 = min(16, L - 16 * g);  // slot bases in the group
+                const int lr = VAR ? (int)lenl[r] : L;
+                const int nb = VAR ? max(0, min(nb0, lr - 16 * g)) : nb0;  // of them, bases of the read
                 const bool lastg = g == G - 1;
-                const int need = nb + (lastg ? 1 : 0);  // the group (+ the byte after the read)
+                const int need = nb + ((lastg && !VAR) ? 1 : 0);  // the group (+ the byte after the read)
                 const int sh = s0 & 3;
                 u32 d[5];
                 if ((s0 & ~3) + 20 <= kFqStage) {
@@ -3590,15 +3653,20 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 const u32 x3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
                 u32 bad;
                 const u32 cw = swar_group(x0, x1, x2, x3, nb, &bad);
-                // a newline is a non-ACGT byte: the exact test only for such groups
-                bool wrong = bad != 0u &&
-                             (has_nl(x0, nb) || has_nl(x1, nb - 4) || has_nl(x2, nb - 8) || has_nl(x3, nb - 12));
-                if (lastg) {
-                    const int e = sh + nb;  // the byte after the read, in d
-                    const u32 nxt = (d[e >> 2] >> (8 * (e & 3))) & 255u;
-                    wrong = wrong || nxt != (u32)'\n' || hrel + s0 + nb >= (long long)n;
+                if constexpr (!VAR) {
+                    // a newline is a non-ACGT byte: the exact test only for such groups
+                    bool wrong = bad != 0u &&
+                                 (has_nl(x0, nb) || has_nl(x1, nb - 4) || has_nl(x2, nb - 8) || has_nl(x3, nb - 12));
+                    if (lastg) {
+                        const int e = sh + nb;  // the byte after the read, in d
+                        const u32 nxt = (d[e >> 2] >> (8 * (e & 3))) & 255u;
+                        wrong = wrong || nxt != (u32)'\n' || hrel + s0 + nb >= (long long)n;
+                    }
+                    if (wrong) err |= ERR_FQ_SEQ_LEN;
+                } else {
+                    if (bad != 0u && lr >= k) vhole = true;
+                    bad |= ((1u << (16 - nb)) - 1u) & ~((1u << (16 - nb0)) - 1u);  // the slot past the read
                 }
-                if (wrong) err |= ERR_FQ_SEQ_LEN;
                 const u64 at = (rec0 + r) * (u64)G + (u64)g;
                 codes[at] = cw;
                 inval[at] = (unsigned short)bad;
@@ -3609,6 +3677,11 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
         }
     }
     if (err) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)err);
+    if constexpr (VAR) {
+        if (__ballot(vhole) && lane == 0) atomicOr((unsigned long long*)&stats[ST_VHOLE], 1ull);
+        for (int o = 32; o >= 1; o >>= 1) vwin += __shfl_xor(vwin, o);
+        if (lane == 0 && vwin) atomicAdd((unsigned long long*)&stats[ST_VWIN], (unsigned long long)vwin);
+    }
 }
 
 hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
@@ -3620,8 +3693,24 @@ hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* lin
     if ((u64)lcap * (u64)G >= 65536) return hipErrorInvalidValue;  // FastDivU range
     const size_t lds = (size_t)kFqWaves * fq_encode_wave_lds(L);
     int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
-    hipLaunchKernelGGL(fq_encode_k, dim3(g ? g : 1), dim3(kBlock), lds, s, base, n, nch, line_base, max_rec, L, G,
-                       lcap, codes, (unsigned short*)inval, stats);
+    hipLaunchKernelGGL(fq_encode_k<false>, dim3(g ? g : 1), dim3(kBlock), lds, s, base, n, nch, line_base, max_rec,
+                       L, G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)nullptr, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
+                                int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen, uint64_t* stats,
+                                hipStream_t s) {
+    if (L < 1 || L > 32767 || k < 1) return hipErrorInvalidValue;
+    u64 nch = fq_chunks(base, n);
+    const int G = groups_per_read(L);
+    const int lcap = kFqHalf / 32 + 2;  // records of >= 32 bytes; denser halves: ERR_FQ_LIST
+    if ((u64)lcap * (u64)G >= 65536) return hipErrorInvalidValue;  // FastDivU range
+    const size_t wl = (size_t)kFqStage + (((size_t)lcap * 4 + 15) & ~(size_t)15);
+    const size_t lds = (size_t)kFqWaves * wl;
+    int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
+    hipLaunchKernelGGL(fq_encode_k<true>, dim3(g ? g : 1), dim3(kBlock), lds, s, base, n, nch, line_base, max_rec, L,
+                       G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)rlen, k);
     return hipGetLastError();
 }
 

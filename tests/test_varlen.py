@@ -20,7 +20,7 @@ import pytest
 import kmer_ref_py as kr
 
 
-def _varlen_fastq(n, lmin, lmax, seed, n_rate=0.01, genome=None):
+def _varlen_fastq(n, lmin, lmax, seed, n_rate=0.01, genome=None, hdr=0):
     rng = random.Random(seed)
     recs = []
     for i in range(n):
@@ -33,7 +33,8 @@ def _varlen_fastq(n, lmin, lmax, seed, n_rate=0.01, genome=None):
         for j in range(L):
             if rng.random() < n_rate:
                 s[j] = rng.choice("NNNnRa")
-        recs.append(f"@r{i}\n{''.join(s)}\n+\n{'I' * L}\n")
+        h = "x" * rng.randint(0, hdr)
+        recs.append(f"@r{i}{h}\n{''.join(s)}\n+\n{'I' * L}\n")
     return "".join(recs).encode()
 
 
@@ -187,3 +188,38 @@ def test_varlen_gpu_synth_device(kca, orc):
         got = ctx.records()
         ctx.free_device(ptr)
     assert got == orc.count_fastq_varlen(host, 31)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,lmin,lmax,hdr", [(31, 0, 150, 0), (31, 100, 150, 60), (9, 0, 12, 0), (21, 0, 24, 0), (19, 0, 40, 300),
+                                             (25, 200, 1500, 5), (55, 0, 150, 20)])
+def test_varlen_fused_matches_two_pass(kca, orc, monkeypatch, k, lmin, lmax, hdr):
+    # the fused index (fq_encode_k<true>: per-half record lists, sequence ends
+    # found past the staged KiB for long reads, dense halves falling back to
+    # the two-pass index) against the two-pass one (fq_emit_k +
+    # encode_reads_var_k) and the oracle
+    fq = _varlen_fastq(max(200, 1_500_000 // (lmax + lmin + hdr + 20)), lmin, lmax, seed=k + lmax + hdr,
+                       n_rate=0.004, hdr=hdr)
+    monkeypatch.delenv("KC_NO_FQ_ENCODE", raising=False)
+    n1, got, st1 = _gpu(kca, fq, k, lmax)
+    monkeypatch.setenv("KC_NO_FQ_ENCODE", "1")
+    n2, ref, st2 = _gpu(kca, fq, k, lmax)
+    assert n1 == n2
+    assert got == ref == orc.count_fastq_varlen(fq, k)
+    assert st1["windows"] == st2["windows"]
+
+
+@pytest.mark.gpu
+def test_varlen_fused_rejects_long_and_malformed(kca):
+    good = _varlen_fastq(3000, 20, 100, seed=41)
+    bad_len = _varlen_fastq(3000, 20, 120, seed=41)
+    with kca.Context(kmer_length=21, line_length=100, variable_length=True) as ctx:
+        with pytest.raises(kca.KcError) as e:
+            ctx.count_fastq(bad_len, 100)  # reads longer than the slot
+        assert e.value.status == 4
+        recs = good.split(b"\n")
+        recs[4 * 1500 + 2] = b"-"  # no '+' line after a sequence
+        with pytest.raises(kca.KcError) as e:
+            ctx.count_fastq(b"\n".join(recs), 100)
+        assert e.value.status == 4
+        assert ctx.count_fastq(good, 100) == 3000
