@@ -2562,10 +2562,12 @@ __device__ __forceinline__ u32 rec_hash(u64 k0, u64 k1) {
     return fmix32(x ^ (y * 0xcc9e2d51u));
 }
 
-static size_t rec_dedup_lds(u32 ngrp) { return (size_t)ngrp * 40 + 64 * 4 + 16; }
+constexpr u32 kRecClaims = 4096;  // P5a: claimed entries listed for the write-back (u16 each)
+
+static size_t rec_dedup_lds(u32 ngrp) { return (size_t)ngrp * 40 + 64 * 4 + 16 + kRecClaims * 2; }
 
 u32 rec_dedup_groups() {
-    u32 g = (u32)((160 * 1024 - 64 * 4 - 16 - 64) / 40);
+    u32 g = (u32)((160 * 1024 - 64 * 4 - 16 - 64 - kRecClaims * 2) / 40);
     return g & ~15u;
 }
 
@@ -2576,7 +2578,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* tab = (u64*)smem;                        // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
     u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);  // 2 ngrp
-    u32* misc = cnt + 2 * (size_t)a.ngrp;         // [0] overflow, [1..16] wave totals, [17] write-back cursor
+    u32* misc = cnt + 2 * (size_t)a.ngrp;         // [0] overflow, [1..16] wave totals, [17] write-back cursor,
+                                                  // [18] claims listed
+    unsigned short* clist = (unsigned short*)(misc + 64);  // entries in claim order (kRecClaims)
     const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
     const u32 nent = 2 * a.ngrp;
     const u64 lt = lanemask_lt();
@@ -2588,6 +2592,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
     if (tid == 0) {
         misc[0] = 0;
         misc[17] = 0;
+        misc[18] = 0;
     }
     __syncthreads();
     constexpr u64 kMark = 0x8000ull << 48;  // replaces the bucket bits: a non-zero word 0
@@ -2651,6 +2656,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
                             atomicAdd(&cnt[e], 1u);
                             done = true;
                             ++claims;
+                            const u32 ci = atomicAdd(&misc[18], 1u);
+                            if (ci < kRecClaims) clist[ci] = (unsigned short)e;
                         }
                         // lost the entry: the group is read again
                     } else {
@@ -2675,9 +2682,32 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
         u32 total = 0;
         for (int w = 0; w < kBucketWaves; w++) total += misc[1 + w];
         if (tid == 0) a.dlen[b] = raw ? kRawList : total;
+        const u64 pos0 = starts_r[b];
+        if (total <= kRecClaims) {
+            // the claimed entries in claim order: distinct record i goes to
+            // pos0 + i, its entry is cleared
+            for (u32 i = (u32)tid; i < total; i += kBucketBlock) {
+                const u32 e = clist[i];
+                if (!raw) {
+                    const u64 q = pos0 + i;
+                    a.recs[q] = (tab[2 * (size_t)e] & kLow48) | ((u64)b << 48);
+                    a.recs[a.stride + q] = tab[2 * (size_t)e + 1];
+                    a.cnt[q] = cnt[e];
+                }
+                tab[2 * (size_t)e] = 0ull;
+                tab[2 * (size_t)e + 1] = 0ull;
+                cnt[e] = 0;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                misc[0] = 0;
+                misc[18] = 0;
+            }
+            __syncthreads();
+            continue;
+        }
         const u32 spw = (nent + kBucketWaves - 1) / kBucketWaves;
         const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
-        const u64 pos0 = starts_r[b];
         for (u32 c0 = s0; c0 < s1; c0 += 64) {
             const u32 i = c0 + (u32)lane;
             const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
@@ -2703,6 +2733,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
         if (tid == 0) {
             misc[0] = 0;
             misc[17] = 0;
+            misc[18] = 0;
         }
         __syncthreads();
     }
