@@ -309,7 +309,8 @@ def main():
     d = kernels[dom]
     traffic = load_traffic()
     t_bytes = None
-    if traffic and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
+    # (the committed PMC summary is of the fixed-length cfg2 run)
+    if traffic and not varlen and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
         t_bytes = traffic.get("kernels", {}).get(d["kernel"].replace(" ", ""), {}).get("bytes_per_launch")
     b_path = nbytes / windows_per_gpu + 8 * W + 8
     step_s = elapsed / args.steps
