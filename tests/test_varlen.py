@@ -223,3 +223,22 @@ def test_varlen_fused_rejects_long_and_malformed(kca):
             ctx.count_fastq(b"\n".join(recs), 100)
         assert e.value.status == 4
         assert ctx.count_fastq(good, 100) == 3000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["alltoall", "none"])
+def test_varlen_cli_two_contexts(kca, orc, tmp_path, exchange):
+    # blocks dealt to two contexts (key-space exchange or run merge), each
+    # counting variable-length reads
+    d = tmp_path / "in"
+    d.mkdir()
+    fa = _varlen_fastq(3000, 0, 150, seed=51, n_rate=0.005)
+    fb = _varlen_fastq(3000, 20, 120, seed=52)
+    (d / "a.fastq").write_bytes(fa)
+    (d / "b.fastq").write_bytes(fb)
+    out = tmp_path / "out.bin"
+    cli = os.path.join(os.path.dirname(kca.LIB_PATH), "kmer-counter")
+    subprocess.run([cli, "kmerLength=31", f"inputFileLocation={d}", f"outputFile={out}", f"tempFileLocation={tmp_path}",
+                    "readLengths=variable", "gpus=2", f"exchange={exchange}", "quiet=1"],
+                   check=True, capture_output=True, timeout=300)
+    assert out.read_bytes() == orc.count_fastq_varlen(fa + fb, 31)
