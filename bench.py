@@ -1,26 +1,38 @@
 #!/usr/bin/env python3
-"""Benchmark of the k-mer count hot path (BASELINE.json metric).
+"""Benchmark of the k-mer count path (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): k=31, 150 bp reads
-sampled from a 250 Mbp random genome (splitmix64 generator, seed 2), 50M reads
-per GPU, FASTQ text resident in HBM (generated on the device, untimed), in-HBM
-hash table only. One step = one full count of the GPU's reads: clear the table,
-index the FASTQ block (K1), encode + window + insert every k-mer (K2), compact
-and radix-sort the table into SortedKMerFile records (K3/K4). N GPUs: one
-process per GPU, each counts its own disjoint 50M-read shard (weak scaling),
-then by default (`--exchange alltoall`) the ranks exchange
-their sorted (key, count) records by key-space owner with one RCCL
-all-to-all and each merges what it receives on the device, so the node's
-SortedKMerFile is the concatenation of the ranks' runs — all inside the timed
-step. `--exchange none` is the read-shard mode (cfg3): no collective, the
-per-GPU runs are left for the host k-way merge (not timed).
+`value` is SURVEY §8d's end-to-end rate: k-mers / wall seconds from the first
+FASTQ byte in to the output file closed. Workload (BASELINE.json configs[1],
+cfg 2): k=31, 50M x 150 bp reads per GPU sampled from a 250 Mbp random genome
+(splitmix64 generator, seed 2), written untimed to a FASTQ file in the work
+directory (page cache: host memory). One step =
+  kc_reset; kc_count_file (pread into pinned blocks, PCIe upload, GPU FASTQ
+  decode, counting) ; kc_finish (sorted SortedKMerFile records in HBM);
+  kc_write_output (device -> pinned -> the output file, closed).
+The timed region is exactly K such steps, bracketed by barrier + device
+synchronize, max over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--exchange alltoall|none] [--no-cpu]
-                    [--min-read-length M]
+Sub-objects of the same line (same input, same context):
+  device_resident : the FASTQ already in HBM, records left in HBM (the
+                    kernel-only figure; roofline and per-kernel rates);
+  host_memory     : the FASTQ in (pageable) host memory, one kc_count_fastq
+                    call, output file written;
+  reference_chunks: the same reads as the reference's chunks (concatenated
+                    sequences of 7.8 MB at gpuMemoryLimit=1e8,
+                    KMerCounter.cpp:193-212) through ~960 kc_count_chunk calls
+                    vs one kc_count_chunk call of all of them, output in HBM.
 
---min-read-length M (0 < M < L): variable-length input (SURVEY §8f row 1,
-KC_FLAG_VARLEN): read i keeps its first M..L bases (generator in
-kc_synth.h); k-mers per step = the reads' own windows (kc_stats.windows).
+N GPUs (one process per GPU, torch.distributed; RCCL = backend nccl): rank r
+counts reads [r R, (r+1) R) from its own input file (weak scaling).
+  --exchange alltoall (default at N > 1): the sorted runs are
+    exchanged by key-space owner (RCCL all-to-all) and merged on the device;
+    every rank writes its owned records at its offset of the one output file,
+    which is then the node's SortedKMerFile (concatenation, no merge).
+  --exchange none (cfg3, read-shard): the runs are gathered to rank 0's GPU
+    (RCCL) and merged there (device merge path), rank 0 writes the file.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5] [--reads R] [--exchange alltoall|none]
+                    [--mode e2e|device] [--no-cpu] [--no-variants] [--workdir DIR] [--min-read-length M]
 
 Prints one JSON line on rank 0 (contract in the task statement).
 """
@@ -46,23 +58,43 @@ def load_pkg():
     return mod
 
 
-def cpu_baseline(kca, reads, L, k, genome, seed, first, threads=None):
+def usable_cpus():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU
+    quota (the GPU box shows 256 CPUs but grants 16)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(kca, reads, L, k, genome, seed, threads):
     """The CPU port of the reference pipeline (oracle refcpu) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: timed as the CPU baseline only
 
-    if threads is None:
-        threads = min(16, os.cpu_count() or 1)
-    fq = kca.synth_fastq(reads, L, seed, genome_length=genome, first_read=first)
+    fq = kca.synth_fastq(reads, L, seed, genome_length=genome)
     t0 = time.perf_counter()
     distinct, windows = oracle.refcpu_count_only(fq, k, gpu_memory_limit=100000000, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": windows / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
-            "sample": f"{reads} reads x {L} bp of the same workload ({windows} k-mers, {distinct} distinct): "
-                      f"oracle refcpu = the reference count path on the CPU (readData chunking at "
-                      f"gpuMemoryLimit=1e8, bitEncode/extractKMers/reduceKMers restated, hash insert into a "
-                      f"sharded-lock table standing in for TBB); timed up to the complete table, as the "
-                      f"reference's DumpResults writes in hash order; {threads} threads, {dt:.2f} s"}
+    return windows / dt, windows, distinct, dt
+
+
+def cpu_baselines(kca, reads, L, k, genome, seed):
+    cores = usable_cpus()
+    v, win, distinct, dt = cpu_baseline(kca, reads, L, k, genome, seed, cores)
+    v1, _, _, dt1 = cpu_baseline(kca, reads, L, k, genome, seed, 1)
+    return {"value": v, "unit": "k-mers/s", "cores": cores, "kind": "port",
+            "sample": f"{reads} reads x {L} bp of the same workload ({win} k-mers, {distinct} distinct): oracle "
+                      f"refcpu = the reference count path on the CPU (readData chunking at gpuMemoryLimit=1e8, "
+                      f"bitEncode/extractKMers/reduceKMers restated, hash insert into a sharded-lock table standing "
+                      f"in for TBB), timed up to the complete table as the reference's DumpResults writes in hash "
+                      f"order; {cores} threads = the CPUs this process may use (cgroup quota of the "
+                      f"{os.cpu_count()} visible), {dt:.2f} s; same sample at 1 thread: {dt1:.2f} s",
+            "value_t1": v1}
 
 
 def cpu_baseline_varlen(kca, reads, L, lmin, k, genome, seed):
@@ -77,10 +109,12 @@ def cpu_baseline_varlen(kca, reads, L, lmin, k, genome, seed):
     t0 = time.perf_counter()
     out = oracle.count_fastq_varlen(fq, k)
     dt = time.perf_counter() - t0
-    return {"value": windows / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": 1, "kind": "oracle-spec",
             "sample": f"{reads} reads of {lmin}..{L} bp of the same workload ({windows} k-mers, "
-                      f"{len(out) // (8 * ((k + 31) // 32) + 4)} distinct): oracle count_fastq_varlen (each read "
-                      f"as a reference chunk of its own length, spec form, sorted output); 1 thread, {dt:.2f} s"}
+                      f"{len(out) // (8 * ((k + 31) // 32) + 4)} distinct): the oracle's specification form "
+                      f"(count_fastq_varlen: each read as a reference chunk of its own length, sorted output), not "
+                      f"a port of a reference pipeline (the reference has none for mixed read lengths); 1 thread, "
+                      f"{dt:.2f} s"}
 
 
 def shard_first(rank: int, reads_per_gpu: int) -> int:
@@ -101,14 +135,103 @@ def max_over_ranks(dist, value: float, device) -> float:
     return float(t.item())
 
 
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_count_kmers.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        return json.load(open(p))
-    except Exception:
-        return None
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.device = self.local
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist_mod
+
+            ndev = max(1, torch.cuda.device_count())
+            self.device = self.local % ndev  # rehearsal: ranks may share a GPU
+            torch.cuda.set_device(self.device)
+            # nccl (= RCCL) by default; KC_BENCH_BACKEND=gloo rehearses several
+            # ranks on one GPU (RCCL refuses duplicate devices)
+            dist_mod.init_process_group(backend=os.environ.get("KC_BENCH_BACKEND", "nccl"))
+            self.dist = dist_mod
+
+    def xdev(self):
+        import torch
+        if self.dist.get_backend() == "gloo":
+            return torch.device("cpu")
+        return torch.device("cuda", self.device)
+
+    def barrier_sync(self):
+        if self.dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            self.dist.barrier()
+            torch.cuda.synchronize()
+
+    def max(self, v):
+        return max_over_ranks(self.dist, float(v), self.xdev() if self.dist is not None else None)
+
+    def sum(self, v):
+        if self.dist is None:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.xdev())
+        self.dist.all_reduce(t)
+        return float(t.item())
+
+    def all_gather_int(self, v):
+        if self.dist is None:
+            return [v]
+        import torch
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self.xdev())
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
+
+
+def gather_runs_to_rank0(kca, ctx, D):
+    """cfg3 (read-shard, --exchange none): every rank's sorted run to rank 0's
+    GPU (one all-to-all in which only rank 0 receives), merged there by merge
+    path (kc_merge_runs_device). Returns rank 0's merged record count."""
+    import torch
+
+    dev = D.xdev()
+    n = ctx.finish()
+    rs = ctx.rs
+    send = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+    ctx.export_records(send)
+    counts = D.all_gather_int(n)
+    recv_sizes = [c * rs for c in counts] if D.rank == 0 else [0] * D.world
+    send_sizes = [n * rs if o == 0 else 0 for o in range(D.world)]
+    recv = torch.empty(sum(recv_sizes), dtype=torch.uint8, device=dev)
+    D.dist.all_to_all_single(recv, send, recv_sizes, send_sizes)
+    if recv.is_cuda:
+        torch.cuda.current_stream(recv.device).synchronize()
+    del send
+    if D.rank == 0:
+        return ctx.merge_runs(recv, counts)
+    return 0
+
+
+def write_node_output(kca, ctx, D, path, exchange):
+    """The node's SortedKMerFile from the ranks' finished runs (see the module
+    docstring). Returns output bytes written by this rank."""
+    if D.world == 1:
+        ctx.write_output(path)
+        return ctx.finish() * ctx.rs
+    if exchange == "alltoall":
+        n = kca.keyspace_exchange(ctx, D.dist, D.xdev())
+        sizes = D.all_gather_int(n * ctx.rs)
+        off = sum(sizes[:D.rank])
+        if D.rank == 0:
+            with open(path, "wb") as f:
+                f.truncate(sum(sizes))
+        D.dist.barrier()
+        ctx.write_output_at(path, off)
+        return sizes[D.rank]
+    n = gather_runs_to_rank0(kca, ctx, D)
+    if D.rank == 0:
+        ctx.write_output(path)
+    return n * ctx.rs
 
 
 def main():
@@ -119,6 +242,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="SURVEY §8d preset: 2 = k=31, 50M x 150 bp from a 250 Mbp genome (the metric's "
                          "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality)")
+    ap.add_argument("--mode", default="e2e", choices=["e2e", "device"],
+                    help="value = file-to-file rate (e2e) or the device-resident rate (device)")
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--L", type=int, default=150)
@@ -126,12 +251,14 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--mem", type=int, default=None, help="gpuMemoryLimit per GPU (bytes)")
     ap.add_argument("--engine", default="auto", choices=["auto", "skm", "partition", "table"])
-    ap.add_argument("--cpu-reads", type=int, default=2_000_000)
+    ap.add_argument("--cpu-reads", type=int, default=1_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the host_memory / reference_chunks lines")
+    ap.add_argument("--workdir", default=None, help="input/output files (default $TMPDIR or /tmp)")
     ap.add_argument("--min-read-length", type=int, default=0,
                     help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
     ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
-                    help="N>1: key-space all-to-all (cfg4) or read-shard only (cfg3); ignored at N=1")
+                    help="N>1: key-space all-to-all (cfg4) or read-shard + merge on rank 0 (cfg3)")
     args = ap.parse_args()
     preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
               5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=72 << 30)}[args.config]
@@ -139,145 +266,233 @@ def main():
         if getattr(args, key) is None:
             setattr(args, key, v)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist_mod
-
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-        # nccl (= RCCL) by default; KC_BENCH_BACKEND=gloo rehearses several
-        # ranks on one GPU (RCCL refuses duplicate devices)
-        dist_mod.init_process_group(backend=os.environ.get("KC_BENCH_BACKEND", "nccl"))
-        dist = dist_mod
+    D = Dist()
+    import numpy as np
 
     kca = load_pkg()
     k, L = args.k, args.L
-    device = local
-    if world > 1:
-        import torch
-        device = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
+    W = (k + 31) // 32
     varlen = 0 < args.min_read_length < L
-    ctx = kca.Context(kmer_length=k, line_length=L, device=device, gpu_memory_limit=args.mem, engine=args.engine,
-                      variable_length=varlen)
-    first = shard_first(rank, args.reads)
-    ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first,
-                                   args.min_read_length if varlen else 0)
+    ctx = kca.Context(kmer_length=k, line_length=L, device=D.device, gpu_memory_limit=args.mem,
+                      engine=args.engine, variable_length=varlen)
+    first = shard_first(D.rank, args.reads)
+    lmin = args.min_read_length if varlen else 0
+    ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first, lmin)
+    exchange = args.exchange if D.world > 1 else "none"
 
-    exchange = args.exchange if world > 1 else "none"
-    xdev = None
-    if exchange == "alltoall":
-        import torch
-        xdev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", device)
+    # ---- input file (untimed): the same bytes, in the page cache ---------------
+    workdir = args.workdir or os.environ.get("TMPDIR") or "/tmp"
+    in_path = os.path.join(workdir, f"kc_bench_in.{os.getpid()}.fq")
+    out_path = os.path.join(workdir, f"kc_bench_out.{D.rank if exchange == 'none' else 'node'}."
+                                     f"{os.getpid() if D.world == 1 else 'x'}.bin")
+    host = np.empty(nbytes, dtype=np.uint8)
+    ctx.copy_to_host_addr(host.ctypes.data, ptr, nbytes)
+    host.tofile(in_path)
+    rs = ctx.rs
+
+    def windows_of_step(st):
+        return st["windows"] if varlen else args.reads * (L - k + 1)
+
+    # ---- end-to-end: file in -> output file closed -------------------------------
+    phase = {"count_file": 0.0, "finish": 0.0, "output": 0.0}
+    out_bytes = [0]
+
+    def e2e_step():
+        t0 = time.perf_counter()
+        ctx.reset()
+        ctx.count_file(in_path, L if varlen else 0)
+        t1 = time.perf_counter()
+        ctx.finish()
+        t2 = time.perf_counter()
+        out_bytes[0] = write_node_output(kca, ctx, D, out_path, exchange)
+        t3 = time.perf_counter()
+        phase["count_file"] += t1 - t0
+        phase["finish"] += t2 - t1
+        phase["output"] += t3 - t2
+
+    def timed(step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        for key in phase:
+            phase[key] = 0.0
+        D.barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        D.barrier_sync()
+        return D.max(time.perf_counter() - t0)
+
+    e2e = None
+    if args.mode == "e2e":
+        el = timed(e2e_step, args.steps, args.warmup)
+        st = ctx.stats()
+        win = D.sum(windows_of_step(st))
+        in_b = D.sum(nbytes)
+        step_s = el / args.steps
+        ph = {key: v / args.steps * 1e3 for key, v in phase.items()}
+        e2e = {"value": win / step_s, "ms_per_step": step_s * 1e3,
+               "phases_ms_rank0": {key: round(v, 2) for key, v in ph.items()},
+               "input_bytes": int(in_b), "output_bytes": int(D.sum(out_bytes[0])),
+               # PCIe / file rates of rank 0's phases (count_file includes the GPU decode and counting of
+               # whatever fits no flush before it; the output phase is D2H + file write)
+               "input_GBps_rank0": round(nbytes / (ph["count_file"] / 1e3) / 1e9, 2),
+               "output_GBps_rank0": round(out_bytes[0] / (ph["output"] / 1e3) / 1e9, 2) if ph["output"] else None,
+               "workdir": workdir}
+
+    # ---- device-resident (kernel-only) figure ----------------------------------
     xch_ms = [0.0]
 
-    def step():
+    def dev_step():
         ctx.reset()
         ctx.count_fastq_device(ptr, nbytes)
         n = ctx.finish()
         if exchange == "alltoall":
             t = time.perf_counter()
-            n = kca.keyspace_exchange(ctx, dist, xdev)
+            n = kca.keyspace_exchange(ctx, D.dist, D.xdev())
+            xch_ms[0] += (time.perf_counter() - t) * 1e3
+        elif exchange == "none" and D.world > 1:
+            t = time.perf_counter()
+            n = gather_runs_to_rank0(kca, ctx, D)
             xch_ms[0] += (time.perf_counter() - t) * 1e3
         return n
 
-    def barrier_sync():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    barrier_sync()
+    for _ in range(args.warmup if args.mode == "device" else 0):
+        dev_step()
+    D.barrier_sync()
     xch_ms[0] = 0.0
+    acc = {"insert_ms": 0.0, "finish_ms": 0.0, "decode_ms": 0.0, "dedup_ms": 0.0, "launches": 0,
+           "part_ms": [0.0] * 5}
     t0 = time.perf_counter()
-    insert_ms = 0.0
-    launches = 0
-    finish_ms = 0.0
-    decode_ms = 0.0
-    part_ms = [0.0] * 5
-    dedup_ms = 0.0
     n_rec = 0
     for _ in range(args.steps):
-        n_rec = step()
+        n_rec = dev_step()
         st = ctx.stats()
-        insert_ms += st["insert_ms"]
-        launches += st["insert_launches"]
-        finish_ms += st["finish_ms"]
-        decode_ms += st["decode_ms"]
-        part_ms = [a + b for a, b in zip(part_ms, st["part_ms"])]
-        dedup_ms += st.get("dedup_ms", 0.0)
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
+        acc["insert_ms"] += st["insert_ms"]
+        acc["launches"] += st["insert_launches"]
+        acc["finish_ms"] += st["finish_ms"]
+        acc["decode_ms"] += st["decode_ms"]
+        acc["dedup_ms"] += st.get("dedup_ms", 0.0)
+        acc["part_ms"] = [a + b for a, b in zip(acc["part_ms"], st["part_ms"])]
+    D.barrier_sync()
+    dev_el = D.max(time.perf_counter() - t0)
     st = ctx.stats()
-    if dist is not None:
-        import torch
-        dev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
-        elapsed = max_over_ranks(dist, elapsed, dev)
-    # variable-length reads: the reads' own windows (ctx stats are per step)
-    windows_per_gpu = st["windows"] if varlen else args.reads * (L - k + 1)
-    if dist is not None and varlen:
-        import torch
-        dev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
-        t = torch.tensor([float(windows_per_gpu)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t)
-        windows_per_gpu = t.item() / world
-    total_kmers = windows_per_gpu * world * args.steps
-    value = total_kmers / elapsed
+    windows_per_gpu = windows_of_step(st)
+    if D.world > 1 and varlen:
+        windows_per_gpu = D.sum(windows_per_gpu) / D.world
+    dev_value = windows_per_gpu * D.world * args.steps / dev_el
+    roofline = device_roofline(args, st, acc, windows_per_gpu, nbytes, dev_el, varlen, k, L, W)
 
-    # Rooflines. Each main kernel of the partition engine is priced by its own
-    # algorithmic HBM bytes: P2 reads the encoded reads
-    # (6 B per 16 bases) and writes 8W B per key; the P3 scatter reads and
-    # writes 8W B per key; P5 reads 8W B per key and writes 8W+4 B per
-    # distinct record. `roofline` is the one with the longest launch; each
-    # achieved = algorithmic bytes per launch / its HIP-event launch time on
-    # the ctx stream. `path_achieved` is SURVEY §8d's whole-path figure:
-    # k-mers/s per GPU x (FASTQ bytes per k-mer + 8W + 8).
-    W = (k + 31) // 32
+    # ---- host-memory input and the reference's chunks (N = 1) --------------------
+    variants = {}
+    if D.world == 1 and not args.no_variants and not varlen:
+        variants = host_variants(kca, ctx, args, host, nbytes, out_path, k, L)
+    del host
+
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu:
+        if varlen:
+            cpu = cpu_baseline_varlen(kca, max(1, args.cpu_reads // 10), L, args.min_read_length, k, args.genome,
+                                      args.seed)
+        else:
+            cpu = cpu_baselines(kca, args.cpu_reads, L, k, args.genome, args.seed)
+
+    src = (f"sampled from a {args.genome} bp random genome" if args.genome else "of iid uniform bases")
+    lens = f"{args.min_read_length}..{L} bp (variable-length, KC_FLAG_VARLEN)" if varlen else f"{L} bp"
+    base = f"k={k}, {args.reads} x {lens} reads per GPU {src} (seed {args.seed})"
+    cfg_tag = f"cfg{args.config}{'v' if varlen else ''}"
+    if args.mode == "e2e":
+        path_desc = ("FASTQ file (page cache) -> pinned blocks -> PCIe -> GPU decode + count -> sorted records -> "
+                     "PCIe -> SortedKMerFile closed")
+    else:
+        path_desc = "FASTQ in HBM -> sorted records in HBM (device-resident)"
+    if D.world == 1:
+        workload, parallelism = f"{cfg_tag}: {base}; {path_desc}", "single GPU"
+    elif exchange == "alltoall":
+        workload = (f"cfg4 pattern at {D.world} GPUs: {base}; {path_desc}; key-space all-to-all of the sorted "
+                    f"(key, count) records + per-GPU merge, each rank writes its key range at its offset of the "
+                    f"one output file")
+        parallelism = f"read-shard count + key-space all-to-all x{D.world}"
+    else:
+        workload = (f"cfg3 pattern at {D.world} GPUs: {base}; {path_desc}; runs gathered to rank 0's GPU "
+                    f"(RCCL) and merged there by merge path, rank 0 writes the file")
+        parallelism = f"read-shard x{D.world} + device merge on rank 0"
+
+    device_resident = {
+        "value": dev_value, "ms_per_step": dev_el / args.steps * 1e3,
+        "breakdown_ms_per_step": {"fastq_index": acc["decode_ms"] / args.steps,
+                                  "finish": acc["finish_ms"] / args.steps,
+                                  "exchange_rank0": xch_ms[0] / args.steps,
+                                  "partition_passes": [round(x / args.steps, 3) for x in acc["part_ms"]],
+                                  "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3)},
+    }
+    if args.mode == "e2e":
+        value, ms = e2e["value"], e2e["ms_per_step"]
+    else:
+        value, ms = dev_value, dev_el / args.steps * 1e3
+    if D.rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": D.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": workload, "k": k, "read_length": L, "reads_per_gpu": args.reads,
+                       "parallelism": parallelism, "gpu_memory_limit": args.mem, "mode": args.mode},
+            "roofline": roofline,
+            "path_frac": roofline["path_frac"],
+            "cpu_baseline": cpu,
+            "end_to_end": e2e,
+            "device_resident": device_resident,
+            "host_variants": variants or None,
+            "engine": args.engine,
+            "engines_used": {1: "skm", 2: "key-prefix partition", 3: "skm + key-prefix",
+                             4: "table"}.get(st.get("engines_used", 0), str(st.get("engines_used"))),
+            "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"], "spill_runs": st["spill_runs"],
+        }
+        print(json.dumps(line), flush=True)
+    for p in (in_path, out_path):
+        try:
+            if D.rank == 0 or p == in_path:
+                os.unlink(p)
+        except OSError:
+            pass
+    ctx.free_device(ptr)
+    ctx.close()
+    if D.dist is not None:
+        D.dist.barrier()
+        D.dist.destroy_process_group()
+
+
+def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W):
+    """Per-kernel rooflines of the device-resident step. Each main kernel is
+    priced by its own algorithmic HBM bytes; `roofline` is the
+    kernel with the largest per-step time; achieved = algorithmic bytes per
+    launch / its HIP-event launch time on the ctx stream. `path_frac` is
+    SURVEY §8d's whole-path figure: k-mers/s per GPU x (FASTQ bytes per k-mer
+    + 8W + 8) over the device-resident step."""
     G = (L + 15) // 16
     steps = args.steps
-    windows_step = windows_per_gpu
-    keys_step = st["keys"] or windows_step  # ctx stats are per step (reset at each step)
+    part_ms = acc["part_ms"]
     recs_step = st["output_records"]
     kernels = {}
     used = st.get("engines_used", 0)
     if used & 1:
-        # super-k-mer engine: F reads the encoded reads (6 B per 16 bases) and
-        # writes the records (8(W+1) B each); each of the two grouping scatters
-        # reads and writes every record; P5 reads the records and writes the
-        # distinct (key, count) records
-        # (S: two scatter launches per batch, each over all records; P5: the
-        # cardinality sample and the main launch together are one pass over
-        # the records, priced per batch)
         rec_step = st["keys"] or 1  # records handed out by F per step
         rb = 8 * (W + 1)
-        # F3 (skm_front3_k<k>, a lane per read) covers W = 1, 19 <= k <= 32
-        # with rows of <= 40 KiB per wave; F2 (skm_front2_k<1, k>) W = 1,
-        # 18 <= k <= 32 with at most 64 8-window chunks per read; the generic F
-        # otherwise
         nw = L - k + 1
         ng = max((L + 15) // 16 + 1, (nw - 1) // 16 + 5) | 1
         f3 = (W == 1 and 19 <= k <= 32 and (320 + 64) * 8 + 256 + 256 * ng <= 40 * 1024
               and not os.environ.get("KC_NO_F3"))
         f2 = W == 1 and 18 <= k <= 32 and (nw + 7) // 8 <= 64 and not os.environ.get("KC_NO_F2")
         fname = f"skm_front3_k<{k}>" if f3 else (f"skm_front2_k<1,{k}>" if f2 else f"skm_front_k<{W}>")
-        dd_step = st.get("dedup_records", 0)  # ctx stats are per step
+        dd_step = st.get("dedup_records", 0)
         specs = [
-            ("F", fname, part_ms[1], launches, windows_step, "k-mers",
+            ("F", fname, part_ms[1], acc["launches"], windows_step, "k-mers",
              (G * 6) / max(1, L - k + 1) + rb * rec_step / windows_step),
             ("S", f"rp_scatter_k<{W + 1},false>", part_ms[2], 2 * steps * st["batches"], 2 * rec_step, "records",
              2 * rb + 1),
         ]
-        if dedup_ms > 0:
-            # P5a reads every record and writes each distinct one with its
-            # multiplicity; P5 then reads the distinct records and writes the
-            # distinct (key, count) records
+        if acc["dedup_ms"] > 0:
             specs += [
-                ("P5a", "count_rec_k", dedup_ms, steps * st["batches"], rec_step, "records",
+                ("P5a", "count_rec_k", acc["dedup_ms"], steps * st["batches"], rec_step, "records",
                  rb + (rb + 4) * dd_step / rec_step),
                 ("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], max(1, dd_step), "distinct records",
                  (rb + 4) + (8 * W + 4) * recs_step / max(1, dd_step)),
@@ -286,89 +501,110 @@ def main():
             specs.append(("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], rec_step, "records",
                           rb + (8 * W + 4) * recs_step / rec_step))
     elif used & 2:
+        keys_step = st["keys"] or windows_step
         p5_per_step = max(1, st["p5_launches"])
         specs = [
-            ("P2", f"count_front<{W},2,true,1024>", part_ms[1], launches, windows_step,
+            ("P2", f"count_front<{W},2,true,1024>", part_ms[1], acc["launches"], windows_step,
              "k-mers", (G * 6) / max(1, L - k + 1) + 8 * W),
             ("P3", f"p3_scatter_k<{W}>", part_ms[2], steps * st["batches"], keys_step, "keys", 16 * W),
             ("P5", f"count_buckets<{W}>", part_ms[4], steps * p5_per_step, keys_step, "keys",
              8 * W + (8 * W + 4) * recs_step / max(1, keys_step)),
         ]
     else:
-        specs = [("insert", f"count_front<{W},0,false,256>", insert_ms, launches, windows_step, "k-mers",
-                  nbytes / windows_per_gpu + 8 * W + 8)]
+        specs = [("insert", f"count_front<{W},0,false,256>", acc["insert_ms"], acc["launches"], windows_step,
+                  "k-mers", nbytes / windows_step + 8 * W + 8)]
     for tag, name, ms_total, nl, units_step, unit_name, bpu in specs:
         nl = max(1, nl)
         avg = ms_total / nl
         units = units_step * steps / nl
         ach = bpu * units / (avg / 1e3) / 1e9 if avg > 0 else 0.0
-        kernels[tag] = {"kernel": name, "avg_launch_ms": round(avg, 3), "units_per_launch": int(units),
-                        "unit": unit_name, "algorithmic_bytes_per_unit": round(bpu, 3),
-                        "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 4)}
-    dom = max(kernels, key=lambda t: kernels[t]["avg_launch_ms"])
+        kernels[tag] = {"kernel": name, "avg_launch_ms": round(avg, 3), "ms_per_step": round(ms_total / steps, 3),
+                        "units_per_launch": int(units), "unit": unit_name,
+                        "algorithmic_bytes_per_unit": round(bpu, 3), "achieved": round(ach, 2),
+                        "frac": round(ach / HBM_PEAK_GBS, 4)}
+    dom = max(kernels, key=lambda t: kernels[t]["ms_per_step"])
     d = kernels[dom]
-    traffic = load_traffic()
     t_bytes = None
+    p = os.path.join(ROOT, "profiles", "pmc_count_kmers.json")
+    try:
+        traffic = json.load(open(p))
+    except (OSError, ValueError):
+        traffic = None
     # (the committed PMC summary is of the fixed-length cfg2 run)
     if traffic and not varlen and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
         t_bytes = traffic.get("kernels", {}).get(d["kernel"].replace(" ", ""), {}).get("bytes_per_launch")
-    b_path = nbytes / windows_per_gpu + 8 * W + 8
-    step_s = elapsed / args.steps
-    path_achieved = b_path * windows_per_gpu / step_s / 1e9
-    roofline = {"bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": d["frac"], "traffic": t_bytes, "kernel": f"{dom}: {d['kernel']}",
-                "avg_launch_ms": d["avg_launch_ms"], "units_per_launch": d["units_per_launch"],
-                "unit_of_work": d["unit"], "algorithmic_bytes_per_unit": d["algorithmic_bytes_per_unit"],
-                "path_achieved": round(path_achieved, 2), "path_frac": round(path_achieved / HBM_PEAK_GBS, 4),
-                "path_bytes_per_kmer": round(b_path, 3), "kernels": kernels}
+    b_path = nbytes / windows_step + 8 * W + 8
+    path_achieved = b_path * windows_step / (dev_el / steps) / 1e9
+    return {"bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": d["frac"], "traffic": t_bytes, "kernel": f"{dom}: {d['kernel']}",
+            "avg_launch_ms": d["avg_launch_ms"], "units_per_launch": d["units_per_launch"],
+            "unit_of_work": d["unit"], "algorithmic_bytes_per_unit": d["algorithmic_bytes_per_unit"],
+            "path_achieved": round(path_achieved, 2), "path_frac": round(path_achieved / HBM_PEAK_GBS, 4),
+            "path_bytes_per_kmer": round(b_path, 3), "kernels": kernels,
+            "note": "dominant kernel = largest device time per step; path_* = SURVEY §8d bytes per k-mer over the "
+                    "device-resident step"}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and varlen:
-        cpu = cpu_baseline_varlen(kca, max(1, args.cpu_reads // 20), L, args.min_read_length, k, args.genome,
-                                  args.seed)
-    elif rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(kca, args.cpu_reads, L, k, args.genome, args.seed, 0)
-        t1 = cpu_baseline(kca, max(1, args.cpu_reads // 10), L, k, args.genome, args.seed, 0, threads=1)
-        cpu["value_t1"] = t1["value"]
-        cpu["sample_t1"] = t1["sample"]
 
-    src = (f"sampled from a {args.genome} bp random genome" if args.genome else "of iid uniform bases")
-    lens = f"{args.min_read_length}..{L} bp (variable-length, KC_FLAG_VARLEN)" if varlen else f"{L} bp"
-    base = (f"k={k}, {args.reads} x {lens} reads per GPU {src} (seed {args.seed}), FASTQ in HBM, "
-            f"in-HBM count")
-    if world == 1:
-        workload, parallelism = f"cfg{args.config}{'v' if varlen else ''}: " + base, "single GPU"
-    elif exchange == "alltoall":
-        workload = (f"cfg4 pattern at {world} GPUs: " + base + "; key-space all-to-all of the sorted (key, count) "
-                    "records + per-GPU merge inside the step (output = concatenation of the ranks' runs)")
-        parallelism = f"read-shard count + key-space all-to-all x{world}"
-    else:
-        workload = f"cfg3 pattern at {world} GPUs: " + base + "; per-GPU sorted runs, host merge not timed"
-        parallelism = f"read-shard x{world}"
-    if rank == 0:
-        line = {
-            "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": workload, "k": k, "read_length": L, "reads_per_gpu": args.reads,
-                       "parallelism": parallelism, "gpu_memory_limit": args.mem},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "breakdown_ms_per_step": {"p2_scatter": insert_ms / args.steps, "fastq_index": decode_ms / args.steps,
-                                      "finish": finish_ms / args.steps,
-                                      "exchange_rank0": xch_ms[0] / args.steps,
-                                      "partition_passes": [round(x / args.steps, 3) for x in part_ms],
-                                      "p5a_dedup": round(dedup_ms / args.steps, 3)},
-            "engine": args.engine, "engines_used": {1: "skm", 2: "key-prefix partition", 3: "skm + key-prefix",
-                                                    4: "table"}.get(st.get("engines_used", 0), str(st.get("engines_used"))),
-            "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"],
-        }
-        print(json.dumps(line), flush=True)
-    ctx.free_device(ptr)
-    ctx.close()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+def host_variants(kca, ctx, args, host, nbytes, out_path, k, L):
+    """host_memory: the FASTQ from pageable host memory in one kc_count_fastq
+    call -> output file. reference_chunks: the same reads as the reference's
+    chunks (sequences only, 7.8 MB each at gpuMemoryLimit=1e8) through
+    kc_count_chunk, against one kc_count_chunk of all of them (records left
+    in HBM in both)."""
+    import numpy as np
+
+    res = {}
+    win = args.reads * (L - k + 1)
+
+    def one(step, reps=1):
+        step()  # warm
+        best = None
+        for _ in range(reps):
+            t = time.perf_counter()
+            step()
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        return best
+
+    def host_step():
+        ctx.reset()
+        ctx.count_fastq_host(host.ctypes.data, nbytes)
+        ctx.write_output(out_path)
+
+    dt = one(host_step)
+    res["host_memory"] = {"value": win / dt, "ms_per_step": dt * 1e3,
+                          "path": "FASTQ in pageable host memory -> pinned ring -> PCIe -> GPU decode + count -> "
+                                  "SortedKMerFile closed"}
+    # the reference's chunk layout: concatenated sequences
+    sptr, sbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, 0, 0, layout=1)
+    seqs = np.empty(sbytes, dtype=np.uint8)
+    ctx.copy_to_host_addr(seqs.ctypes.data, sptr, sbytes)
+    ctx.free_device(sptr)
+    # KMerCounter::GetChunkSize at the reference's default gpuMemoryLimit (main.cpp:28)
+    kb = (k + 3) // 4
+    per = ((kb + 7) // 8 + 1) * 8 * (L - k + 1)
+    cs = L * ((100000000 - L) // (per - 1))
+    base = seqs.ctypes.data
+
+    def chunks_step():
+        ctx.reset()
+        for off in range(0, sbytes, cs):
+            ctx.count_chunk_host(base + off, min(cs, sbytes - off), L)
+        ctx.finish()
+
+    def block_step():
+        ctx.reset()
+        ctx.count_chunk_host(base, sbytes, L)
+        ctx.finish()
+
+    tc = one(chunks_step)
+    tb = one(block_step)
+    res["reference_chunks"] = {"chunk_bytes": cs, "chunks": (sbytes + cs - 1) // cs,
+                               "value_chunks": win / tc, "ms_chunks": tc * 1e3,
+                               "value_one_block": win / tb, "ms_one_block": tb * 1e3,
+                               "chunks_over_block_time": round(tc / tb, 3)}
+    del seqs
+    return res
 
 
 if __name__ == "__main__":

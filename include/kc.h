@@ -56,7 +56,8 @@
 extern "C" {
 #endif
 
-#define KC_ABI_VERSION 3 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length */
+#define KC_ABI_VERSION 4 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
+                            4: kc_count_file, kc_checkpoint / kc_rollback / kc_commit */
 #define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
 
 typedef enum kc_status {
@@ -158,7 +159,7 @@ typedef struct kc_stats {
     uint64_t dedup_records;    /* distinct records P5a listed since the last reset */
 } kc_stats;
 
-/* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". */
+/* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". (ABI 4: layout) */
 typedef struct kc_synth_spec {
     uint64_t n_reads;
     int64_t read_length;   /* L */
@@ -172,6 +173,11 @@ typedef struct kc_synth_spec {
                               min + rand(i) mod (read_length - min + 1) bases
                               and its header is padded with 'x' to keep the
                               record size (variable-length input, KC_FLAG_VARLEN) */
+    uint32_t layout;       /* 0 = FASTQ records; 1 = the sequences only, read i at
+                              (i - first_read) * read_length: the bytes of a
+                              reference chunk (FASTQFileReader.cpp:49-89), for
+                              kc_count_chunk (fixed read length only) */
+    uint32_t reserved;
 } kc_synth_spec;
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -206,6 +212,49 @@ kc_status kc_count_fastq_device(kc_ctx* ctx, const void* d_fastq, uint64_t n_byt
 /* Validation only (the GPU index of kc_count_fastq without counting). */
 kc_status kc_check_fastq(kc_ctx* ctx, const char* fastq, uint64_t n_bytes, int64_t line_length, uint64_t* n_reads);
 
+/* Batching. kc_count_chunk / kc_count_fastq* decode and 2-bit encode each
+ * block on the GPU at once (a malformed FASTQ block is reported by its own
+ * call) but count the encoded reads in batches: a batch is counted when the
+ * next block does not fit it (gpu_memory_limit), when the read length
+ * changes, or at kc_finish. Many small calls (the reference's 7.8 MB chunks)
+ * therefore cost about what one large block costs. Host buffers may be reused
+ * as soon as a call returns. */
+
+/* Checkpoint of the ctx's input: kc_rollback forgets every block counted
+ * since, as long as no batch was counted in between (KC_ERR_STATE otherwise;
+ * while a checkpoint is held, batches grow up to 1/8 of device memory before
+ * they are counted). kc_commit drops the checkpoint. Used by kc_count_file's
+ * auto mode to fall back to the reference chunker after a malformed block
+ * without reading the file twice. */
+kc_status kc_checkpoint(kc_ctx* ctx);
+kc_status kc_rollback(kc_ctx* ctx);
+kc_status kc_commit(kc_ctx* ctx);
+
+/* Whole FASTQ file (replaces InputFileHandler::read + FASTQFileReader::readData,
+ * InputFileHandler.cpp:82-95, FASTQFileReader.cpp:49-89, and the chunk loop of
+ * KMerCounter::Start, KMerCounter.cpp:123-143). The file is read in 256 MiB
+ * blocks (pread into pinned buffers, read ahead of the GPU), cut at record
+ * boundaries, and each block goes to one of the n_ctx contexts (read-shard: a
+ * block to whichever context is free). line_length 0 = the file's line 2
+ * (FASTQFileReader.cpp:31-35; the ctx's L with KC_FLAG_VARLEN); a file whose
+ * reads are shorter than k counts nothing. mode:
+ *   KC_INPUT_AUTO  : GPU FASTQ decode; if a block is not 4-line records of
+ *                    L-base reads, the whole file is counted in the
+ *                    reference's own chunks instead (as KC_INPUT_EXACT) —
+ *                    bit-exact with the reference on any input;
+ *   KC_INPUT_FASTQ : GPU FASTQ decode; a malformed block is KC_ERR_FORMAT;
+ *   KC_INPUT_EXACT : the reference's chunker (readData with the chunk size of
+ *                    KMerCounter::GetChunkSize from gpu_memory_limit, header
+ *                    >= 2L records lost at chunk edges as in the reference)
+ *                    on ctxs[0], through kc_count_chunk.
+ * Variable-length contexts always decode FASTQ. *n_reads (may be NULL)
+ * receives the reads counted. */
+#define KC_INPUT_AUTO 0u
+#define KC_INPUT_FASTQ 1u
+#define KC_INPUT_EXACT 2u
+kc_status kc_count_file(kc_ctx* const* ctxs, uint32_t n_ctx, const char* path, int64_t line_length, uint32_t mode,
+                        uint64_t* n_reads);
+
 /* ---- results ------------------------------------------------------------ */
 /* Compacts and radix-sorts the hash table on the device. *n_records receives
  * the number of records of the table run (spill runs not included). After
@@ -222,6 +271,10 @@ kc_status kc_device_records(kc_ctx* ctx, const void** d_records, uint64_t* n_byt
  * up to `merge_threads` threads, equal keys summed as uint32). The file is
  * truncated first (the reference appends, KMerFileMerger.cpp:129). */
 kc_status kc_write_output(kc_ctx* ctx, const char* path, uint32_t merge_fan_in, uint32_t merge_threads);
+/* Writes the finished table run (no spill runs) into an existing file at byte
+ * `offset` without truncating it: the ranks of a key-space exchange write
+ * their key ranges of one output file side by side. */
+kc_status kc_write_output_at(kc_ctx* ctx, const char* path, uint64_t offset);
 /* Writes the table run plus spill runs as separate sorted run files
  * "<prefix>.<i>" and returns how many were written (for multi-GPU merges). */
 kc_status kc_write_runs(kc_ctx* ctx, const char* prefix, uint32_t* n_runs);

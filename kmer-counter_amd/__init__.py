@@ -35,6 +35,11 @@ KC_ERR_STATE = 6
 KC_ERR_NODEVICE = 7
 KC_ERR_INTERNAL = 8
 
+KC_INPUT_AUTO = 0
+KC_INPUT_FASTQ = 1
+KC_INPUT_EXACT = 2
+_INPUT_MODES = {"auto": KC_INPUT_AUTO, "fastq": KC_INPUT_FASTQ, "exact": KC_INPUT_EXACT}
+
 
 class KcError(RuntimeError):
     def __init__(self, status: int, msg: str):
@@ -96,6 +101,8 @@ class _Synth(ctypes.Structure):
         ("n_rate", ctypes.c_double),
         ("first_read", ctypes.c_uint64),
         ("min_read_length", ctypes.c_int64),
+        ("layout", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -149,6 +156,11 @@ def lib() -> ctypes.CDLL:
         "kc_copy_device": ([vp, vp, vp, u64], ctypes.c_int),
         "kc_exchange_contexts": ([P(vp), u32], ctypes.c_int),
         "kc_merge_runs_device": ([vp, vp, P(u64), u32], ctypes.c_int),
+        "kc_checkpoint": ([vp], ctypes.c_int),
+        "kc_rollback": ([vp], ctypes.c_int),
+        "kc_commit": ([vp], ctypes.c_int),
+        "kc_count_file": ([P(vp), u32, ctypes.c_char_p, i64, u32, P(u64)], ctypes.c_int),
+        "kc_write_output_at": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -158,15 +170,16 @@ def lib() -> ctypes.CDLL:
     return L
 
 
-def _spec(n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0, min_read_length=0):
-    return _Synth(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length)
+def _spec(n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0, min_read_length=0, layout=0):
+    return _Synth(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length, layout, 0)
 
 
 def synth_fastq(n_reads: int, read_length: int, seed: int, genome_length: int = 0, n_rate: float = 0.0,
-                first_read: int = 0, min_read_length: int = 0) -> bytes:
-    """Synthetic FASTQ text (SURVEY §8d generator) produced by the library's host generator."""
+                first_read: int = 0, min_read_length: int = 0, layout: int = 0) -> bytes:
+    """Synthetic FASTQ text (SURVEY §8d generator) produced by the library's host generator
+    (layout 1: the sequences only, concatenated — a reference chunk)."""
     L = lib()
-    sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length)
+    sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length, layout)
     n = L.kc_synth_fastq_bytes(ctypes.byref(sp))
     buf = ctypes.create_string_buffer(n + 1)
     st = L.kc_synth_fastq_host(ctypes.byref(sp), buf, n + 1)
@@ -247,15 +260,43 @@ class Context:
         self._chk(self._L.kc_check_fastq(self._h, data, len(data), line_length, ctypes.byref(n)))
         return n.value
 
+    def count_chunk_host(self, addr: int, size: int, line_length: int):
+        """kc_count_chunk on raw host memory (e.g. a numpy array's address)."""
+        self._chk(self._L.kc_count_chunk(self._h, ctypes.cast(addr, ctypes.c_char_p), size, line_length))
+
+    def count_fastq_host(self, addr: int, size: int, line_length: int = 0) -> int:
+        """kc_count_fastq on raw host memory (e.g. a numpy array's address)."""
+        n = ctypes.c_uint64()
+        self._chk(self._L.kc_count_fastq(self._h, ctypes.cast(addr, ctypes.c_char_p), size, line_length,
+                                         ctypes.byref(n)))
+        return n.value
+
+    def copy_to_host_addr(self, addr: int, ptr: int, n: int):
+        """Device -> host copy into raw host memory (e.g. a numpy array's address)."""
+        self._chk(self._L.kc_copy_to_host(self._h, ctypes.c_void_p(addr), ctypes.c_void_p(ptr), n))
+
     def count_fastq_device(self, ptr: int, size: int, line_length: int = 0) -> int:
         n = ctypes.c_uint64()
         self._chk(self._L.kc_count_fastq_device(self._h, ctypes.c_void_p(ptr), size, line_length, ctypes.byref(n)))
         return n.value
 
+    def count_file(self, path: str, line_length: int = 0, mode: str = "auto") -> int:
+        """kc_count_file on this context alone; returns the reads counted."""
+        return count_file([self], path, line_length, mode)
+
+    def checkpoint(self):
+        self._chk(self._L.kc_checkpoint(self._h))
+
+    def rollback(self):
+        self._chk(self._L.kc_rollback(self._h))
+
+    def commit(self):
+        self._chk(self._L.kc_commit(self._h))
+
     def synth_device(self, n_reads, read_length, seed, genome_length=0, n_rate=0.0, first_read=0,
-                     min_read_length=0):
+                     min_read_length=0, layout=0):
         """Generates synthetic FASTQ directly in device memory; returns (ptr, nbytes)."""
-        sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length)
+        sp = _spec(n_reads, read_length, seed, genome_length, n_rate, first_read, min_read_length, layout)
         p = ctypes.c_void_p()
         n = ctypes.c_uint64()
         self._chk(self._L.kc_synth_fastq_device(self._h, ctypes.byref(sp), ctypes.byref(p), ctypes.byref(n)))
@@ -339,6 +380,11 @@ class Context:
         self.finish()
         self._chk(self._L.kc_write_output(self._h, path.encode(), fan_in, threads))
 
+    def write_output_at(self, path: str, offset: int):
+        """The finished table run into an existing file at `offset` (kc_write_output_at)."""
+        self.finish()
+        self._chk(self._L.kc_write_output_at(self._h, path.encode(), offset))
+
     def write_runs(self, prefix: str) -> List[str]:
         self.finish()
         n = ctypes.c_uint32()
@@ -358,6 +404,18 @@ class Context:
         s = Stats()
         self._chk(self._L.kc_get_stats(self._h, ctypes.byref(s)))
         return s.as_dict()
+
+
+def count_file(ctxs, path: str, line_length: int = 0, mode: str = "auto") -> int:
+    """kc_count_file: a FASTQ file read in pinned blocks and dealt to the
+    contexts (read-shard); mode auto | fastq | exact (include/kc.h)."""
+    L = lib()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    n = ctypes.c_uint64()
+    st = L.kc_count_file(arr, len(ctxs), path.encode(), line_length, _INPUT_MODES[mode], ctypes.byref(n))
+    if st:
+        raise KcError(st, f"{L.kc_strerror(st).decode()}: {L.kc_last_error(ctxs[0]._h).decode()}")
+    return n.value
 
 
 def owner_of(key0: int, world: int) -> int:

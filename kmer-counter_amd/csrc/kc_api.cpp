@@ -4,19 +4,23 @@
 //
 // Replaces PrepareGPU / processKMers / FreeGPU (GPUHandler.cu:397-519) and the
 // host aggregation of KMerCounter (KMerCounter.cpp:51-106).
+#include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kc.h"
 #include "kc_device.h"
 #include "kc_io.h"
+#include "kc_stage.h"
 
 using namespace kc;
 
@@ -96,6 +100,25 @@ struct kc_ctx {
     DevBuf fq_counts, fq_base, fq_tmp, seq_off, seq_end;
     DevBuf spill_keys2, rle_flags, rle_pos, rle_head, rle_tmp, run_keys, run_cnts, run_packed;
     DevBuf fin_keys[2], fin_cnts[2], fin_hist, fin_packed, fin_misc;
+
+    // host staging (kc_stage.h), created on the first host-pointer input or output
+    kc::Pool* pool = nullptr;
+    kc::PinnedRing* ring = nullptr;
+
+    // Pending batch: reads already indexed and 2-bit encoded into part_codes /
+    // part_inval (/ part_rlen) by kc_count_* calls, counted together at the
+    // next flush (when the next block does not fit, its read length differs,
+    // or at kc_finish). Many small calls thus count as one batch.
+    int64_t pend_L = 0;
+    bool pend_var = false;
+    uint64_t pend_reads = 0;
+    uint64_t flushes = 0;
+    uint64_t dev_total = 0;  // device memory (bytes)
+    // kc_checkpoint / kc_rollback: the pending state and the counters a
+    // rolled-back block may have changed
+    bool ckpt = false;
+    uint64_t ckpt_reads = 0, ckpt_flushes = 0, ckpt_st_reads = 0, ckpt_st_windows = 0;
+    uint64_t ckpt_stats[ST_N];
 
     // results
     bool finished = false;
@@ -331,8 +354,6 @@ static kc_status count_reads_table(kc_ctx* c, const uint8_t* base, const uint64_
     c->st.insert_ms += ms;
     c->st.last_count_ms = ms;
     c->engines_used |= 4u;
-    c->st.reads += n_reads;
-    c->st.windows += n_reads * nw;
     c->st.valid_kmers = c->stats_h[ST_VALID];
     c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
     return KC_OK;
@@ -445,7 +466,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         c->st.insert_launches++;
         c->st.insert_ms += t;
 
-        if (getenv("KC_P2_SKIP")) {  // timing experiment: keys are invalid, stop after P2
+        if (experiment_knob("KC_P2_SKIP")) {  // keys are invalid, stop after P2
             c->batches++;
             done += nr;
             continue;
@@ -552,8 +573,6 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         c->engines_used |= 2u;
         done += nr;
     }
-    c->st.reads += n_reads;
-    c->st.windows += n_reads * nw;
     c->st.valid_kmers = c->stats_h[ST_VALID];
     c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
     return KC_OK;
@@ -710,7 +729,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             max_reads = nr / 2;
             continue;
         }
-        if (getenv("KC_F_SKIP")) {  // timing experiment: records are invalid, stop after F
+        if (experiment_knob("KC_F_SKIP")) {  // records are invalid, stop after F
             c->batches++;
             done += nr;
             continue;
@@ -814,8 +833,6 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                     memcpy(c->stats_h, saved.data(), ST_N * 8);
                     c->rec_n = rec_batch0;
                     c->skm_hc = true;
-                    c->st.reads += done;
-                    c->st.windows += done * nw;
                     if (getenv("KC_DEBUG"))
                         fprintf(stderr, "kc: skm sample %llu distinct / %llu keys: key-prefix engine\n",
                                 (unsigned long long)dist_s, (unsigned long long)keys_s);
@@ -846,18 +863,9 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         c->batches++;
         done += nr;
     }
-    c->st.reads += n_reads;
-    c->st.windows += n_reads * nw;
     c->st.valid_kmers = c->stats_h[ST_VALID];
     c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
     return KC_OK;
-}
-
-// The engine count_reads takes for L reads (same order of tests): the skm and
-// key-prefix engines read 2-bit codes, the table engine the text
-static bool engine_reads_codes(const kc_ctx* c, int64_t L) {
-    if (c->skm && !c->skm_hc && skm_geometry((int)L, (int)c->k).ok) return true;
-    return c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= kMaxLds;
 }
 
 // pre0 >= 0: the reads are pre-encoded in part_codes / part_inval from read pre0
@@ -875,17 +883,155 @@ static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq
     return count_reads_table(c, base, seq_off, n_reads, L);
 }
 
-// K1. With `encoded` (counting), when the engine reads codes and the block is
-// one batch, the emit pass also encodes every read (fq_encode: the text is read
-// twice instead of three times) and *encoded is set; seq_off is then unset.
-static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_rec_out,
-                             bool* encoded = nullptr, bool varlen = false, bool two_pass_var = false) {
-    if (encoded) *encoded = false;
+// ---------------------------------------------------------------------------
+// pending batch (see kc_ctx::pend_*)
+// ---------------------------------------------------------------------------
+
+// Reads of length L one engine batch holds (its window capacity key_cap)
+static uint64_t batch_reads(const kc_ctx* c, int64_t L) {
+    const uint64_t m = c->key_cap / (uint64_t)(L - c->k + 1);
+    return m ? m : 1;
+}
+
+// Pending reads of length L allowed before a flush. While a checkpoint is held
+// the batch may grow past one engine batch (count_reads splits it) up to
+// 1/8 of the device's memory in codes (6 B per 16 bases), so a malformed block
+// later in the same file can still be rolled back.
+static uint64_t pend_room(const kc_ctx* c, int64_t L) {
+    const uint64_t b = batch_reads(c, L);
+    if (!c->ckpt) return b;
+    const uint64_t per_read = 6 * (uint64_t)groups_per_read((int)L) + 2;
+    const uint64_t budget = c->dev_total / 8 / per_read;
+    return budget > b ? budget : b;
+}
+
+// Grows b to at least `bytes`, keeping its first `keep` bytes.
+static kc_status grow_keep(kc_ctx* c, DevBuf& b, size_t bytes, size_t keep) {
+    if (b.p && b.bytes >= bytes) return KC_OK;
+    size_t want = bytes < 256 ? 256 : bytes;
+    if (b.p && want < b.bytes + b.bytes / 2) want = b.bytes + b.bytes / 2;
+    void* np = nullptr;
+    HIPCHK(c, hipMalloc(&np, want));
+    if (b.p && keep) HIPCHK(c, hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (b.p) HIPCHK(c, hipFree(b.p));
+    b.p = np;
+    b.bytes = want;
+    return KC_OK;
+}
+
+// Counts the pending batch (the engines: count_reads with pre-encoded reads).
+static kc_status pend_flush(kc_ctx* c) {
+    if (c->pend_reads == 0) return KC_OK;
+    const uint64_t n = c->pend_reads;
+    c->pend_reads = 0;  // a failed count is not counted again
+    c->flushes++;
+    if (!c->pend_var) return count_reads(c, nullptr, nullptr, n, c->pend_L, 0);
+    // variable-length reads: the slot padding's invalid windows are no holes;
+    // key 0^W is present iff a read of >= k bases holds a not-ACGT base
+    // (ST_VHOLE, written by the encoders) or a key-0 window was counted
+    kc_status s = sync_stats(c);
+    if (s) return s;
+    const uint64_t present0 = c->stats_h[ST_KEY0_PRESENT];
+    c->var_rlen = (const uint16_t*)c->part_rlen.p;
+    s = count_reads(c, nullptr, nullptr, n, c->pend_L, 0);
+    c->var_rlen = nullptr;
+    if (s) return s;
+    if ((s = sync_stats(c))) return s;
+    const uint64_t present = (present0 | c->stats_h[ST_VHOLE] | (c->stats_h[ST_KEY0] != 0 ? 1u : 0u)) ? 1u : 0u;
+    c->stats_h[ST_KEY0_PRESENT] = present;
+    HIPCHK(c, hipMemcpyAsync(c->stats + ST_KEY0_PRESENT, &c->stats_h[ST_KEY0_PRESENT], 8, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KC_OK;
+}
+
+// Room for n_new more pending reads of length L (fixed or variable): the
+// pending batch is counted first when it is of another kind or n_new would
+// not fit; the buffers grow keeping the pending reads. *off receives the
+// read index where the new reads go.
+static kc_status pend_reserve(kc_ctx* c, int64_t L, bool var, uint64_t n_new, uint64_t* off) {
+    kc_status s;
+    if (c->pend_reads && (c->pend_L != L || c->pend_var != var || c->pend_reads + n_new > pend_room(c, L)))
+        if ((s = pend_flush(c))) return s;
+    const uint64_t G = (uint64_t)groups_per_read((int)L);
+    const uint64_t keep = c->pend_reads * G, need = (c->pend_reads + n_new) * G;
+    if ((s = grow_keep(c, c->part_codes, need * 4 + 16, keep * 4)) ||
+        (s = grow_keep(c, c->part_inval, need * 2 + 16, keep * 2)))
+        return s;
+    if (var && (s = grow_keep(c, c->part_rlen, (c->pend_reads + n_new) * 2 + 16, c->pend_reads * 2))) return s;
+    c->pend_L = L;
+    c->pend_var = var;
+    *off = c->pend_reads;
+    return KC_OK;
+}
+
+// Encodes n_reads reads of device text into the pending batch, one engine
+// batch at a time (kernel E): reads at r * L (reference chunks, seq_off null)
+// or at seq_off[r] (variable-length: up to seq_end[r], padded slots).
+static kc_status pend_add_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, const uint64_t* seq_end,
+                                uint64_t n_reads, int64_t L, bool var) {
+    kc_status s;
+    const uint64_t G = (uint64_t)groups_per_read((int)L);
+    uint64_t done = 0;
+    while (done < n_reads) {
+        uint64_t free = 0;
+        if (c->pend_L == L && c->pend_var == var && c->pend_reads < pend_room(c, L))
+            free = pend_room(c, L) - c->pend_reads;
+        if (free == 0 || c->pend_reads == 0) free = pend_room(c, L);
+        const uint64_t m = n_reads - done < free ? n_reads - done : free;
+        uint64_t off = 0;
+        if ((s = pend_reserve(c, L, var, m, &off))) return s;
+        uint32_t* codes = (uint32_t*)c->part_codes.p + off * G;
+        uint16_t* inval = (uint16_t*)c->part_inval.p + off * G;
+        if (var) {
+            HIPCHK(c, launch_encode_reads_var(base, seq_off + done, seq_end + done, m, (int)L, (int)c->k, codes, inval,
+                                              (uint16_t*)c->part_rlen.p + off, c->stats, c->stream));
+        } else {
+            CountLaunch l;
+            l.base = base;
+            l.seq_off = seq_off;
+            l.read0 = done;
+            l.n_reads = m;
+            l.L = (int)L;
+            l.k = (int)c->k;
+            HIPCHK(c, launch_encode_reads(l, codes, inval, c->stream));
+        }
+        c->pend_reads += m;
+        done += m;
+    }
+    return KC_OK;
+}
+
+// The engine count_reads takes for L reads (same order of tests): the skm and
+// key-prefix engines read 2-bit codes, the table engine the text
+static bool engine_reads_codes(const kc_ctx* c, int64_t L) {
+    if (c->skm && !c->skm_hc && skm_geometry((int)L, (int)c->k).ok) return true;
+    return c->part && part_geometry((int)L, (int)c->k, 1).lds_scatter <= kMaxLds;
+}
+
+// K1 for one record-aligned FASTQ block in device memory (GPU FASTQ decode,
+// replacing FASTQFileReader::readData, FASTQFileReader.cpp:49-89): newline
+// counts per 16 KiB chunk -> each chunk's first line index -> one of
+//   fused   : index + checks + 2-bit encode in one read of the text, straight
+//             into the pending batch (fq_encode_k; fq_encode_k<true> for
+//             variable-length reads), when the block fits the pending room;
+//   two-pass: sequence offsets (fq_emit_k) + length check (fq_validate_k),
+//             then encode per batch (kernel E) — blocks larger than a batch,
+//             and the table engine, which counts the text itself.
+// The whole block is checked before any of its reads is pending or counted: a
+// malformed block changes nothing and returns KC_ERR_FORMAT. With count =
+// false only the checks run (kc_check_fastq).
+static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, bool var, bool count,
+                              uint64_t* n_rec_out, bool two_pass = false) {
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
     if ((s = ensure(c, c->fq_counts, nch * 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
         (s = ensure(c, c->fq_tmp, scan_tmp_elems(nch) * 8)))
         return s;
+    if ((s = sync_stats(c))) return s;
+    uint64_t snap[ST_N];
+    memcpy(snap, c->stats_h, sizeof(snap));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
     HIPCHK(c, launch_fq_count(base, n, (uint64_t*)c->fq_counts.p, c->stream));
@@ -895,76 +1041,94 @@ static kc_status index_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t
     HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->fq_base.p + nch - 1, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->fq_counts.p + nch - 1, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    uint64_t lines = tail[0] + tail[1];
+    const uint64_t lines = tail[0] + tail[1];
     if (lines % 4 != 0)
         return fail(c, KC_ERR_FORMAT, "FASTQ block has %llu lines, not a multiple of 4", (unsigned long long)lines);
-    uint64_t n_rec = lines / 4;
-    const uint64_t nw = (uint64_t)(L - c->k + 1);
-    const bool fuse = encoded && !varlen && !getenv("KC_NO_FQ_ENCODE") && L >= c->k && engine_reads_codes(c, L) &&
-                      n_rec * nw <= c->key_cap;
-    // variable-length reads: the fused index + encode unless a half held more
-    // records than its list (then again with the two-pass index)
-    const bool fuse_var = varlen && !two_pass_var && !getenv("KC_NO_FQ_ENCODE");
-    if (fuse) {
-        const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
-        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))) return s;
-        HIPCHK(c, launch_fq_encode(base, n, (uint64_t*)c->fq_base.p, n_rec, (int)L, (uint32_t*)c->part_codes.p,
-                                   (uint16_t*)c->part_inval.p, c->stats, c->stream));
-    } else if (fuse_var) {
-        const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
-        if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16)) ||
-            (s = ensure(c, c->part_rlen, n_rec * 2 + 16)))
-            return s;
-        HIPCHK(c, hipMemsetAsync(c->stats + ST_VHOLE, 0, 16, c->stream));
+    const uint64_t n_rec = lines / 4;
+    const uint64_t G = (uint64_t)groups_per_read((int)L);
+    const bool codes = engine_reads_codes(c, L);
+    if (var && (!c->part || !codes))
+        return fail(c, KC_ERR_ARG, "variable-length reads need an engine that reads encoded reads (L = %lld)",
+                    (long long)L);
+    // where the block's reads go: the pending batch when they fit it (after
+    // counting a pending batch of another kind or too full to take them)
+    uint64_t off = 0;
+    const bool into_pend = codes && n_rec > 0 && n_rec <= pend_room(c, L);
+    if (into_pend && (s = pend_reserve(c, L, var, n_rec, &off))) return s;
+    const bool no_fuse = getenv("KC_NO_FQ_ENCODE") != nullptr;  // path selector (tests): same bytes either way
+    const bool fused = into_pend && !var && !no_fuse;                               // fq_encode_k
+    const bool whole_var = into_pend && var;                                         // the block encoded whole
+    const bool fused_var = whole_var && !two_pass && !no_fuse && fq_encode_var_ok((int)L);  // fq_encode_k<true>
+    if (fused) {
+        HIPCHK(c, launch_fq_encode(base, n, (uint64_t*)c->fq_base.p, n_rec, (int)L,
+                                   (uint32_t*)c->part_codes.p + off * G, (uint16_t*)c->part_inval.p + off * G,
+                                   c->stats, c->stream));
+    } else if (fused_var) {
         HIPCHK(c, launch_fq_encode_var(base, n, (uint64_t*)c->fq_base.p, n_rec, (int)L, (int)c->k,
-                                       (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p,
-                                       (uint16_t*)c->part_rlen.p, c->stats, c->stream));
+                                       (uint32_t*)c->part_codes.p + off * G, (uint16_t*)c->part_inval.p + off * G,
+                                       (uint16_t*)c->part_rlen.p + off, c->stats, c->stream));
     } else {
         if ((s = ensure(c, c->seq_off, n_rec * 8 + 8)) || (s = ensure(c, c->seq_end, n_rec * 8 + 8))) return s;
         HIPCHK(c, launch_fq_emit(base, n, (uint64_t*)c->fq_base.p, (uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p,
                                  n_rec, c->stats, c->stream));
-        if (varlen) {
-            // sequence lengths up to L, checked (and the reads encoded) by E-var
-            const uint64_t ng = n_rec * (uint64_t)groups_per_read((int)L);
-            if ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16)) ||
-                (s = ensure(c, c->part_rlen, n_rec * 2 + 16)))
-                return s;
-            HIPCHK(c, hipMemsetAsync(c->stats + ST_VHOLE, 0, 16, c->stream));
-            HIPCHK(c, launch_encode_reads_var(base, (const uint64_t*)c->seq_off.p, (const uint64_t*)c->seq_end.p, n_rec,
-                                              (int)L, (int)c->k, (uint32_t*)c->part_codes.p,
-                                              (uint16_t*)c->part_inval.p, (uint16_t*)c->part_rlen.p, c->stats,
-                                              c->stream));
-        } else {
-            HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
-                                         c->stream));
-        }
+        HIPCHK(c, launch_fq_validate((uint64_t*)c->seq_off.p, (uint64_t*)c->seq_end.p, n_rec, (int)L, c->stats,
+                                     c->stream, var));
+        if (whole_var)
+            HIPCHK(c, launch_encode_reads_var(base, (const uint64_t*)c->seq_off.p, (const uint64_t*)c->seq_end.p,
+                                              n_rec, (int)L, (int)c->k, (uint32_t*)c->part_codes.p + off * G,
+                                              (uint16_t*)c->part_inval.p + off * G, (uint16_t*)c->part_rlen.p + off,
+                                              c->stats, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     if ((s = sync_stats(c))) return s;
     float t = 0.f;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
     c->st.decode_ms += t;
-    uint64_t e = c->stats_h[ST_ERR];
-    if (fuse_var && (e & ERR_FQ_LIST)) {
-        HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
+    const uint64_t e = c->stats_h[ST_ERR];
+    auto restore = [&]() -> kc_status {
+        // the counters the index / encode kernels touched (errors, variable-length hole flag and windows)
+        snap[ST_ERR] = 0;
+        HIPCHK(c, hipMemcpyAsync(c->stats, snap, sizeof(snap), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->stats_h[ST_ERR] = 0;
-        return index_fastq(c, base, n, L, n_rec_out, encoded, varlen, true);
+        memcpy(c->stats_h, snap, sizeof(snap));
+        return KC_OK;
+    };
+    if (fused_var && (e & ERR_FQ_LIST)) {
+        // a half held more records than the fused list: the two-pass index
+        if ((s = restore())) return s;
+        return ingest_fastq(c, base, n, L, var, count, n_rec_out, true);
     }
     if (e) {
         std::string why;
         if (e & ERR_FQ_NOT_AT) why += " record-does-not-start-with-@";
         if (e & ERR_FQ_NO_PLUS) why += " no-+-line-after-sequence";
-        if (e & ERR_FQ_SEQ_LEN) why += varlen ? " sequence-longer-than-L" : " sequence-length-differs-from-L";
+        if (e & ERR_FQ_SEQ_LEN) why += var ? " sequence-longer-than-L" : " sequence-length-differs-from-L";
         if (e & ERR_FQ_TOO_MANY) why += " index-overflow";
         if (e & ERR_FQ_NO_FINAL_NL) why += " block-does-not-end-with-newline";
-        HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
-        c->stats_h[ST_ERR] = 0;
+        if ((s = restore())) return s;
         return fail(c, KC_ERR_FORMAT, "FASTQ block is not 4-line records with %s%lld-base reads:%s",
-                    varlen ? "at most " : "", (long long)L, why.c_str());
+                    var ? "at most " : "", (long long)L, why.c_str());
     }
-    *n_rec_out = n_rec;
-    if (encoded) *encoded = fuse;
+    if (n_rec_out) *n_rec_out = n_rec;
+    if (!count) return var ? restore() : KC_OK;  // (the encoded reads past pend_reads are dropped)
+    const uint64_t vwin0 = snap[ST_VWIN];
+    c->st.reads += n_rec;
+    if (fused || whole_var) {
+        c->pend_reads += n_rec;
+    } else if (codes) {
+        if ((s = pend_add_reads(c, base, (const uint64_t*)c->seq_off.p, (const uint64_t*)c->seq_end.p, n_rec, L, var)))
+            return s;
+    } else {
+        // the table engine reads the text: counted now
+        if ((s = pend_flush(c))) return s;
+        if ((s = count_reads(c, base, (const uint64_t*)c->seq_off.p, n_rec, L))) return s;
+    }
+    if (var) {
+        if ((s = sync_stats(c))) return s;
+        c->st.windows += c->stats_h[ST_VWIN] - vwin0;  // the reads' own windows, not the padded slots'
+    } else {
+        c->st.windows += n_rec * (uint64_t)(L - c->k + 1);
+    }
     return KC_OK;
 }
 
@@ -1071,6 +1235,8 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
         if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess && prop.multiProcessorCount > 0)
             c->n_cu = prop.multiProcessorCount;
     }
+    size_t mfree = 0, mtotal = 0;
+    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess) c->dev_total = mtotal;
     s = kc_reset(c);
     if (s) return bail(s);
     *out = c;
@@ -1080,6 +1246,8 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
 void kc_destroy(kc_ctx* c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    delete c->ring;  // waits for its DMAs
+    delete c->pool;
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     DevBuf* bufs[] = {&c->in_stage, &c->fq_counts, &c->fq_base, &c->fq_tmp, &c->seq_off, &c->seq_end,
@@ -1146,10 +1314,43 @@ kc_status kc_reset(kc_ctx* c) {
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
     c->spilled_flushed = 0;
+    c->pend_reads = 0;
+    c->pend_L = 0;
+    c->pend_var = false;
+    c->ckpt = false;
     c->finished = false;
     c->n_records = 0;
     memset(&c->st, 0, sizeof(c->st));
     c->st.table_capacity = c->cap;
+    return KC_OK;
+}
+
+// Host staging (pinned ring + copy pool), created on first use.
+static kc_status stage_init(kc_ctx* c) {
+    if (!c->pool) c->pool = new kc::Pool(8);
+    if (!c->ring) {
+        c->ring = new kc::PinnedRing();
+        HIPCHK(c, c->ring->init((size_t)64 << 20, 4));
+    }
+    return KC_OK;
+}
+
+// Reference-exact chunk in device memory: floor(size / L) reads at stride L
+// (GPUHandler.cu:13-15), encoded into the pending batch (codes engines) or
+// counted from the text (table engine).
+static kc_status chunk_device(kc_ctx* c, const uint8_t* d, int64_t size, int64_t L) {
+    if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
+    const uint64_t n = (uint64_t)(size / L);
+    if (n == 0) return KC_OK;
+    kc_status s;
+    if (engine_reads_codes(c, L)) {
+        if ((s = pend_add_reads(c, d, nullptr, nullptr, n, L, false))) return s;
+    } else {
+        if ((s = pend_flush(c))) return s;
+        if ((s = count_reads(c, d, nullptr, n, L))) return s;
+    }
+    c->st.reads += n;
+    c->st.windows += n * (uint64_t)(L - c->k + 1);
     return KC_OK;
 }
 
@@ -1158,57 +1359,29 @@ kc_status kc_count_chunk_device(kc_ctx* c, const void* d_chunk, int64_t size, in
     kc_status s = check_line(c, L);
     if (s) return s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    uint64_t n = (uint64_t)(size / L);
-    if (n == 0) return KC_OK;
-    return count_reads(c, (const uint8_t*)d_chunk, nullptr, n, L);
+    if ((s = chunk_device(c, (const uint8_t*)d_chunk, size, L))) return s;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's buffer was read by the encoder
+    return KC_OK;
 }
 
+// Host chunk: its whole reads go through the pinned ring into the staging
+// buffer; the encode is queued behind the upload on the ctx stream and the
+// call returns as soon as the caller's bytes are in pinned memory, so
+// consecutive chunks (the reference's ~7.8 MB at gpuMemoryLimit=1e8,
+// KMerCounter.cpp:193-212) stream at the PCIe rate.
 kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) {
     if (!c || (!chunk && size > 0) || size < 0) return KC_ERR_ARG;
     kc_status s = check_line(c, L);
     if (s) return s;
-    if (size / L == 0) return KC_OK;
+    const uint64_t n = (uint64_t)(size / L);
+    if (n == 0) return KC_OK;
+    if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if ((s = ensure(c, c->in_stage, (size_t)size + 64))) return s;
-    HIPCHK(c, hipMemcpyAsync(c->in_stage.p, chunk, (size_t)size, hipMemcpyHostToDevice, c->stream));
-    return count_reads(c, (const uint8_t*)c->in_stage.p, nullptr, (uint64_t)(size / L), L);
-}
-
-// KC_FLAG_VARLEN: reads of 0..L bases, each counted as a reference read of
-// its own length (the reference concatenates sequences
-// without separators and cuts them at multiples of the first read's length,
-// FASTQFileReader.cpp:57-79, GPUHandler.cu:13-15, so it has no defined result
-// here). The reads are encoded into L-base slots padded with not-ACGT bases,
-// so every engine that reads codes counts exactly their own windows. The
-// padding's invalid windows are no holes: key 0^W is present iff a read of
-// >= k bases holds a not-ACGT base (ST_VHOLE) or a key-0 window was counted.
-static kc_status fastq_device_var(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, uint64_t* n_reads,
-                                  bool count) {
-    kc_status s;
-    if (!c->part || !engine_reads_codes(c, L))
-        return fail(c, KC_ERR_ARG, "variable-length reads need an engine that reads encoded reads (L = %lld)",
-                    (long long)L);
-    uint64_t n_rec = 0;
-    if ((s = index_fastq(c, base, n, L, &n_rec, nullptr, true))) return s;
-    if (count && n_rec > 0) {
-        if ((s = sync_stats(c))) return s;
-        const uint64_t present0 = c->stats_h[ST_KEY0_PRESENT];
-        const uint64_t vhole = c->stats_h[ST_VHOLE], vwin = c->stats_h[ST_VWIN];
-        const uint64_t win0 = c->st.windows;
-        c->var_rlen = (const uint16_t*)c->part_rlen.p;
-        s = count_reads(c, base, nullptr, n_rec, L, 0);
-        c->var_rlen = nullptr;
-        if (s) return s;
-        if ((s = sync_stats(c))) return s;
-        const uint64_t present = (present0 | vhole | (c->stats_h[ST_KEY0] != 0 ? 1u : 0u)) ? 1u : 0u;
-        c->stats_h[ST_KEY0_PRESENT] = present;
-        HIPCHK(c, hipMemcpyAsync(c->stats + ST_KEY0_PRESENT, &c->stats_h[ST_KEY0_PRESENT], 8, hipMemcpyHostToDevice,
-                                 c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->st.windows = win0 + vwin;  // the reads' own windows, not the padded slots'
-    }
-    if (n_reads) *n_reads = n_rec;
-    return KC_OK;
+    if ((s = stage_init(c))) return s;
+    const size_t bytes = (size_t)(n * (uint64_t)L);
+    if ((s = ensure(c, c->in_stage, bytes + 64))) return s;
+    HIPCHK(c, c->ring->upload(c->in_stage.p, chunk, bytes, c->stream, c->pool));
+    return chunk_device(c, (const uint8_t*)c->in_stage.p, (int64_t)bytes, L);
 }
 
 static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_t L, uint64_t* n_reads,
@@ -1221,25 +1394,21 @@ static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_
     kc_status s = check_line(c, L);
     if (s) return s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    uint64_t n_rec = 0;
-    if (c->cfg.flags & KC_FLAG_VARLEN) return fastq_device_var(c, (const uint8_t*)d_fastq, n, L, n_reads, count);
-    bool enc = false;
-    if ((s = index_fastq(c, (const uint8_t*)d_fastq, n, L, &n_rec, count ? &enc : nullptr))) return s;
-    if (count && (s = count_reads(c, (const uint8_t*)d_fastq, enc ? nullptr : (const uint64_t*)c->seq_off.p, n_rec, L,
-                                  enc ? 0 : -1)))
-        return s;
-    if (n_reads) *n_reads = n_rec;
-    return KC_OK;
+    return ingest_fastq(c, (const uint8_t*)d_fastq, n, L, (c->cfg.flags & KC_FLAG_VARLEN) != 0, count, n_reads);
 }
 
+// Host FASTQ block: uploaded through the pinned ring (pageable) or directly
+// (pinned), then decoded on the GPU (ingest_fastq, which waits for the
+// checks: a malformed block is reported by this call).
 static kc_status fastq_host(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, uint64_t* n_reads, bool count) {
     if (!c || (!fastq && n > 0)) return KC_ERR_ARG;
     if (n_reads) *n_reads = 0;
     if (n == 0) return KC_OK;
     kc_status s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if ((s = stage_init(c))) return s;
     if ((s = ensure(c, c->in_stage, (size_t)n + 64))) return s;
-    HIPCHK(c, hipMemcpyAsync(c->in_stage.p, fastq, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, c->ring->upload(c->in_stage.p, fastq, n, c->stream, c->pool));
     return fastq_device(c, c->in_stage.p, n, L, n_reads, count);
 }
 
@@ -1253,6 +1422,206 @@ kc_status kc_count_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, ui
 
 kc_status kc_check_fastq(kc_ctx* c, const char* fastq, uint64_t n, int64_t L, uint64_t* n_reads) {
     return fastq_host(c, fastq, n, L, n_reads, false);
+}
+
+// ---- file input (InputFileHandler / FASTQFileReader + the Start loop) ----
+
+static const size_t kFileBlock = (size_t)256 << 20;
+
+// Block size of the file reader; KC_FILE_BLOCK (bytes) is a path selector for
+// tests (many blocks from small files: cut search, carries; same counts).
+static size_t file_block_bytes() {
+    if (const char* e = getenv("KC_FILE_BLOCK")) {
+        const long long v = atoll(e);
+        if (v >= 4096) return (size_t)v;
+    }
+    return kFileBlock;
+}
+
+// A block of the file reader (pinned): DMA straight into the staging buffer,
+// then the GPU decode (which waits for its checks, so the reader may refill
+// the block when this returns).
+static kc_status file_block(kc_ctx* c, const char* p, size_t n, int64_t L, bool count, uint64_t* got) {
+    kc_status s;
+    if ((s = ensure(c, c->in_stage, n + 64))) return s;
+    HIPCHK(c, hipMemcpyAsync(c->in_stage.p, p, n, hipMemcpyHostToDevice, c->stream));
+    return fastq_device(c, c->in_stage.p, n, L, got, count);
+}
+
+// Streams the file's blocks to the contexts (each block to whichever context
+// is free: counting is order-independent). On the first failing block every
+// context stops; *failed names the context that reported it.
+static kc_status file_blocks(kc_ctx* const* ctxs, uint32_t n_ctx, const char* path, int64_t L, bool count,
+                             uint64_t* reads, kc_ctx** failed) {
+    kc::FastqFileReader rd(file_block_bytes(), (int)n_ctx + 2, 8);
+    std::string err;
+    *failed = ctxs[0];
+    if (!rd.open(path, &err)) return fail(ctxs[0], KC_ERR_IO, "%s", err.c_str());
+    std::atomic<bool> stop(false);
+    std::vector<kc_status> st(n_ctx, KC_OK);
+    std::vector<uint64_t> nr(n_ctx, 0);
+    auto work = [&](uint32_t g) {
+        kc_ctx* c = ctxs[g];
+        if (hipSetDevice(c->cfg.device) != hipSuccess) {
+            st[g] = fail(c, KC_ERR_HIP, "hipSetDevice(%d)", c->cfg.device);
+            stop = true;
+            return;
+        }
+        kc::FastqFileReader::Block b;
+        while (!stop && rd.next(&b)) {
+            uint64_t got = 0;
+            kc_status s = file_block(c, b.p, b.n, L, count, &got);
+            rd.release(b);
+            if (s) {
+                st[g] = s;
+                stop = true;
+                return;
+            }
+            nr[g] += got;
+        }
+    };
+    if (n_ctx == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (uint32_t g = 0; g < n_ctx; g++) th.emplace_back(work, g);
+        for (auto& t : th) t.join();
+    }
+    for (uint32_t g = 0; g < n_ctx; g++)
+        if (st[g]) {
+            *failed = ctxs[g];
+            return st[g];
+        }
+    err = rd.error();
+    if (!err.empty()) return fail(ctxs[0], KC_ERR_IO, "%s: %s", path, err.c_str());
+    for (uint32_t g = 0; g < n_ctx; g++) *reads += nr[g];
+    return KC_OK;
+}
+
+// inputMode=exact: the reference's chunks (ExactChunker, GetChunkSize with
+// the ctx's gpuMemoryLimit) through kc_count_chunk.
+static kc_status file_exact(kc_ctx* c, const char* path, int64_t L, uint64_t* reads) {
+    const int64_t limit = c->cfg.gpu_memory_limit ? (int64_t)c->cfg.gpu_memory_limit : 100000000;
+    const int64_t cs = kc::reference_chunk_size(L, c->k, limit);
+    kc::ExactChunker ch(path, L);
+    std::vector<char> buf;
+    while (!ch.done()) {
+        const int64_t n = ch.next(cs, buf);
+        if (n > 0 && n >= L) {  // KMerCounter.cpp:130
+            kc_status s = kc_count_chunk(c, buf.data(), n, L);
+            if (s) return s;
+            *reads += (uint64_t)(n / L);
+        }
+    }
+    return KC_OK;
+}
+
+extern "C" kc_status kc_count_file(kc_ctx* const* ctxs, uint32_t n_ctx, const char* path, int64_t L, uint32_t mode,
+                                   uint64_t* n_reads) {
+    if (!ctxs || n_ctx == 0 || !path || mode > KC_INPUT_EXACT) return KC_ERR_ARG;
+    for (uint32_t g = 0; g < n_ctx; g++)
+        if (!ctxs[g] || ctxs[g]->k != ctxs[0]->k) return KC_ERR_ARG;
+    kc_ctx* c0 = ctxs[0];
+    const bool var = (c0->cfg.flags & KC_FLAG_VARLEN) != 0;
+    if (n_reads) *n_reads = 0;
+    if (L == 0) L = var ? c0->cfg.line_length : kc::file_line2_length(path);
+    // reads shorter than k have no windows (the reference's CLI skips such files)
+    if (L < c0->k) return KC_OK;
+    kc_status s = check_line(c0, L);
+    if (s) return s;
+    uint64_t reads = 0;
+    kc_ctx* failed = nullptr;
+    if (mode == KC_INPUT_EXACT) {
+        if (var) return fail(c0, KC_ERR_ARG, "variable-length reads have no reference chunk form");
+        s = file_exact(c0, path, L, &reads);
+    } else if (mode == KC_INPUT_FASTQ || var) {
+        s = file_blocks(ctxs, n_ctx, path, L, true, &reads, &failed);
+    } else {
+        // auto: GPU decode; a malformed block sends the whole file to the
+        // reference chunker. The file is read once when its reads fit every
+        // context's checkpoint room (rolled back on a malformed block), else
+        // it is validated first.
+        struct stat sb;
+        if (stat(path, &sb) != 0) return fail(c0, KC_ERR_IO, "cannot stat %s", path);
+        const uint64_t est = (uint64_t)sb.st_size / (uint64_t)(2 * L + 6) + 1;  // records are >= 2L + 6 bytes
+        bool once = true;
+        for (uint32_t g = 0; g < n_ctx; g++) {
+            kc_ctx* c = ctxs[g];
+            c->ckpt = true;
+            const uint64_t room = pend_room(c, L);
+            c->ckpt = false;
+            if ((c->pend_reads && (c->pend_L != L || c->pend_var)) || (c->pend_L == L ? c->pend_reads : 0) + est > room)
+                once = false;
+        }
+        bool exact = false;
+        if (once) {
+            for (uint32_t g = 0; g < n_ctx; g++)
+                if ((s = kc_checkpoint(ctxs[g]))) return s;
+            s = file_blocks(ctxs, n_ctx, path, L, true, &reads, &failed);
+            if (s == KC_ERR_FORMAT) {
+                for (uint32_t g = 0; g < n_ctx; g++) {
+                    kc_status r = kc_rollback(ctxs[g]);
+                    if (r) return r;
+                }
+                exact = true;
+                reads = 0;
+            } else {
+                for (uint32_t g = 0; g < n_ctx; g++) kc_commit(ctxs[g]);
+            }
+        } else {
+            uint64_t dummy = 0;
+            s = file_blocks(ctxs, n_ctx, path, L, false, &dummy, &failed);
+            if (s == KC_ERR_FORMAT) {
+                exact = true;
+            } else if (!s) {
+                s = file_blocks(ctxs, n_ctx, path, L, true, &reads, &failed);
+            }
+        }
+        if (exact) s = file_exact(c0, path, L, &reads);
+    }
+    if (s) {
+        if (failed && failed != c0) c0->err = failed->err;  // the caller reads ctxs[0]'s message
+        return s;
+    }
+    if (n_reads) *n_reads = reads;
+    return KC_OK;
+}
+
+kc_status kc_checkpoint(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    kc_status s = sync_stats(c);
+    if (s) return s;
+    c->ckpt = true;
+    c->ckpt_reads = c->pend_reads;
+    c->ckpt_flushes = c->flushes;
+    c->ckpt_st_reads = c->st.reads;
+    c->ckpt_st_windows = c->st.windows;
+    memcpy(c->ckpt_stats, c->stats_h, sizeof(c->ckpt_stats));
+    return KC_OK;
+}
+
+kc_status kc_rollback(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->ckpt) return fail(c, KC_ERR_STATE, "no checkpoint");
+    c->ckpt = false;
+    if (c->flushes != c->ckpt_flushes || c->finished)
+        return fail(c, KC_ERR_STATE, "reads were counted since the checkpoint: it cannot be rolled back");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    c->pend_reads = c->ckpt_reads;
+    c->st.reads = c->ckpt_st_reads;
+    c->st.windows = c->ckpt_st_windows;
+    HIPCHK(c, hipMemcpyAsync(c->stats, c->ckpt_stats, sizeof(c->ckpt_stats), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    memcpy(c->stats_h, c->ckpt_stats, sizeof(c->ckpt_stats));
+    return KC_OK;
+}
+
+kc_status kc_commit(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    c->ckpt = false;
+    return KC_OK;
 }
 
 static kc_status sort_reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, bool dups, uint64_t* n_out);
@@ -1499,6 +1868,8 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     }
     HIPCHK(c, hipSetDevice(c->cfg.device));
     kc_status s;
+    c->ckpt = false;
+    if ((s = pend_flush(c))) return s;
     if ((s = sync_stats(c))) return s;
     if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;
     const int W = c->W;
@@ -1578,31 +1949,60 @@ kc_status kc_device_records(kc_ctx* c, const void** d_records, uint64_t* n_bytes
     return KC_OK;
 }
 
+// The finished table run (SortedKMerFile bytes) to host memory through the
+// pinned ring, the pieces copied out by the pool while the next DMA runs.
 static kc_status table_run_to_host(kc_ctx* c, std::vector<uint8_t>* mem) {
-    uint64_t bytes = c->n_records * c->rs;
+    const uint64_t bytes = c->n_records * c->rs;
     mem->resize(bytes);
+    if (!bytes) return KC_OK;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    kc_status s = stage_init(c);
+    if (s) return s;
+    uint8_t* dst = mem->data();
+    HIPCHK(c, c->ring->download(c->fin_packed.p, bytes, c->stream, [&](const char* p, size_t n, size_t off) {
+        kc::par_memcpy(c->pool, dst + off, p, n);
+        return true;
+    }));
+    return KC_OK;
+}
+
+// The finished table run into a file at byte `at` (a new file, truncated,
+// when `truncate`): device -> pinned slot DMAs overlap the writes of the
+// previous slot.
+static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0, bool truncate = true) {
+    const uint64_t bytes = c->n_records * c->rs;
+    int fd = open(path, O_CREAT | O_WRONLY | (truncate ? O_TRUNC : 0), 0644);
+    if (fd < 0) return fail(c, KC_ERR_IO, "cannot open output file %s", path);
+    kc_status s = KC_OK;
     if (bytes) {
         HIPCHK(c, hipSetDevice(c->cfg.device));
-        HIPCHK(c, hipMemcpyAsync(mem->data(), c->fin_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if ((s = stage_init(c))) {
+            close(fd);
+            return s;
+        }
+        hipError_t e = c->ring->download(c->fin_packed.p, bytes, c->stream, [&](const char* p, size_t n, size_t off) {
+            size_t done = 0;
+            while (done < n) {
+                ssize_t w = pwrite(fd, p + done, n - done, (off_t)(at + off + done));
+                if (w <= 0) return false;
+                done += (size_t)w;
+            }
+            return true;
+        });
+        if (e == hipErrorUnknown) s = fail(c, KC_ERR_IO, "short write to %s", path);
+        else if (e != hipSuccess) s = fail(c, KC_ERR_HIP, "output copy: %s", hipGetErrorString(e));
     }
-    return KC_OK;
+    if (close(fd) != 0 && !s) s = fail(c, KC_ERR_IO, "cannot close %s", path);
+    return s;
 }
 
 kc_status kc_write_output(kc_ctx* c, const char* path, uint32_t fan_in, uint32_t threads) {
     if (!c || !path) return KC_ERR_ARG;
     if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (c->runs.empty()) return table_run_to_file(c, path);
     std::vector<uint8_t> table_run;
     kc_status s = table_run_to_host(c, &table_run);
     if (s) return s;
-    if (c->runs.empty()) {
-        FILE* f = fopen(path, "wb");
-        if (!f) return fail(c, KC_ERR_IO, "cannot open output file %s", path);
-        size_t w = table_run.empty() ? 0 : fwrite(table_run.data(), 1, table_run.size(), f);
-        int e = fclose(f);
-        if (w != table_run.size() || e != 0) return fail(c, KC_ERR_IO, "short write to %s", path);
-        return KC_OK;
-    }
     std::vector<RunSource> src;
     RunSource t;
     t.mem = table_run.data();
@@ -1623,6 +2023,13 @@ kc_status kc_write_output(kc_ctx* c, const char* path, uint32_t fan_in, uint32_t
     if (!merge_tree(src, path, c->W, fan_in, threads, tmp_prefix, &err))
         return fail(c, KC_ERR_IO, "%s", err.c_str());
     return KC_OK;
+}
+
+kc_status kc_write_output_at(kc_ctx* c, const char* path, uint64_t offset) {
+    if (!c || !path) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist: use kc_write_output");
+    return table_run_to_file(c, path, offset, false);
 }
 
 kc_status kc_write_runs(kc_ctx* c, const char* prefix, uint32_t* n_runs) {
@@ -1698,7 +2105,7 @@ kc_status kc_merge_files(const char* const* inputs, uint32_t n_inputs, const cha
 
 uint64_t kc_synth_fastq_bytes(const kc_synth_spec* sp) {
     if (!sp) return 0;
-    return synth_bytes(sp->first_read, sp->n_reads, sp->read_length);
+    return synth_bytes(sp->first_read, sp->n_reads, sp->read_length, (int)sp->layout);
 }
 
 static SynthArgs synth_args(const kc_synth_spec* sp) {
@@ -1709,6 +2116,7 @@ static SynthArgs synth_args(const kc_synth_spec* sp) {
     a.genome = sp->genome_length;
     a.L = sp->read_length;
     a.Lmin = sp->min_read_length;
+    a.layout = (int)sp->layout;
     double thr = sp->n_rate * 9007199254740992.0;
     a.n_threshold = sp->n_rate <= 0 ? 0 : (thr >= 9007199254740992.0 ? (1ull << 53) : (uint64_t)thr);
     return a;
@@ -1716,7 +2124,8 @@ static SynthArgs synth_args(const kc_synth_spec* sp) {
 
 static bool synth_ok(const kc_synth_spec* sp) {
     return sp && sp->read_length > 0 && (sp->genome_length == 0 || sp->genome_length >= (uint64_t)sp->read_length) &&
-           sp->min_read_length >= 0 && sp->min_read_length <= sp->read_length;
+           sp->min_read_length >= 0 && sp->min_read_length <= sp->read_length && sp->layout <= 1 &&
+           (sp->layout == 0 || sp->min_read_length == 0 || sp->min_read_length == sp->read_length);
 }
 
 kc_status kc_synth_fastq_host(const kc_synth_spec* sp, char* dst, uint64_t dst_bytes) {

@@ -47,6 +47,7 @@
 #include <unistd.h>
 
 #include <fstream>
+#include <initializer_list>
 #include <string>
 #include <thread>
 #include <vector>
@@ -78,6 +79,7 @@ bool starts(const char* s, const char* p) { return strncmp(s, p, strlen(p)) == 0
 
 Options parse(int argc, char** argv) {
     Options o;
+    std::string read_lengths = "fixed", output_format = "sorted";
     for (int i = 0; i < argc; i++) {
         const char* a = argv[i];
         if (starts(a, "kmerLength=")) {
@@ -113,24 +115,32 @@ Options parse(int argc, char** argv) {
         if (starts(a, "exchange=")) o.exchange = a + 9;
         if (starts(a, "tableBytes=")) o.table_bytes = strtoull(a + 11, nullptr, 10);
         if (starts(a, "quiet=")) o.quiet = atoi(a + 6) != 0;
-        if (starts(a, "readLengths=")) o.varlen = strcmp(a + 12, "variable") == 0;
-        if (starts(a, "outputFormat=")) o.dump = strcmp(a + 13, "dump") == 0;
+        if (starts(a, "readLengths=")) read_lengths = a + 12;
+        if (starts(a, "outputFormat=")) output_format = a + 13;
     }
     if (o.gpus < 1) o.gpus = 1;
-    if (o.exchange != "none" && o.exchange != "alltoall") {
-        fprintf(stderr, "exchange must be none or alltoall\n");
+    // additive keys take only their listed values (a typo must not select a
+    // different mode silently)
+    auto one_of = [](const char* key, const std::string& v, std::initializer_list<const char*> ok) {
+        for (const char* x : ok)
+            if (v == x) return;
+        std::string all;
+        for (const char* x : ok) all += std::string(all.empty() ? "" : "|") + x;
+        fprintf(stderr, "kmer-counter: %s=%s: expected %s\n", key, v.c_str(), all.c_str());
+        exit(1);
+    };
+    one_of("exchange", o.exchange, {"none", "alltoall"});
+    one_of("inputMode", o.input_mode, {"auto", "fastq", "exact"});
+    one_of("readLengths", read_lengths, {"fixed", "variable"});
+    one_of("outputFormat", output_format, {"sorted", "dump"});
+    o.varlen = read_lengths == "variable";
+    o.dump = output_format == "dump";
+    if (o.varlen && o.input_mode == "exact") {
+        // the reference's chunker has no variable-length form
+        fprintf(stderr, "kmer-counter: readLengths=variable cannot be combined with inputMode=exact\n");
         exit(1);
     }
     return o;
-}
-
-// KMerCounter::GetChunkSize (KMerCounter.cpp:193-212).
-int64_t chunk_size(int64_t L, int64_t k, int64_t limit) {
-    int64_t kb = (k + 3) / 4;
-    int64_t rec = ((kb + 7) / 8 + 1) * 8;
-    int64_t per = rec * (L - k + 1);
-    if (per - 1 == 0) return 0;
-    return L * ((limit - L) / (per - 1));
 }
 
 // ---------------------------------------------------------------------------
@@ -235,81 +245,6 @@ struct Mapped {
     }
 };
 
-// Splits a FASTQ byte range into blocks of whole 4-line groups of roughly
-// `target` bytes (line counting from the start, so alignment is exact).
-std::vector<std::pair<size_t, size_t>> fastq_blocks(const char* p, size_t n, size_t target) {
-    std::vector<std::pair<size_t, size_t>> out;
-    size_t start = 0;
-    while (start < n) {
-        if (n - start <= target) {
-            out.push_back({start, n});
-            break;
-        }
-        size_t pos = start + target;
-        // walk back to the start of the 4-line group containing pos: count the
-        // lines of [start, pos) and move to the end of the current group
-        size_t lines = 0;
-        const char* q = p + start;
-        const char* e = p + pos;
-        while (q < e) {
-            const char* nl = (const char*)memchr(q, '\n', (size_t)(e - q));
-            if (!nl) break;
-            lines++;
-            q = nl + 1;
-        }
-        size_t cut = (size_t)(q - p);
-        while (lines % 4 != 0 && cut < n) {
-            const char* nl = (const char*)memchr(p + cut, '\n', n - cut);
-            cut = nl ? (size_t)(nl - p) + 1 : n;
-            lines++;
-        }
-        if (cut <= start) cut = n;
-        out.push_back({start, cut});
-        start = cut;
-    }
-    return out;
-}
-
-// The reference's chunker (FASTQFileReader::readData, FASTQFileReader.cpp:49-89)
-// driven the way InputFileHandler::read and KMerCounter::Start drive it
-// (InputFileHandler.cpp:82-95, KMerCounter.cpp:123-143).
-class ExactChunker {
-  public:
-    ExactChunker(const std::string& path, int64_t L) : L_(L) {
-        std::ifstream sz(path.c_str(), std::ios::ate | std::ios::binary);
-        size_ = sz.is_open() ? (int64_t)sz.tellg() : 0;
-        in_.open(path.c_str());
-    }
-    bool done() const { return done_; }
-    // Fills `chunk` with the next chunk's bytes; returns its size.
-    int64_t next(int64_t cap, std::vector<char>& chunk) {
-        chunk.resize((size_t)(cap > 0 ? cap : 0) + 1);
-        int64_t used = 0;
-        std::string prev, cur;
-        std::getline(in_, prev);
-        std::getline(in_, cur);
-        while (!cur.empty() && used + (int64_t)prev.size() < cap) {
-            if (cur[0] == '+') {
-                memcpy(chunk.data() + used, prev.data(), prev.size());
-                used += (int64_t)prev.size();
-                std::getline(in_, prev);
-                std::getline(in_, cur);
-            } else {
-                prev.swap(cur);
-                std::getline(in_, cur);
-            }
-        }
-        int64_t at = (int64_t)in_.tellg();
-        if (at + L_ > size_ || used == 0) done_ = true;
-        return used;
-    }
-
-  private:
-    std::ifstream in_;
-    int64_t size_ = 0, L_;
-    bool done_ = false;
-};
-
 // outputFormat=dump for k > 32: rewrites the SortedKMerFile in place as word 0
 // + count per record (DumpResults, KMerCounter.cpp:96-103).
 bool to_dump_format(const std::string& path, int W) {
@@ -343,20 +278,6 @@ bool to_dump_format(const std::string& path, int W) {
 void die(kc_ctx* c, kc_status s, const char* what) {
     fprintf(stderr, "kmer-counter: %s: %s%s%s\n", what, kc_strerror(s), c ? ": " : "", c ? kc_last_error(c) : "");
     exit(1);
-}
-
-kc_status count_exact(kc_ctx* c, const InputFile& f, const Options& o) {
-    int64_t cs = chunk_size(f.L, o.kmer_length, o.gpu_memory_limit);
-    ExactChunker ch(f.path, f.L);
-    std::vector<char> buf;
-    while (!ch.done()) {
-        int64_t n = ch.next(cs, buf);
-        if (n > 0 && n >= f.L) {  // KMerCounter.cpp:130
-            kc_status s = kc_count_chunk(c, buf.data(), n, f.L);
-            if (s) return s;
-        }
-    }
-    return KC_OK;
 }
 
 struct GpuWork {
@@ -403,74 +324,30 @@ int main(int argc, char** argv) {
         if (s) die(nullptr, s, "cannot create device context");
     }
 
-    struct Job {
-        const char* p;
-        size_t n;
-        int64_t L;
-    };
-    size_t next_block = 0;
+    // every file through kc_count_file: 256 MiB blocks read ahead into pinned
+    // memory, decoded on the GPU, dealt to the contexts (read-shard, no
+    // collective); auto mode falls back to the reference's chunker for a
+    // file the GPU decoder rejects (KMerCounter.cpp:123-143,
+    // FASTQFileReader.cpp:49-89)
+    std::vector<kc_ctx*> ctxs;
+    for (auto& w : gw) ctxs.push_back(w.ctx);
+    const uint32_t mode = o.input_mode == "exact" ? KC_INPUT_EXACT
+                          : o.input_mode == "fastq" ? KC_INPUT_FASTQ
+                                                    : KC_INPUT_AUTO;
     for (const InputFile& file : files) {
         InputFile f = file;
         if (!o.varlen && f.L < o.kmer_length) continue;
-        bool exact = o.input_mode == "exact" && !o.varlen;
-        Mapped m;
-        if (!exact) {
+        if (o.varlen) {
+            // every read fits a slot of the file's longest sequence line
+            Mapped m;
             if (!m.map(f.path)) die(nullptr, KC_ERR_IO, f.path.c_str());
             if (m.n == 0) continue;
-        }
-        if (o.varlen) {
-            f.L = max_seq_line(m.p, m.n);  // every read fits a slot of the longest one
+            f.L = max_seq_line(m.p, m.n);
             if (f.L < o.kmer_length) continue;
         }
-        std::vector<std::pair<size_t, size_t>> blocks;
-        if (!exact) blocks = fastq_blocks(m.p, m.n, (size_t)1 << 30);
-        if (!exact && o.input_mode == "auto" && blocks.size() > 1 && !o.varlen) {
-            // validate every block before counting anything from the file
-            kc_ctx* c = gw[0].ctx;
-            for (auto& b : blocks) {
-                uint64_t nr = 0;
-                kc_status s = kc_check_fastq(c, m.p + b.first, b.second - b.first, f.L, &nr);
-                if (s == KC_ERR_FORMAT) {
-                    exact = true;
-                    break;
-                }
-                if (s) die(c, s, f.path.c_str());
-            }
-        }
-        if (!exact) {
-            std::vector<std::thread> th;
-            std::vector<kc_status> st(o.gpus, KC_OK);
-            bool fallback = false;
-            const size_t shift = next_block;  // deal blocks round-robin across files too
-            next_block += blocks.size();
-            for (int g = 0; g < o.gpus; g++) {
-                th.emplace_back([&, g, shift]() {
-                    for (size_t i = (g + o.gpus - shift % o.gpus) % o.gpus; i < blocks.size(); i += o.gpus) {
-                        uint64_t nr = 0;
-                        kc_status s = kc_count_fastq(gw[g].ctx, m.p + blocks[i].first,
-                                                       blocks[i].second - blocks[i].first, f.L, &nr);
-                        if (s) {
-                            st[g] = s;
-                            return;
-                        }
-                    }
-                });
-            }
-            for (auto& t : th) t.join();
-            for (int g = 0; g < o.gpus; g++) {
-                if (st[g] == KC_ERR_FORMAT && o.input_mode == "auto" && blocks.size() == 1 && !o.varlen) {
-                    fallback = true;  // a single block validates before counting
-                } else if (st[g]) {
-                    die(gw[g].ctx, st[g], f.path.c_str());
-                }
-            }
-            if (!fallback) continue;
-            exact = true;
-        }
-        if (exact) {
-            kc_status s = count_exact(gw[0].ctx, f, o);
-            if (s) die(gw[0].ctx, s, f.path.c_str());
-        }
+        uint64_t nr = 0;
+        kc_status s = kc_count_file(ctxs.data(), (uint32_t)ctxs.size(), f.path.c_str(), f.L, mode, &nr);
+        if (s) die(ctxs[0], s, f.path.c_str());
     }
 
     // finish every GPU, then write (one GPU) or merge the per-GPU runs

@@ -3,8 +3,22 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace kc {
+
+// Timing ablations (skip a stage; every output after it is invalid) exist only
+// in experiment builds (-DKC_EXPERIMENTS, tools/build_variant.sh). The release
+// library never reads these variables, so a stray one cannot change a count.
+inline int experiment_knob(const char* name) {
+#ifdef KC_EXPERIMENTS
+    const char* e = getenv(name);
+    return e ? atoi(e) : 0;
+#else
+    (void)name;
+    return 0;
+#endif
+}
 
 // Device counters, one uint64 each, in a small device array owned by the ctx.
 enum Stat : int {
@@ -206,7 +220,8 @@ hipError_t launch_fq_count(const uint8_t* base, uint64_t n, uint64_t* counts, hi
 hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t* seq_off,
                           uint64_t* seq_end, uint64_t max_rec, uint64_t* stats, hipStream_t s);
 hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, uint64_t n_rec, int L,
-                              uint64_t* stats, hipStream_t s);
+                              uint64_t* stats, hipStream_t s,
+                              bool at_most = false);
 // K1 emit + E in one pass (after fq_count + scan): codes / inval of every read
 // of the block (groups_per_read(L) each, read r at r * G), the same format
 // checks as fq_emit + fq_validate; seq_off / seq_end are not written.
@@ -216,6 +231,8 @@ hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* lin
 // bases encoded as launch_encode_reads_var does (slot padding, rlen, ST_VHOLE,
 // ST_VWIN); ERR_FQ_LIST when a half holds more records than its list (then
 // index the block with the two-pass path).
+// The fused variable-length index + encode handles reads up to ~4060 bases (else two-pass)
+bool fq_encode_var_ok(int L);
 hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
                                 int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen, uint64_t* stats,
                                 hipStream_t s);
@@ -277,9 +294,10 @@ struct SynthArgs {
     uint64_t first, n, seed, genome, n_threshold;
     int64_t L;
     int64_t Lmin = 0;  // variable read lengths in [Lmin, L] (0: fixed)
+    int layout = 0;    // 1: concatenated sequences (reference chunk layout)
 };
 hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s);
 void synth_host(const SynthArgs& a, char* out);
-uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L);
+uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L, int layout);
 
 }  // namespace kc

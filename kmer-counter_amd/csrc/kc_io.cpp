@@ -219,4 +219,48 @@ bool merge_tree(const std::vector<RunSource>& runs_in, const std::string& out, i
     return ok;
 }
 
+int64_t reference_chunk_size(int64_t L, int64_t k, int64_t limit) {
+    const int64_t kb = (k + 3) / 4;                   // bytes of a k-mer's bases
+    const int64_t rec = ((kb + 7) / 8 + 1) * 8;       // rounded to words, plus one word
+    const int64_t per = rec * (L - k + 1);            // record bytes of one read
+    if (per - 1 == 0) return 0;
+    return L * ((limit - L) / (per - 1));
+}
+
+int64_t file_line2_length(const std::string& path) {
+    std::ifstream s(path.c_str());
+    std::string l1, l2;
+    std::getline(s, l1);
+    std::getline(s, l2);
+    return (int64_t)l2.size();
+}
+
+ExactChunker::ExactChunker(const std::string& path, int64_t L) : L_(L) {
+    std::ifstream sz(path.c_str(), std::ios::ate | std::ios::binary);
+    size_ = sz.is_open() ? (int64_t)sz.tellg() : 0;
+    in_.open(path.c_str());
+}
+
+int64_t ExactChunker::next(int64_t cap, std::vector<char>& chunk) {
+    chunk.resize((size_t)(cap > 0 ? cap : 0) + 1);
+    int64_t used = 0;
+    std::string prev, cur;
+    std::getline(in_, prev);
+    std::getline(in_, cur);
+    while (!cur.empty() && used + (int64_t)prev.size() < cap) {
+        if (cur[0] == '+') {
+            memcpy(chunk.data() + used, prev.data(), prev.size());
+            used += (int64_t)prev.size();
+            std::getline(in_, prev);
+            std::getline(in_, cur);
+        } else {
+            prev.swap(cur);
+            std::getline(in_, cur);
+        }
+    }
+    int64_t at = (int64_t)in_.tellg();
+    if (at + L_ > size_ || used == 0) done_ = true;
+    return used;
+}
+
 }  // namespace kc

@@ -7,6 +7,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <fstream>
 #include <string>
 #include <vector>
 
@@ -76,5 +77,33 @@ bool merge_tree(const std::vector<RunSource>& runs, const std::string& out, int 
                 uint32_t threads, const std::string& tmp_prefix, std::string* err);
 
 int key_compare(const uint8_t* a, const uint8_t* b, int W);
+
+// KMerCounter::GetChunkSize (KMerCounter.cpp:193-212): bytes of sequence per
+// reference chunk for read length L, k and gpuMemoryLimit.
+int64_t reference_chunk_size(int64_t L, int64_t k, int64_t limit);
+
+// Length of line 2 of a file: the read length L the reference takes per file
+// (FASTQFileReader.cpp:31-35). 0 when the file has no second line.
+int64_t file_line2_length(const std::string& path);
+
+// The reference's chunker (FASTQFileReader::readData, FASTQFileReader.cpp:
+// 49-89) driven the way InputFileHandler::read and KMerCounter::Start drive it
+// (InputFileHandler.cpp:82-95, KMerCounter.cpp:123-143): the sequence lines
+// (the line before each '+' line) concatenated without separators while the
+// chunk has room; a record is lost at a chunk edge when its header is >= 2L
+// long, exactly as in the reference. Used for inputMode=exact and as the
+// fallback for input the GPU FASTQ decoder rejects.
+class ExactChunker {
+  public:
+    ExactChunker(const std::string& path, int64_t L);
+    bool done() const { return done_; }
+    // Fills `chunk` with the next chunk's bytes; returns its size.
+    int64_t next(int64_t cap, std::vector<char>& chunk);
+
+  private:
+    std::ifstream in_;
+    int64_t size_ = 0, L_;
+    bool done_ = false;
+};
 
 }  // namespace kc

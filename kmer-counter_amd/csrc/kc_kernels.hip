@@ -1007,10 +1007,7 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa.shift = shift;
     pa.max_win = pg.max_win;
     pa.scap = pg.scap;
-    {
-        const char* e = getenv("KC_P2_SKIP");
-        pa.skip = e ? atoi(e) : 0;
-    }
+    pa.skip = experiment_knob("KC_P2_SKIP");
     size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
     KC_FRONT_SWITCH(SINK_SCATTER, true, kP2Block, grid, lds, s, a, pa)
@@ -2152,10 +2149,7 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
                                 hipStream_t s) {
     BucketArgs a;
-    {
-        const char* e = getenv("KC_P5_SKIP");
-        a.skip = e ? atoi(e) : 0;
-    }
+    a.skip = experiment_knob("KC_P5_SKIP");
     a.desc_key = desc_key;
     a.desc_start = desc_start;
     a.desc_len = desc_len;
@@ -2965,8 +2959,7 @@ hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, 
     if (e != hipSuccess) return e;
     const size_t lds_msd = (seg_sort_msd_lds(W) + 15) & ~(size_t)15;
     const size_t lds = (seg_sort_lds(W) + 15) & ~(size_t)15;
-    const char* se = getenv("KC_SEG_SKIP");  // timing experiments: 1 output stores, 2 insertion sort
-    const int skip = se ? atoi(se) : 0;
+    const int skip = experiment_knob("KC_SEG_SKIP");  // 1 output stores, 2 insertion sort
 #define KC_SEG(WW)                                                                                                  \
     hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds_msd, s, rkeys, rcnts, rstride, order,       \
                        dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, fb, fb_n, skip); \
@@ -3308,10 +3301,12 @@ __global__ __launch_bounds__(kBlock) void fq_emit_k(const uint8_t* __restrict__ 
 
 __global__ __launch_bounds__(kBlock) void fq_validate_k(const u64* __restrict__ seq_off,
                                                         const u64* __restrict__ seq_end, u64 n_rec, int L,
-                                                        u64* stats) {
+                                                        u64* stats, int at_most) {
     bool bad = false;
-    for (u64 r = (u64)blockIdx.x * kBlock + threadIdx.x; r < n_rec; r += (u64)gridDim.x * kBlock)
-        bad |= (seq_end[r] - seq_off[r]) != (u64)L;
+    for (u64 r = (u64)blockIdx.x * kBlock + threadIdx.x; r < n_rec; r += (u64)gridDim.x * kBlock) {
+        const u64 len = seq_end[r] - seq_off[r];
+        bad |= at_most ? len > (u64)L : len != (u64)L;
+    }
     if (__ballot(bad) && lane_id() == 0)
         atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_FQ_SEQ_LEN);
 }
@@ -3698,14 +3693,21 @@ hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* lin
     return hipGetLastError();
 }
 
+// records of >= 32 bytes per half's list; denser halves: ERR_FQ_LIST
+constexpr int kFqVarListCap = kFqHalf / 32 + 2;
+
+bool fq_encode_var_ok(int L) {
+    // (list entry, group) items are split by a FastDivU over lcap * G < 2^16
+    return L >= 1 && L <= 32767 && (u64)kFqVarListCap * (u64)groups_per_read(L) < 65536;
+}
+
 hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
                                 int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen, uint64_t* stats,
                                 hipStream_t s) {
-    if (L < 1 || L > 32767 || k < 1) return hipErrorInvalidValue;
+    if (!fq_encode_var_ok(L) || k < 1) return hipErrorInvalidValue;
     u64 nch = fq_chunks(base, n);
     const int G = groups_per_read(L);
-    const int lcap = kFqHalf / 32 + 2;  // records of >= 32 bytes; denser halves: ERR_FQ_LIST
-    if ((u64)lcap * (u64)G >= 65536) return hipErrorInvalidValue;  // FastDivU range
+    const int lcap = kFqVarListCap;
     const size_t wl = (size_t)kFqStage + (((size_t)lcap * 4 + 15) & ~(size_t)15);
     const size_t lds = (size_t)kFqWaves * wl;
     int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
@@ -3731,9 +3733,10 @@ hipError_t launch_fq_emit(const uint8_t* base, uint64_t n, const uint64_t* line_
 }
 
 hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, uint64_t n_rec, int L,
-                              uint64_t* stats, hipStream_t s) {
+                              uint64_t* stats, hipStream_t s, bool at_most) {
     if (n_rec == 0) return hipSuccess;
-    hipLaunchKernelGGL(fq_validate_k, dim3(grid_for(n_rec)), dim3(kBlock), 0, s, seq_off, seq_end, n_rec, L, stats);
+    hipLaunchKernelGGL(fq_validate_k, dim3(grid_for(n_rec)), dim3(kBlock), 0, s, seq_off, seq_end, n_rec, L, stats,
+                       at_most ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -3744,7 +3747,10 @@ hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, 
 __global__ __launch_bounds__(kBlock) void synth_k(kc_synth_params p, char* out) {
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < p.n; i += (u64)gridDim.x * kBlock) {
         u64 rec = p.first + i;
-        kc_synth_record(p, rec, out + kc_synth_offset(p.first, rec, p.L));
+        if (p.layout == 1)
+            kc_synth_sequence(p, rec, out + i * (u64)p.L);
+        else
+            kc_synth_record(p, rec, out + kc_synth_offset(p.first, rec, p.L));
     }
 }
 
@@ -3757,6 +3763,7 @@ static kc_synth_params to_params(const SynthArgs& a) {
     p.n_threshold = a.n_threshold;
     p.L = a.L;
     p.Lmin = a.Lmin;
+    p.layout = a.layout;
     return p;
 }
 
@@ -3770,11 +3777,16 @@ void synth_host(const SynthArgs& a, char* out) {
     kc_synth_params p = to_params(a);
     for (u64 i = 0; i < a.n; i++) {
         u64 rec = a.first + i;
-        kc_synth_record(p, rec, out + kc_synth_offset(a.first, rec, a.L));
+        if (a.layout == 1)
+            kc_synth_sequence(p, rec, out + i * (u64)a.L);
+        else
+            kc_synth_record(p, rec, out + kc_synth_offset(a.first, rec, a.L));
     }
 }
 
-uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L) { return kc_synth_offset(first, first + n, L); }
+uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L, int layout) {
+    return layout == 1 ? n * (uint64_t)L : kc_synth_offset(first, first + n, L);
+}
 
 // super-k-mer engine (F, rp_*, count_skm): see kc_skm.inl
 #include "kc_skm.inl"

@@ -1393,7 +1393,7 @@ SkmGeom skm_geometry(int L, int k) {
     // than nmax are split, so aim k - m + 1 <= nmax (m in [11, 24])
     int m = k - g.nmax + 1;
     int mmin = 11;
-    if (const char* e = getenv("KC_SKM_MMIN")) mmin = atoi(e);  // tuning experiments
+    if (const int e = experiment_knob("KC_SKM_MMIN")) mmin = e;
     if (m < mmin) m = mmin;
     if (m > 24) m = 24;
     if (k - m + 1 < 8) m = k - 7;
@@ -1444,10 +1444,7 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
     a.hq = g.hq;
     a.chunk = (u64)g.R * (u64)(l.L - l.k + 1);
     if (a.chunk < 1024) a.chunk = 1024;
-    {
-        const char* e = getenv("KC_F_SKIP");
-        a.skip = e ? atoi(e) : 0;
-    }
+    a.skip = experiment_knob("KC_F_SKIP");
     {
         F3Args f3;
         size_t f3lds = 0;
@@ -1465,10 +1462,7 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
             f3.dig1 = dig1;
             f3.stats = l.stats;
             f3.rlen = (const unsigned short*)l.rlen;
-            {
-                const char* e = getenv("KC_F_SKIP");
-                f3.skip = e ? atoi(e) : 0;
-            }
+            f3.skip = experiment_knob("KC_F_SKIP");
             int per_cu = 0, n_cu = 0, dev = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1506,10 +1500,7 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
             f2.pool_cursor = pool_cursor;
             f2.dig1 = dig1;
             f2.stats = l.stats;
-            {
-                const char* e = getenv("KC_F_SKIP");
-                f2.skip = e ? atoi(e) : 0;
-            }
+            f2.skip = experiment_knob("KC_F_SKIP");
             int per_cu = 0, n_cu = 0, dev = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -2489,10 +2480,7 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
     SkmBucketArgs a;
     a.dcnt = dd ? dd->cnt : nullptr;
     a.dlen = dd ? dd->len : nullptr;
-    {
-        const char* e = getenv("KC_P5_SKIP");
-        a.skip = e ? atoi(e) : 0;
-    }
+    a.skip = experiment_knob("KC_P5_SKIP");
     const bool mask_last = ((k + 3) / 4) < 8 * W;
     a.last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
     a.recs = recs;

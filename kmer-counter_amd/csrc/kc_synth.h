@@ -17,6 +17,9 @@
 //       len_i = Lmin + rand(seed, 5, i) mod (L - Lmin + 1) bases (sequence and
 //       quality lines), and its header gains 2 (L - len_i) 'x' bytes, so every
 //       record keeps the fixed-length record's size and offset.
+//   Layout 1 (chunks): only the sequences, read i at (i - first) * L — the
+//       bytes FASTQFileReader::readData concatenates into a reference chunk
+//       (FASTQFileReader.cpp:49-89); fixed read length only.
 #pragma once
 #include <stdint.h>
 
@@ -66,6 +69,7 @@ struct kc_synth_params {
     uint64_t first, n, seed, genome, n_threshold;
     int64_t L;
     int64_t Lmin;  // 0: every read has L bases
+    int layout;    // 0: FASTQ records, 1: concatenated sequences (reference chunk layout)
 };
 
 KC_SYNTH_HD int64_t kc_synth_len(const kc_synth_params& p, uint64_t i) {
@@ -84,6 +88,13 @@ KC_SYNTH_HD char kc_synth_base(const kc_synth_params& p, uint64_t i, int64_t j, 
     }
     if (p.n_threshold && (kc_synth_rand(p.seed, 3, i * (uint64_t)p.L + (uint64_t)j) >> 11) < p.n_threshold) return 'N';
     return "ACGT"[c];
+}
+
+// Writes the L bases of read i at dst (layout 1).
+KC_SYNTH_HD void kc_synth_sequence(const kc_synth_params& p, uint64_t i, char* dst) {
+    uint64_t pos = 0;
+    if (p.genome > 0) pos = kc_synth_rand(p.seed, 1, i) % (p.genome - (uint64_t)p.L + 1);
+    for (int64_t j = 0; j < p.L; j++) dst[j] = kc_synth_base(p, i, j, pos);
 }
 
 // Writes record i at dst (which points at the record's first byte).

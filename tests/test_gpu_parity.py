@@ -274,6 +274,47 @@ def test_config2_full_size_properties(kca):
     assert np.all(recs["c"][idx] >= np.array([cnt[key] for key in cnt], dtype=np.uint32))
 
 
+def _usable_cpus():
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+@pytest.mark.slow
+def test_config2_prefix_bit_exact_through_file_path(kca, orc, tmp_path):
+    """BASELINE config 2's read stream (k=31, 150 bp from the 250 Mbp genome,
+    seed 2), its first 10M reads (1.2e9 k-mers), end to end through the
+    product path: FASTQ file -> kc_count_file -> kc_write_output. The output
+    file's sha256 equals that of the reference-structured CPU pipeline (oracle
+    refcpu: readData chunks at gpuMemoryLimit=1e8, bitEncode / extractKMers /
+    reduceKMers restated, hash aggregation, sorted) run on every usable core."""
+    import hashlib
+
+    n, L, k = 10_000_000, 150, 31
+    fq_path, out = tmp_path / "cfg2_prefix.fq", tmp_path / "out.bin"
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=24 << 30) as ctx:
+        ptr, nb = ctx.synth_device(n, L, 2, 250_000_000, 0.0, 0)
+        host = np.empty(nb, dtype=np.uint8)
+        ctx.copy_to_host_addr(host.ctypes.data, ptr, nb)
+        ctx.free_device(ptr)
+        host.tofile(str(fq_path))
+        assert ctx.count_file(str(fq_path)) == n
+        ctx.write_output(str(out))
+        st = ctx.stats()
+    got = hashlib.sha256(out.read_bytes()).hexdigest()
+    fq = host.tobytes()
+    del host
+    want, windows = orc.refcpu(fq, k, threads=_usable_cpus())
+    assert windows == n * (L - k + 1) == st["windows"]
+    assert st["spilled_kmers"] == 0
+    assert got == hashlib.sha256(want).hexdigest()
+
+
 def _owner_slices(kca, recs, rs, world):
     out = [bytearray() for _ in range(world)]
     for i in range(0, len(recs), rs):

@@ -136,18 +136,19 @@ def test_auto_engine_keeps_skm_on_genome_reads(kca, orc):
 
 
 def test_auto_engine_switch_after_skm_batches(kca, orc):
-    """A small working set: the first batches are below the sample threshold
-    (skm), a later one is sampled and switches; skm and key-prefix records
-    meet in one finish."""
-    L, k = 150, 31
-    blocks = [kca.synth_fastq(25_000, L, seed=79), kca.synth_fastq(175_000, L, seed=79, first_read=25_000)]
-    with kca.Context(kmer_length=k, line_length=L, engine="auto", gpu_memory_limit=3 << 30) as ctx:
+    """The first batch is below the sample threshold (skm), a later one is
+    sampled and switches; skm and key-prefix records meet in one finish. (The
+    blocks differ in read length, so the first is counted as a batch of its
+    own before the second joins the pending batch.)"""
+    k = 31
+    blocks = [kca.synth_fastq(25_000, 140, seed=79), kca.synth_fastq(175_000, 150, seed=79, first_read=25_000)]
+    with kca.Context(kmer_length=k, line_length=150, engine="auto", gpu_memory_limit=3 << 30) as ctx:
         for b in blocks:
-            ctx.count_fastq(b)
+            ctx.count_fastq(b, len(b.split(b"\n")[1]))
         got = ctx.records()
         st = ctx.stats()
     assert st["engines_used"] == 3
-    assert got == orc.count_fastq(b"".join(blocks), k)
+    assert got == orc.count_chunks([(c, ll) for b in blocks for c, ll in orc.chunks_of(b, 1 << 26)], k)
 
 
 def _special_reads(L, n, seed):
@@ -244,17 +245,6 @@ def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
     assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
 
 
-def test_skm_dedup_list_overflow(kca, orc, monkeypatch):
-    """The distinct lists capped below the batch's distinct records
-    (KC_P5A_CAP): the buckets whose list does not fit are walked raw."""
-    monkeypatch.setenv("KC_P5A_CAP", "50000")
-    fq = kca.synth_fastq(60000, 150, seed=34, genome_length=300_000)
-    with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
-        ctx.count_fastq(fq)
-        got = ctx.records()
-    assert got == orc.count_fastq(fq, 31)
-
-
 @pytest.mark.parametrize("k", [21, 31])
 def test_skm_dedup_weighted_spill(kca, orc, tmp_path, k):
     """Deduplicated records with multiplicities > 1 through the last-resort
@@ -268,3 +258,17 @@ def test_skm_dedup_weighted_spill(kca, orc, tmp_path, k):
         st = ctx.stats()
     assert st["spilled_kmers"] > 0
     assert got == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("engine", ["skm", "partition"])
+def test_release_build_ignores_ablation_variables(kca, orc, monkeypatch, engine):
+    """Stray timing-ablation variables (they skip stages in experiment builds)
+    change nothing in the release library: same bytes as the oracle."""
+    for v in ("KC_F_SKIP", "KC_P2_SKIP", "KC_P5_SKIP", "KC_SEG_SKIP"):
+        monkeypatch.setenv(v, "1")
+    monkeypatch.setenv("KC_SKM_MMIN", "14")
+    fq = kca.synth_fastq(20000, 150, seed=77, genome_length=200_000, n_rate=0.001)
+    with kca.Context(kmer_length=31, line_length=150, engine=engine) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    assert got == orc.count_fastq(fq, 31)

@@ -18,8 +18,20 @@ def test_library_exports_header_symbols(kca):
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.kc_abi_version() == 3
+    assert L.kc_abi_version() == 4
     assert L.kc_strerror(4) == b"malformed FASTQ block"
+
+
+EXPERIMENT_KNOBS = ("KC_F_SKIP", "KC_P2_SKIP", "KC_P5_SKIP", "KC_SEG_SKIP", "KC_SKM_MMIN")
+
+
+def test_release_library_ignores_timing_ablations(kca):
+    """The stage-skipping timing knobs (outputs invalid after the skipped
+    stage) exist only in experiment builds (-DKC_EXPERIMENTS,
+    tools/build_variant.sh): the release library does not even hold their
+    names, so no environment variable can change what it counts."""
+    blob = open(kca.LIB_PATH, "rb").read()
+    assert [k for k in EXPERIMENT_KNOBS if k.encode() in blob] == []
 
 
 def test_no_device_is_an_error_not_a_fallback(kca):
@@ -188,6 +200,21 @@ def test_cli_options_surface(kca, tmp_path):
                         f"Updating Input File Location='{tmp_path}'", "Updating Temp File Location='/tmp/x'",
                         f"Updating Output File='{tmp_path}/o.bin'", "Updating No Of Mergers At Once='3'",
                         "Updating No Of Merge Threads='4'", "Updating KmerLength=25"]
+
+
+@pytest.mark.parametrize("arg", ["readLengths=varaible", "outputFormat=dmup", "inputMode=fast", "exchange=all"])
+def test_cli_rejects_unknown_mode_values(kca, tmp_path, arg):
+    """Additive keys take only their listed values: a typo is an error, not a
+    silent switch to another mode (parsing runs before any device is opened)."""
+    r = subprocess.run([kca.CLI_PATH, "kmerLength=21", f"inputFileLocation={tmp_path}", arg],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "expected" in r.stderr
+
+
+def test_cli_rejects_variable_lengths_in_exact_mode(kca, tmp_path):
+    r = subprocess.run([kca.CLI_PATH, "kmerLength=21", "readLengths=variable", "inputMode=exact"],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "inputMode=exact" in r.stderr
 
 
 def test_python_options_mirror_reference_defaults(kca, orc):

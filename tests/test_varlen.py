@@ -90,6 +90,18 @@ def test_varlen_gpu_matches_oracle(kca, orc, k, lmin, lmax, engine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,lmin,lmax", [(31, 3000, 5000), (55, 4000, 6000)])
+def test_varlen_gpu_reads_past_fused_index_limit(kca, orc, k, lmin, lmax):
+    """Reads of > 4065 bases exceed the fused variable-length index's item
+    range (list cap x 16-base groups < 2^16): those blocks take the two-pass
+    index (fq_emit + encode_reads_var) instead of failing."""
+    fq = _varlen_fastq(300, lmin, lmax, seed=k + lmax, n_rate=0.001)
+    n, got, st = _gpu(kca, fq, k, lmax, engine="partition")
+    assert n == 300
+    assert got == orc.count_fastq_varlen(fq, k)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [21, 31])
 def test_varlen_gpu_genome_reads_skm(kca, orc, k):
     # coverage (the super-k-mer engine's dedup path), trimmed reads
