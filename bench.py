@@ -26,8 +26,8 @@ N GPUs (one process per GPU, torch.distributed; RCCL = backend nccl): rank r
 counts reads [r R, (r+1) R) from its own input file (weak scaling).
   --exchange alltoall (default at N > 1): the sorted runs are
     exchanged by key-space owner (RCCL all-to-all) and merged on the device;
-    every rank writes its owned records at its offset of the one output file,
-    which is then the node's SortedKMerFile (concatenation, no merge).
+    every rank writes its owned key range as its own part file; the parts in
+    rank order are the node's SortedKMerFile (concatenation, no merge).
   --exchange none (cfg3, read-shard): the runs are gathered to rank 0's GPU
     (RCCL) and merged there (device merge path), rank 0 writes the file.
 
@@ -214,20 +214,22 @@ def gather_runs_to_rank0(kca, ctx, D):
 
 def write_node_output(kca, ctx, D, path, exchange):
     """The node's SortedKMerFile from the ranks' finished runs (see the module
-    docstring). Returns output bytes written by this rank."""
+    docstring). Returns output bytes written by this rank.
+
+    N > 1, key-space exchange: rank r owns the r-th key range after the
+    exchange and writes it as its own part file `path.part<r>`; the parts in
+    rank order are the node's SortedKMerFile (the final merge is a
+    concatenation). One file per rank because buffered writes into one file
+    are serialised by its inode (~10 GB/s on the GPU box), separate files are
+    not. N > 1, read-shard: rank 0 merges every rank's run on its GPU and
+    writes the one file."""
     if D.world == 1:
         ctx.write_output(path)
         return ctx.finish() * ctx.rs
     if exchange == "alltoall":
         n = kca.keyspace_exchange(ctx, D.dist, D.xdev())
-        sizes = D.all_gather_int(n * ctx.rs)
-        off = sum(sizes[:D.rank])
-        if D.rank == 0:
-            with open(path, "wb") as f:
-                f.truncate(sum(sizes))
-        D.dist.barrier()
-        ctx.write_output_at(path, off)
-        return sizes[D.rank]
+        ctx.write_output(f"{path}.part{D.rank}")
+        return n * ctx.rs
     n = gather_runs_to_rank0(kca, ctx, D)
     if D.rank == 0:
         ctx.write_output(path)
@@ -283,8 +285,7 @@ def main():
     # ---- input file (untimed): the same bytes, in the page cache ---------------
     workdir = args.workdir or os.environ.get("TMPDIR") or "/tmp"
     in_path = os.path.join(workdir, f"kc_bench_in.{os.getpid()}.fq")
-    out_path = os.path.join(workdir, f"kc_bench_out.{D.rank if exchange == 'none' else 'node'}."
-                                     f"{os.getpid() if D.world == 1 else 'x'}.bin")
+    out_path = os.path.join(workdir, f"kc_bench_out.{os.getpid() if D.world == 1 else 'node'}.bin")
     host = np.empty(nbytes, dtype=np.uint8)
     ctx.copy_to_host_addr(host.ctypes.data, ptr, nbytes)
     host.tofile(in_path)
@@ -409,8 +410,8 @@ def main():
         workload, parallelism = f"{cfg_tag}: {base}; {path_desc}", "single GPU"
     elif exchange == "alltoall":
         workload = (f"cfg4 pattern at {D.world} GPUs: {base}; {path_desc}; key-space all-to-all of the sorted "
-                    f"(key, count) records + per-GPU merge, each rank writes its key range at its offset of the "
-                    f"one output file")
+                    f"(key, count) records + per-GPU merge, each rank writes its key range as a part file "
+                    f"(rank-order concatenation = the SortedKMerFile)")
         parallelism = f"read-shard count + key-space all-to-all x{D.world}"
     else:
         workload = (f"cfg3 pattern at {D.world} GPUs: {base}; {path_desc}; runs gathered to rank 0's GPU "
@@ -448,9 +449,9 @@ def main():
             "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"], "spill_runs": st["spill_runs"],
         }
         print(json.dumps(line), flush=True)
-    for p in (in_path, out_path):
+    for p in (in_path, out_path, f"{out_path}.part{D.rank}"):
         try:
-            if D.rank == 0 or p == in_path:
+            if D.rank == 0 or p != out_path:
                 os.unlink(p)
         except OSError:
             pass

@@ -120,6 +120,13 @@ struct kc_ctx {
     uint64_t ckpt_reads = 0, ckpt_flushes = 0, ckpt_st_reads = 0, ckpt_st_windows = 0;
     uint64_t ckpt_stats[ST_N];
 
+    // Sorted runs cut from the records when they outgrow half the working set
+    // (cut_run): kept in HBM outside the counting working set (host memory
+    // only when HBM is short, as c->runs), merged on the device by kc_finish
+    std::vector<DevBuf> dev_runs;
+    std::vector<uint64_t> dev_run_n;
+    uint64_t runs_cut = 0;
+
     // results
     bool finished = false;
     uint64_t n_records = 0;  // table run
@@ -129,6 +136,10 @@ struct kc_ctx {
     kc_stats st;
     std::string err;
 };
+
+static kc_status cut_run(kc_ctx* c);
+static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
+static void release_dev_runs(kc_ctx* c);
 
 static kc_status fail(kc_ctx* c, kc_status s, const char* fmt, ...) {
     if (c) {
@@ -920,18 +931,23 @@ static kc_status grow_keep(kc_ctx* c, DevBuf& b, size_t bytes, size_t keep) {
     return KC_OK;
 }
 
+static kc_status cut_run_if_full(kc_ctx* c);
+
 // Counts the pending batch (the engines: count_reads with pre-encoded reads).
 static kc_status pend_flush(kc_ctx* c) {
     if (c->pend_reads == 0) return KC_OK;
     const uint64_t n = c->pend_reads;
     c->pend_reads = 0;  // a failed count is not counted again
     c->flushes++;
-    if (!c->pend_var) return count_reads(c, nullptr, nullptr, n, c->pend_L, 0);
+    kc_status s;
+    if (!c->pend_var) {
+        if ((s = count_reads(c, nullptr, nullptr, n, c->pend_L, 0))) return s;
+        return cut_run_if_full(c);
+    }
     // variable-length reads: the slot padding's invalid windows are no holes;
     // key 0^W is present iff a read of >= k bases holds a not-ACGT base
     // (ST_VHOLE, written by the encoders) or a key-0 window was counted
-    kc_status s = sync_stats(c);
-    if (s) return s;
+    if ((s = sync_stats(c))) return s;
     const uint64_t present0 = c->stats_h[ST_KEY0_PRESENT];
     c->var_rlen = (const uint16_t*)c->part_rlen.p;
     s = count_reads(c, nullptr, nullptr, n, c->pend_L, 0);
@@ -943,7 +959,7 @@ static kc_status pend_flush(kc_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(c->stats + ST_KEY0_PRESENT, &c->stats_h[ST_KEY0_PRESENT], 8, hipMemcpyHostToDevice,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return KC_OK;
+    return cut_run_if_full(c);
 }
 
 // Room for n_new more pending reads of length L (fixed or variable): the
@@ -1248,6 +1264,7 @@ void kc_destroy(kc_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     delete c->ring;  // waits for its DMAs
     delete c->pool;
+    release_dev_runs(c);
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     DevBuf* bufs[] = {&c->in_stage, &c->fq_counts, &c->fq_base, &c->fq_tmp, &c->seq_off, &c->seq_end,
@@ -1314,6 +1331,8 @@ kc_status kc_reset(kc_ctx* c) {
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
     c->spilled_flushed = 0;
+    release_dev_runs(c);
+    c->runs_cut = 0;
     c->pend_reads = 0;
     c->pend_L = 0;
     c->pend_var = false;
@@ -1872,6 +1891,18 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     if ((s = pend_flush(c))) return s;
     if ((s = sync_stats(c))) return s;
     if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;
+    if (!c->dev_runs.empty()) {
+        // the rest of the records as the last run, then one merge of all runs
+        if ((s = cut_run(c))) return s;
+        std::vector<std::pair<const void*, uint64_t>> runs;
+        for (size_t r = 0; r < c->dev_runs.size(); r++) runs.push_back({c->dev_runs[r].p, c->dev_run_n[r]});
+        s = merge_runs_list(c, runs);
+        release_dev_runs(c);
+        if (s) return s;
+        c->st.table_used = 0;
+        if (n_records) *n_records = c->n_records;
+        return KC_OK;
+    }
     const int W = c->W;
     uint64_t out_cap = c->stats_h[ST_CLAIMED] + 1;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -2081,7 +2112,7 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     out->p5_launches = c->p5_launches;
     out->table_capacity = c->cap;
     out->valid_kmers = c->stats_h[ST_VALID];
-    out->spill_runs = c->runs.size();
+    out->spill_runs = c->runs_cut + c->runs.size();
     out->engines_used = c->engines_used;
     out->dedup_ms = c->dedup_ms;
     out->dedup_records = c->stats_h[ST_DEDUP];
@@ -2197,14 +2228,18 @@ kc_status kc_merge_records_device(kc_ctx* c, const void* d_packed, uint64_t n_re
     return KC_OK;
 }
 
-kc_status kc_merge_runs_device(kc_ctx* c, const void* d_packed, const uint64_t* run_counts, uint32_t nruns) {
-    if (!c || (nruns && !run_counts)) return KC_ERR_ARG;
-    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
-    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist");
+}  // extern "C"
+
+// Merges sorted packed runs (each a device pointer + record count; equal keys
+// within and across runs allowed) into the ctx's finished table run:
+// unpacked side by side into SoA keys, merged pairwise by merge path
+// (adjacent runs merge into the same range of the other buffer), equal keys
+// summed (u32, wrapping), packed into fin_packed.
+static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs) {
+    const uint32_t nruns = (uint32_t)runs.size();
     std::vector<uint64_t> off(nruns + 1, 0);
-    for (uint32_t r = 0; r < nruns; r++) off[r + 1] = off[r] + run_counts[r];
+    for (uint32_t r = 0; r < nruns; r++) off[r + 1] = off[r] + runs[r].second;
     const uint64_t n = off[nruns];
-    if (n && !d_packed) return KC_ERR_ARG;
     kc_status s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
     const uint64_t out_cap = n + 1;
@@ -2215,10 +2250,10 @@ kc_status kc_merge_runs_device(kc_ctx* c, const void* d_packed, const uint64_t* 
     }
     if ((s = ensure(c, c->fin_misc, merge_split_elems(n) * 8 + 64))) return s;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_unpack(W, d_packed, n, (uint64_t*)c->fin_keys[0].p, out_cap, (uint32_t*)c->fin_cnts[0].p,
-                            c->stream));
-    // pairwise merge levels: runs 2i and 2i+1 are adjacent, so their merge
-    // occupies the same range of the other buffer
+    for (uint32_t r = 0; r < nruns; r++)
+        if (runs[r].second)
+            HIPCHK(c, launch_unpack(W, runs[r].first, runs[r].second, (uint64_t*)c->fin_keys[0].p + off[r], out_cap,
+                                    (uint32_t*)c->fin_cnts[0].p + off[r], c->stream));
     int which = 0;
     std::vector<uint64_t> ro = off;
     while (ro.size() > 2) {
@@ -2258,6 +2293,82 @@ kc_status kc_merge_runs_device(kc_ctx* c, const void* d_packed, const uint64_t* 
     c->st.output_records = nout;
     c->finished = true;
     return KC_OK;
+}
+
+// The records counted so far become a sorted run — the reference's sorted
+// spill (sortKmers + reduceKMers + FileDump::dumpKmersToFile,
+// GPUHandler.cu:456-468, FileDump.cpp:51-58): finished into packed
+// SortedKMerFile records (finish_part), kept in HBM outside the counting
+// working set (host memory, as a spill run, when HBM is short), and the
+// record state starts empty. kc_finish merges the runs on the device.
+static kc_status cut_run(kc_ctx* c) {
+    kc_status s;
+    if ((s = sync_stats(c))) return s;
+    uint64_t n = 0;
+    if ((s = finish_part(c, &n))) return s;  // fin_packed
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t bytes = (size_t)n * c->rs;
+    if (n) {
+        size_t mfree = 0, mtotal = 0;
+        DevBuf run;
+        if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > bytes + ((size_t)4 << 30) &&
+            hipMalloc(&run.p, bytes) == hipSuccess) {
+            run.bytes = bytes;
+            HIPCHK(c, hipMemcpyAsync(run.p, c->fin_packed.p, bytes, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->dev_runs.push_back(run);
+            c->dev_run_n.push_back(n);
+            c->runs_cut++;
+        } else {
+            (void)hipGetLastError();
+            HostRun hr;
+            hr.records = n;
+            hr.mem.resize(bytes);
+            HIPCHK(c, hipMemcpyAsync(hr.mem.data(), c->fin_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->runs.push_back(std::move(hr));
+        }
+    }
+    // empty record state: records, batch count, table claims, key 0, descriptors
+    c->rec_n = 0;
+    c->batches = 0;
+    c->skm_used = false;
+    HIPCHK(c, hipMemsetAsync(c->rec_cursor, 0, 8, c->stream));
+    if (c->stats_h[ST_CLAIMED]) HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
+    for (int st : {(int)ST_CLAIMED, (int)ST_KEY0, (int)ST_KEY0_PRESENT, (int)ST_DESC_FILL}) c->stats_h[st] = 0;
+    HIPCHK(c, hipMemcpyAsync(c->stats, c->stats_h, ST_N * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KC_OK;
+}
+
+// A run is cut when the records outgrow half the working set (the reference's
+// "table capacity < distinct" case, SURVEY §8d cfg 5).
+static kc_status cut_run_if_full(kc_ctx* c) {
+    const uint64_t M = c->cfg.gpu_memory_limit ? c->cfg.gpu_memory_limit : 100000000ull;
+    if (!c->part || c->rec_n * (uint64_t)c->rs <= M / 2) return KC_OK;
+    return cut_run(c);
+}
+
+static void release_dev_runs(kc_ctx* c) {
+    for (auto& r : c->dev_runs) release(r);
+    c->dev_runs.clear();
+    c->dev_run_n.clear();
+}
+
+extern "C" {
+
+kc_status kc_merge_runs_device(kc_ctx* c, const void* d_packed, const uint64_t* run_counts, uint32_t nruns) {
+    if (!c || (nruns && !run_counts)) return KC_ERR_ARG;
+    if (!c->finished) return fail(c, KC_ERR_STATE, "call kc_finish first");
+    if (!c->runs.empty()) return fail(c, KC_ERR_STATE, "spill runs exist");
+    std::vector<std::pair<const void*, uint64_t>> runs;
+    uint64_t off = 0;
+    for (uint32_t r = 0; r < nruns; r++) {
+        runs.push_back({(const uint8_t*)d_packed + off * c->rs, run_counts[r]});
+        off += run_counts[r];
+    }
+    if (off && !d_packed) return KC_ERR_ARG;
+    return merge_runs_list(c, runs);
 }
 
 kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n) {

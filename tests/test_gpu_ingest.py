@@ -233,3 +233,26 @@ def test_cli_streams_files_end_to_end(kca, orc, tmp_path):
     lim = 100000000
     chunks = [(c, ll) for t in texts + [bad] for c, ll in orc.chunks_of(t, orc.chunk_size(120, 27, lim))]
     assert out.read_bytes() == orc.count_chunks(chunks, 27)
+
+
+def test_write_output_at_offsets_after_exchange(kca, orc, tmp_path):
+    """kc_write_output_at: after the in-process key-space exchange every
+    context writes its key range at its offset of one pre-sized file; the file
+    is the whole count."""
+    shards = [kca.synth_fastq(2500, 150, 31 + r, n_rate=0.001, genome_length=80_000) for r in range(3)]
+    ctxs = [kca.Context(kmer_length=31, line_length=150) for _ in shards]
+    out = tmp_path / "o.bin"
+    try:
+        for c, fq in zip(ctxs, shards):
+            c.count_fastq(fq)
+            c.finish()
+        kca.exchange_contexts(ctxs)
+        sizes = [c.finish() * c.rs for c in ctxs]
+        with open(out, "wb") as f:
+            f.truncate(sum(sizes))
+        for i in (2, 0, 1):
+            ctxs[i].write_output_at(str(out), sum(sizes[:i]))
+    finally:
+        for c in ctxs:
+            c.close()
+    assert out.read_bytes() == orc.count_fastq(b"".join(shards), 31)
