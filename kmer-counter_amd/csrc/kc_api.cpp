@@ -68,6 +68,8 @@ struct kc_ctx {
     bool skm_checked = false;      // the skm cardinality sample has run since the last reset
     uint32_t engines_used = 0;     // kc_stats.engines_used
     bool skm_hc = false;           // high cardinality seen: the key-prefix engine counts
+    bool hc_hint = false;          // most keys were distinct (the skm sample or the last key-prefix batch):
+                                   // P5 splits buckets by their key count up front
     uint64_t* pool_cursor = nullptr;  // device u64: skm pool allocator
     uint64_t key_cap = 0;          // keys per batch
     uint64_t* keys_a = nullptr;    // W x key_cap
@@ -100,6 +102,7 @@ struct kc_ctx {
     DevBuf fq_counts, fq_base, fq_tmp, seq_off, seq_end;
     DevBuf spill_keys2, rle_flags, rle_pos, rle_head, rle_tmp, run_keys, run_cnts, run_packed;
     DevBuf fin_keys[2], fin_cnts[2], fin_hist, fin_packed, fin_misc;
+    DevBuf merge_tmp;  // packed run merge: the other ping-pong buffer
 
     // host staging (kc_stage.h), created on the first host-pointer input or output
     kc::Pool* pool = nullptr;
@@ -126,6 +129,7 @@ struct kc_ctx {
     std::vector<DevBuf> dev_runs;
     std::vector<uint64_t> dev_run_n;
     uint64_t runs_cut = 0;
+    uint64_t batches_cut = 0;  // batches of the records already cut into runs
 
     // results
     bool finished = false;
@@ -139,6 +143,7 @@ struct kc_ctx {
 
 static kc_status cut_run(kc_ctx* c);
 static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
+static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
 static void release_dev_runs(kc_ctx* c);
 
 static kc_status fail(kc_ctx* c, kc_status s, const char* fmt, ...) {
@@ -544,7 +549,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                                                c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
                                                c->keys_a, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
                                                c->n_cu, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,
-                                               (uint32_t*)c->desc_len.p, kDescCap, c->stream));
+                                               (uint32_t*)c->desc_len.p, kDescCap, c->stream, c->hc_hint));
                 HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                 HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
                 if ((s = sync_stats(c))) return s;
@@ -569,6 +574,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 c->stats_h[ST_ERR] = err;
                 c->rec_n = rec0;
             }
+            // the next batch's P5 starts from this one's cardinality
+            c->hc_hint = (c->rec_n - rec0) * 2 > n;
             if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
             uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
             if (n2) {
@@ -844,6 +851,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                     memcpy(c->stats_h, saved.data(), ST_N * 8);
                     c->rec_n = rec_batch0;
                     c->skm_hc = true;
+                    c->hc_hint = true;
                     if (getenv("KC_DEBUG"))
                         fprintf(stderr, "kc: skm sample %llu distinct / %llu keys: key-prefix engine\n",
                                 (unsigned long long)dist_s, (unsigned long long)keys_s);
@@ -936,6 +944,7 @@ static kc_status cut_run_if_full(kc_ctx* c);
 // Counts the pending batch (the engines: count_reads with pre-encoded reads).
 static kc_status pend_flush(kc_ctx* c) {
     if (c->pend_reads == 0) return KC_OK;
+    kc::trace("flush %llu reads of length %lld", (unsigned long long)c->pend_reads, (long long)c->pend_L);
     const uint64_t n = c->pend_reads;
     c->pend_reads = 0;  // a failed count is not counted again
     c->flushes++;
@@ -1270,7 +1279,7 @@ void kc_destroy(kc_ctx* c) {
     DevBuf* bufs[] = {&c->in_stage, &c->fq_counts, &c->fq_base, &c->fq_tmp, &c->seq_off, &c->seq_end,
                       &c->spill_keys2, &c->rle_flags, &c->rle_pos, &c->rle_head, &c->rle_tmp, &c->run_keys,
                       &c->run_cnts, &c->run_packed, &c->fin_keys[0], &c->fin_keys[1], &c->fin_cnts[0],
-                      &c->fin_cnts[1], &c->fin_hist, &c->fin_packed, &c->fin_misc};
+                      &c->fin_cnts[1], &c->fin_hist, &c->fin_packed, &c->fin_misc, &c->merge_tmp};
     for (DevBuf* b : bufs) release(*b);
     if (c->table) (void)hipFree(c->table);
     if (c->spill) (void)hipFree(c->spill);
@@ -1326,6 +1335,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->skm_used = false;
     c->skm_checked = false;
     c->skm_hc = false;
+    c->hc_hint = false;
     c->engines_used = 0;
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
@@ -1333,6 +1343,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->spilled_flushed = 0;
     release_dev_runs(c);
     c->runs_cut = 0;
+    c->batches_cut = 0;
     c->pend_reads = 0;
     c->pend_L = 0;
     c->pend_var = false;
@@ -1489,7 +1500,10 @@ static kc_status file_blocks(kc_ctx* const* ctxs, uint32_t n_ctx, const char* pa
         kc::FastqFileReader::Block b;
         while (!stop && rd.next(&b)) {
             uint64_t got = 0;
+            const double t0 = kc::trace_on() ? kc::now_s() : 0;
             kc_status s = file_block(c, b.p, b.n, L, count, &got);
+            if (kc::trace_on()) kc::trace("ctx %u block %llu: %zu bytes, upload + decode %.3f ms", g,
+                                          (unsigned long long)b.index, b.n, (kc::now_s() - t0) * 1e3);
             rd.release(b);
             if (s) {
                 st[g] = s;
@@ -1896,7 +1910,7 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
         if ((s = cut_run(c))) return s;
         std::vector<std::pair<const void*, uint64_t>> runs;
         for (size_t r = 0; r < c->dev_runs.size(); r++) runs.push_back({c->dev_runs[r].p, c->dev_run_n[r]});
-        s = merge_runs_list(c, runs);
+        s = merge_runs_packed(c, runs);
         release_dev_runs(c);
         if (s) return s;
         c->st.table_used = 0;
@@ -2002,7 +2016,9 @@ static kc_status table_run_to_host(kc_ctx* c, std::vector<uint8_t>* mem) {
 // previous slot.
 static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0, bool truncate = true) {
     const uint64_t bytes = c->n_records * c->rs;
+    const double t0 = kc::trace_on() ? kc::now_s() : 0;
     int fd = open(path, O_CREAT | O_WRONLY | (truncate ? O_TRUNC : 0), 0644);
+    if (kc::trace_on()) kc::trace("output open%s %.3f ms", truncate ? " (truncate)" : "", (kc::now_s() - t0) * 1e3);
     if (fd < 0) return fail(c, KC_ERR_IO, "cannot open output file %s", path);
     kc_status s = KC_OK;
     if (bytes) {
@@ -2024,6 +2040,7 @@ static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0,
         else if (e != hipSuccess) s = fail(c, KC_ERR_HIP, "output copy: %s", hipGetErrorString(e));
     }
     if (close(fd) != 0 && !s) s = fail(c, KC_ERR_IO, "cannot close %s", path);
+    if (kc::trace_on()) kc::trace("output %llu bytes in %.3f ms", (unsigned long long)bytes, (kc::now_s() - t0) * 1e3);
     return s;
 }
 
@@ -2107,7 +2124,7 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     if (!c || !out) return KC_ERR_ARG;
     *out = c->st;
     for (int i = 0; i < 5; i++) out->part_ms[i] = c->part_ms[i];
-    out->batches = c->batches;
+    out->batches = c->batches_cut + c->batches;
     out->keys = c->part_keys;
     out->p5_launches = c->p5_launches;
     out->table_capacity = c->cap;
@@ -2295,6 +2312,84 @@ static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const vo
     return KC_OK;
 }
 
+// Sorted runs without repeated keys (kc_finish output, cut runs, slices of
+// them) -> the finished table run: pairwise merge path over the packed
+// records, level by level (launch_merge_packed), into ping-pong buffers; keys
+// present in several runs come out as adjacent records and are summed after
+// the last level (SoA segmented reduce). One run is taken as it is.
+static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs0) {
+    kc_status s;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    std::vector<std::pair<const void*, uint64_t>> runs;
+    uint64_t n = 0;
+    for (auto& r : runs0)
+        if (r.second) {
+            runs.push_back(r);
+            n += r.second;
+        }
+    const size_t rs = (size_t)c->rs;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if ((s = ensure(c, c->fin_misc, (merge_packed_split_elems(c->W, n) + 8) * 8))) return s;
+    uint32_t* dup = (uint32_t*)((uint64_t*)c->fin_misc.p + merge_packed_split_elems(c->W, n) + 2);
+    uint64_t* split = (uint64_t*)c->fin_misc.p;
+    HIPCHK(c, hipMemsetAsync(dup, 0, 4, c->stream));
+    if (runs.size() <= 1) {
+        if ((s = ensure(c, c->fin_packed, n * rs + 16))) return s;
+        if (n && runs[0].first != c->fin_packed.p)
+            HIPCHK(c, hipMemcpyAsync(c->fin_packed.p, runs[0].first, n * rs, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+        DevBuf* out[2] = {&c->fin_packed, &c->merge_tmp};
+        int lvl = 0;
+        while (runs.size() > 1) {
+            DevBuf* o = out[lvl & 1];
+            if ((s = ensure(c, *o, n * rs + 16))) return s;
+            std::vector<std::pair<const void*, uint64_t>> next;
+            uint64_t off = 0;
+            for (size_t r = 0; r < runs.size(); r += 2) {
+                uint8_t* dst = (uint8_t*)o->p + off * rs;
+                if (r + 1 < runs.size()) {
+                    HIPCHK(c, launch_merge_packed(c->W, runs[r].first, runs[r].second, runs[r + 1].first,
+                                                  runs[r + 1].second, dst, split, dup, c->stream));
+                    next.push_back({dst, runs[r].second + runs[r + 1].second});
+                } else {
+                    HIPCHK(c, hipMemcpyAsync(dst, runs[r].first, runs[r].second * rs, hipMemcpyDeviceToDevice,
+                                             c->stream));
+                    next.push_back({dst, runs[r].second});
+                }
+                off += next.back().second;
+            }
+            runs.swap(next);
+            lvl++;
+        }
+        if (runs[0].first != c->fin_packed.p) std::swap(c->fin_packed, c->merge_tmp);
+    }
+    uint32_t dup_h = 0;
+    HIPCHK(c, hipMemcpyAsync(&dup_h, dup, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t nout = n;
+    if (dup_h) {
+        // keys of several runs: sum them (unpack, segmented reduce, pack)
+        const uint64_t out_cap = n + 1;
+        const int W = c->W;
+        for (int i = 0; i < 2; i++)
+            if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) ||
+                (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
+                return s;
+        HIPCHK(c, launch_unpack(W, c->fin_packed.p, n, (uint64_t*)c->fin_keys[0].p, out_cap,
+                                (uint32_t*)c->fin_cnts[0].p, c->stream));
+        if ((s = reduce_pack(c, out_cap, n, 0, true, &nout))) return s;
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    c->st.finish_ms += t;
+    c->n_records = nout;
+    c->st.output_records = nout;
+    c->finished = true;
+    return KC_OK;
+}
+
 // The records counted so far become a sorted run — the reference's sorted
 // spill (sortKmers + reduceKMers + FileDump::dumpKmersToFile,
 // GPUHandler.cu:456-468, FileDump.cpp:51-58): finished into packed
@@ -2331,6 +2426,7 @@ static kc_status cut_run(kc_ctx* c) {
     }
     // empty record state: records, batch count, table claims, key 0, descriptors
     c->rec_n = 0;
+    c->batches_cut += c->batches;
     c->batches = 0;
     c->skm_used = false;
     HIPCHK(c, hipMemsetAsync(c->rec_cursor, 0, 8, c->stream));
@@ -2368,6 +2464,9 @@ kc_status kc_merge_runs_device(kc_ctx* c, const void* d_packed, const uint64_t* 
         off += run_counts[r];
     }
     if (off && !d_packed) return KC_ERR_ARG;
+    // one run may repeat keys (the SoA path sums them); two or more runs come
+    // from finished runs: merged packed, repeated keys summed after the merge
+    if (nruns >= 2) return merge_runs_packed(c, runs);
     return merge_runs_list(c, runs);
 }
 

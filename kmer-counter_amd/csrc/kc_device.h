@@ -143,7 +143,7 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
-                                hipStream_t s);
+                                hipStream_t s, bool distinct = false);
 // Finish without a global sort (see kc_kernels.hip): lens_sorted[i] = len[order[i]];
 // seg_sort writes each descriptor's records sorted at out_off[i].
 hipError_t launch_desc_prep(const uint32_t* order, const uint32_t* len, uint64_t n, uint64_t* lens_sorted,
@@ -211,6 +211,12 @@ hipError_t launch_merge(int W, const uint64_t* ka, const uint32_t* ca, uint64_t 
                         const uint32_t* cb, uint64_t sb, uint64_t nb, uint64_t* ko, uint32_t* co, uint64_t so,
                         uint64_t* split, hipStream_t s);
 uint64_t merge_split_elems(uint64_t n);
+// Merge path over two sorted, deduplicated packed runs (SortedKMerFile
+// records) into `out` (packed, sorted; a key of both runs leaves two adjacent
+// records and sets *dup). split: merge_packed_split_elems(W, na + nb) u64.
+hipError_t launch_merge_packed(int W, const void* a, uint64_t na, const void* b, uint64_t nb, void* out,
+                               uint64_t* split, uint32_t* dup, hipStream_t s);
+uint64_t merge_packed_split_elems(int W, uint64_t n);
 hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, uint64_t stride, uint32_t* cnts,
                          hipStream_t s);
 

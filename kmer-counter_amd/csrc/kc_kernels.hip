@@ -1742,6 +1742,8 @@ struct BucketArgs {
     u32* desc_len;    //   records
     u64 desc_cap;
     int skip;         // timing experiments only (KC_P5_SKIP): 1 = no LDS inserts
+    int distinct;     // input where most keys are distinct (high cardinality): a bucket's
+                      // first split m is taken from its key count (no aborted first pass)
 };
 
 // 48-bit slot fraction of a key for the P5 LDS table: multiply-shift (the
@@ -1902,6 +1904,12 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         if (stop) return;
         const u64 lo = a.starts[b], hi = a.starts[b + 1];
         u32 m = 1, sub = 0;
+        if (a.distinct) {
+            // every key may be distinct: enough passes that each fills the
+            // table to at most 7/8 of its abort limit
+            const u64 per = (u64)limit * 7 / 8;
+            while (m < mmax && (u64)m * per < hi - lo) m *= 2;
+        }
         while (sub < m) {
             const bool last = m >= mmax;
             u64 scanned = 0;
@@ -2147,9 +2155,10 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
-                                hipStream_t s) {
+                                hipStream_t s, bool distinct) {
     BucketArgs a;
     a.skip = experiment_knob("KC_P5_SKIP");
+    a.distinct = distinct ? 1 : 0;
     a.desc_key = desc_key;
     a.desc_start = desc_start;
     a.desc_len = desc_len;
@@ -3143,6 +3152,160 @@ hipError_t launch_merge(int W, const uint64_t* ka, const uint32_t* ca, uint64_t 
 }
 
 uint64_t merge_split_elems(uint64_t n) { return n / 1024 + 2; }
+
+// ---------------------------------------------------------------------------
+// Merge path over packed runs (SortedKMerFile records: W LE u64 key words +
+// LE u32 count, RW = 2W + 1 u32 per record), without unpacking: two sorted,
+// deduplicated runs A, B -> one sorted packed run (A first on equal keys). A
+// key present in both runs leaves two adjacent records; *dup is then set and
+// the caller sums them. Tiles of TILE outputs: merge_split_packed_k finds each
+// tile's split by a binary search on the cross diagonal; merge_tile_packed_k
+// stages the tile's A and B slices in LDS (coalesced u32 copies), every
+// thread merges ITEMS consecutive outputs into an LDS staging tile, which is
+// copied out with coalesced u32 stores.
+// ---------------------------------------------------------------------------
+
+template <int W>
+struct MergePkCfg {
+    static constexpr int RW = 2 * W + 1;
+    static constexpr int ITEMS = W <= 2 ? 8 : 4;
+    static constexpr int TILE = kBlock * ITEMS;
+};
+
+template <int W>
+__device__ __forceinline__ bool pk_le(const u32* __restrict__ a, const u32* __restrict__ b) {
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        const u64 x = (u64)a[2 * j] | ((u64)a[2 * j + 1] << 32);
+        const u64 y = (u64)b[2 * j] | ((u64)b[2 * j + 1] << 32);
+        if (x != y) return x < y;
+    }
+    return true;
+}
+
+template <int W>
+__device__ __forceinline__ bool pk_eq(const u32* __restrict__ a, const u32* __restrict__ b) {
+#pragma unroll
+    for (int j = 0; j < 2 * W; j++)
+        if (a[j] != b[j]) return false;
+    return true;
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void merge_split_packed_k(const u32* __restrict__ A, u64 na,
+                                                               const u32* __restrict__ B, u64 nb, u64 ntiles,
+                                                               u64* __restrict__ split) {
+    constexpr int RW = MergePkCfg<W>::RW;
+    constexpr u64 TILE = MergePkCfg<W>::TILE;
+    for (u64 t = (u64)blockIdx.x * kBlock + threadIdx.x; t <= ntiles; t += (u64)gridDim.x * kBlock) {
+        const u64 diag = min(t * TILE, na + nb);
+        u64 lo = diag > nb ? diag - nb : 0, hi = diag < na ? diag : na;
+        while (lo < hi) {
+            const u64 mid = (lo + hi) >> 1;
+            if (pk_le<W>(A + mid * RW, B + (diag - 1 - mid) * RW))
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        split[t] = lo;
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void merge_tile_packed_k(const u32* __restrict__ A, u64 na,
+                                                              const u32* __restrict__ B, u64 nb,
+                                                              const u64* __restrict__ split, u64 ntiles,
+                                                              u32* __restrict__ out, u32* __restrict__ dup) {
+    constexpr int RW = MergePkCfg<W>::RW;
+    constexpr int ITEMS = MergePkCfg<W>::ITEMS;
+    constexpr int TILE = MergePkCfg<W>::TILE;
+    __shared__ u32 sin[TILE * RW];   // A slice, then B slice
+    __shared__ u32 sout[TILE * RW];  // merged tile
+    const int tid = threadIdx.x;
+    bool seen_dup = false;
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const u64 d0 = t * (u64)TILE, d1 = min(d0 + TILE, na + nb);
+        const u64 i0 = split[t], i1 = split[t + 1];
+        const u64 j0 = d0 - i0, j1 = d1 - i1;
+        const u32 la = (u32)(i1 - i0), lb = (u32)(j1 - j0), n = la + lb;
+        for (u32 x = tid; x < la * RW; x += kBlock) sin[x] = __builtin_nontemporal_load(A + i0 * RW + x);
+        for (u32 x = tid; x < lb * RW; x += kBlock) sin[la * RW + x] = __builtin_nontemporal_load(B + j0 * RW + x);
+        __syncthreads();
+        const u32 dl = min((u32)tid * ITEMS, n);
+        u32 lo = dl > lb ? dl - lb : 0, hi = dl < la ? dl : la;
+        while (lo < hi) {
+            const u32 mid = (lo + hi) >> 1;
+            if (pk_le<W>(sin + mid * RW, sin + (la + dl - 1 - mid) * RW))
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        u32 ia = lo, ib = dl - lo;
+        const u32 de = min(dl + ITEMS, n);
+        for (u32 d = dl; d < de; d++) {
+            const bool takea = ib >= lb || (ia < la && pk_le<W>(sin + ia * RW, sin + (la + ib) * RW));
+            const u32 x = takea ? ia : la + ib;
+            if (takea)
+                ia++;
+            else
+                ib++;
+#pragma unroll
+            for (int j = 0; j < RW; j++) sout[d * RW + j] = sin[x * RW + j];
+        }
+        __syncthreads();
+        // a key of both runs: two equal neighbours in the output (at the tile
+        // start, the neighbour is the larger of A[i0 - 1], B[j0 - 1])
+        for (u32 d = tid; d < n; d += kBlock) {
+            if (d > 0) {
+                seen_dup |= pk_eq<W>(sout + d * RW, sout + (d - 1) * RW);
+            } else {
+                if (i0 > 0) {
+                    u32 p[RW];
+#pragma unroll
+                    for (int j = 0; j < RW; j++) p[j] = A[(i0 - 1) * RW + j];
+                    seen_dup |= pk_eq<W>(sout, p);
+                }
+                if (j0 > 0) {
+                    u32 p[RW];
+#pragma unroll
+                    for (int j = 0; j < RW; j++) p[j] = B[(j0 - 1) * RW + j];
+                    seen_dup |= pk_eq<W>(sout, p);
+                }
+            }
+        }
+        for (u32 x = tid; x < n * RW; x += kBlock) out[d0 * RW + x] = sout[x];
+        __syncthreads();
+    }
+    if (__ballot(seen_dup) && lane_id() == 0) atomicOr(dup, 1u);
+}
+
+hipError_t launch_merge_packed(int W, const void* a, uint64_t na, const void* b, uint64_t nb, void* out,
+                               uint64_t* split, uint32_t* dup, hipStream_t s) {
+    const u64 n = na + nb;
+    if (n == 0) return hipSuccess;
+    const u64 tile = (u64)kBlock * (W <= 2 ? 8 : 4);
+    const u64 ntiles = (n + tile - 1) / tile;
+    const int gs = (int)hmin((ntiles + 1 + kBlock - 1) / kBlock, 4096);
+    const int gt = (int)hmin(ntiles, 8192);
+#define KC_MGP(WW)                                                                                                \
+    hipLaunchKernelGGL(merge_split_packed_k<WW>, dim3(gs), dim3(kBlock), 0, s, (const u32*)a, na, (const u32*)b, \
+                       nb, ntiles, split);                                                                        \
+    hipLaunchKernelGGL(merge_tile_packed_k<WW>, dim3(gt), dim3(kBlock), 0, s, (const u32*)a, na, (const u32*)b,  \
+                       nb, (const u64*)split, ntiles, (u32*)out, dup)
+    switch (W) {
+    case 1: KC_MGP(1); break;
+    case 2: KC_MGP(2); break;
+    case 3: KC_MGP(3); break;
+    case 4: KC_MGP(4); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef KC_MGP
+    return hipGetLastError();
+}
+
+uint64_t merge_packed_split_elems(int W, uint64_t n) {
+    return n / ((uint64_t)kBlock * (W <= 2 ? 8 : 4)) + 2;
+}
 
 hipError_t launch_unpack(int W, const void* packed, uint64_t n, uint64_t* keys, uint64_t stride, uint32_t* cnts,
                          hipStream_t s) {

@@ -3,12 +3,35 @@
 #include "kc_stage.h"
 
 #include <fcntl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 
 namespace kc {
+
+bool trace_on() {
+    static const bool on = getenv("KC_TRACE") != nullptr;
+    return on;
+}
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void trace(const char* fmt, ...) {
+    if (!trace_on()) return;
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "kc-trace %.6f %s\n", now_s(), buf);
+}
 
 // ---------------------------------------------------------------------------
 // Pool
@@ -85,7 +108,7 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
 }
 
 void par_memcpy(Pool* pool, void* dst, const void* src, size_t n) {
-    const size_t kPiece = (size_t)4 << 20;
+    const size_t kPiece = (size_t)1 << 20;
     int parts = pool ? (int)std::min<size_t>((size_t)pool->size(), (n + kPiece - 1) / kPiece) : 1;
     if (parts <= 1) {
         memcpy(dst, src, n);
@@ -197,9 +220,13 @@ hipError_t PinnedRing::download(const void* d_src, size_t n, hipStream_t s,
             issued++;
         }
         const int i = (int)(j % K);
+        const double t0 = trace_on() ? now_s() : 0;
         if ((r = take(i)) != hipSuccess) return r;
+        const double t1 = trace_on() ? now_s() : 0;
         const size_t off = j * slot_bytes_;
-        if (!sink(slot_[i], std::min(slot_bytes_, n - off), off)) {
+        const bool ok = sink(slot_[i], std::min(slot_bytes_, n - off), off);
+        if (trace_on()) trace("download piece %zu: wait %.3f ms sink %.3f ms", j, (t1 - t0) * 1e3, (now_s() - t1) * 1e3);
+        if (!ok) {
             (void)drain();
             return hipErrorUnknown;
         }
@@ -321,6 +348,7 @@ bool FastqFileReader::fill(int b, int prev) {
         err_ = "read error";
         return false;
     }
+    if (trace_on()) trace("reader block %zu bytes at %llu", want, (unsigned long long)at);
     pos_ += want;
     len_[b] = carry + want;
     if (pos_ >= size_) {
@@ -384,6 +412,7 @@ void FastqFileReader::produce() {
 
 bool FastqFileReader::next(Block* b) {
     std::unique_lock<std::mutex> g(m_);
+    if (trace_on() && !(ready_head_ < ready_.size() || done_)) trace("consumer waits for a block");
     cv_.wait(g, [&]() { return ready_head_ < ready_.size() || done_; });
     if (ready_head_ >= ready_.size()) return false;
     *b = ready_[ready_head_++];

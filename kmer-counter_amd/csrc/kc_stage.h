@@ -30,6 +30,12 @@
 
 namespace kc {
 
+// Host-side phase tracing (KC_TRACE=1): one line per phase on stderr with
+// its wall time; the tracing subsystem the reference lacks.
+bool trace_on();
+double now_s();
+void trace(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
 class Pool {
   public:
     explicit Pool(int n_threads);

@@ -56,6 +56,11 @@ def lib():
     return _lib
 
 
+def _take(ptr, n: int) -> bytes:
+    """n bytes at a C pointer (ctypes.string_at takes a C int size: <= 2 GiB)."""
+    return (ctypes.c_char * n).from_address(ptr.value if hasattr(ptr, "value") else ptr).raw
+
+
 def rs_of(k: int) -> int:
     return 8 * ((k + 31) // 32) + 4
 
@@ -71,7 +76,7 @@ def count_fastq(data: bytes, k: int, gpu_memory_limit: int = 100000000, mode: st
     n = L.oracle_count_fastq(data, len(data), k, gpu_memory_limit, 1 if mode == "ref" else 0, ctypes.byref(out))
     if n < 0:
         raise ValueError("bad oracle arguments")
-    res = ctypes.string_at(out, n * rs_of(k)) if n else b""
+    res = _take(out, n * rs_of(k)) if n else b""
     L.oracle_free(out)
     return res
 
@@ -87,7 +92,7 @@ def count_chunks(chunks, k: int, mode: str = "spec") -> bytes:
             L.oracle_acc_add_chunk_spec(acc, data, len(data), ll)
     out = ctypes.c_void_p()
     n = L.oracle_acc_finish(acc, ctypes.byref(out))
-    res = ctypes.string_at(out, n * rs_of(k)) if n else b""
+    res = _take(out, n * rs_of(k)) if n else b""
     L.oracle_free(out)
     L.oracle_acc_free(acc)
     return res
@@ -125,7 +130,7 @@ def refcpu(data: bytes, k: int, gpu_memory_limit: int = 100000000, threads: int 
     n = L.oracle_refcpu_count(data, len(data), k, gpu_memory_limit, threads, ctypes.byref(out), ctypes.byref(win))
     if n < 0:
         raise ValueError("bad oracle arguments")
-    res = ctypes.string_at(out, n * rs_of(k)) if n else b""
+    res = _take(out, n * rs_of(k)) if n else b""
     L.oracle_free(out)
     return res, win.value
 
