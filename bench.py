@@ -243,7 +243,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="SURVEY §8d preset: 2 = k=31, 50M x 150 bp from a 250 Mbp genome (the metric's "
-                         "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality)")
+                         "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality) with a "
+                         "48 GiB working set: the records outgrow half of it and are cut into sorted runs (the "
+                         "spill -> sort -> merge path), merged on the device")
     ap.add_argument("--mode", default="e2e", choices=["e2e", "device"],
                     help="value = file-to-file rate (e2e) or the device-resident rate (device)")
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
@@ -263,7 +265,7 @@ def main():
                     help="N>1: key-space all-to-all (cfg4) or read-shard + merge on rank 0 (cfg3)")
     args = ap.parse_args()
     preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
-              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=72 << 30)}[args.config]
+              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=48 << 30)}[args.config]
     for key, v in preset.items():
         if getattr(args, key) is None:
             setattr(args, key, v)
@@ -297,15 +299,20 @@ def main():
     # ---- end-to-end: file in -> output file closed -------------------------------
     phase = {"count_file": 0.0, "finish": 0.0, "output": 0.0}
     out_bytes = [0]
+    out_files = []
 
     def e2e_step():
+        # every step writes a new output file (no page cache of an earlier
+        # output to overwrite); the files are removed after the timed region
+        path = f"{out_path}.{len(out_files)}"
+        out_files.append(path)
         t0 = time.perf_counter()
         ctx.reset()
         ctx.count_file(in_path, L if varlen else 0)
         t1 = time.perf_counter()
         ctx.finish()
         t2 = time.perf_counter()
-        out_bytes[0] = write_node_output(kca, ctx, D, out_path, exchange)
+        out_bytes[0] = write_node_output(kca, ctx, D, path, exchange)
         t3 = time.perf_counter()
         phase["count_file"] += t1 - t0
         phase["finish"] += t2 - t1
@@ -326,6 +333,10 @@ def main():
     e2e = None
     if args.mode == "e2e":
         el = timed(e2e_step, args.steps, args.warmup)
+        for p in out_files:
+            for q in (p, f"{p}.part{D.rank}"):
+                if os.path.exists(q) and (D.rank == 0 or q != p):
+                    os.unlink(q)
         st = ctx.stats()
         win = D.sum(windows_of_step(st))
         in_b = D.sum(nbytes)
@@ -567,12 +578,17 @@ def host_variants(kca, ctx, args, host, nbytes, out_path, k, L):
             best = dt if best is None else min(best, dt)
         return best
 
+    outs = []
+
     def host_step():
+        outs.append(f"{out_path}.h{len(outs)}")
         ctx.reset()
         ctx.count_fastq_host(host.ctypes.data, nbytes)
-        ctx.write_output(out_path)
+        ctx.write_output(outs[-1])
 
     dt = one(host_step)
+    for p in outs:
+        os.unlink(p)
     res["host_memory"] = {"value": win / dt, "ms_per_step": dt * 1e3,
                           "path": "FASTQ in pageable host memory -> pinned ring -> PCIe -> GPU decode + count -> "
                                   "SortedKMerFile closed"}

@@ -305,6 +305,14 @@ kc_status kc_merge_runs_device(kc_ctx* ctx, const void* d_packed, const uint64_t
  * contexts' runs one after another in order is the whole SortedKMerFile.
  * Slices move by hipMemcpyPeer. Every ctx finished, same k, no spill runs. */
 kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n);
+/* Read-shard merge between n contexts of one process (the CLI's gpus=N,
+ * exchange=none): every finished context's sorted run is copied to ctxs[0]'s
+ * device (hipMemcpyPeer) and merged there by merge path (the device form of
+ * the reference's KMerFileMergeHandler k-way merge,
+ * KMerFileMergeHandler.cpp:49-100); ctxs[0] then holds the whole count.
+ * KC_ERR_STATE when a context keeps spill runs in host memory (merge those
+ * with kc_write_runs + kc_merge_files). */
+kc_status kc_gather_contexts(kc_ctx* const* ctxs, uint32_t n);
 /* Device->device copy on the ctx's stream (exchange staging). */
 kc_status kc_copy_device(kc_ctx* ctx, void* d_dst, const void* d_src, uint64_t n_bytes);
 

@@ -161,6 +161,7 @@ def lib() -> ctypes.CDLL:
         "kc_commit": ([vp], ctypes.c_int),
         "kc_count_file": ([P(vp), u32, ctypes.c_char_p, i64, u32, P(u64)], ctypes.c_int),
         "kc_write_output_at": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
+        "kc_gather_contexts": ([P(vp), u32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -431,6 +432,15 @@ def exchange_contexts(ctxs) -> None:
     L = lib()
     arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
     st = L.kc_exchange_contexts(arr, len(ctxs))
+    if st:
+        raise KcError(st, f"{L.kc_strerror(st).decode()}: {L.kc_last_error(ctxs[0]._h).decode()}")
+
+
+def gather_contexts(ctxs) -> None:
+    """kc_gather_contexts: every context's run merged on ctxs[0]'s device."""
+    L = lib()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    st = L.kc_gather_contexts(arr, len(ctxs))
     if st:
         raise KcError(st, f"{L.kc_strerror(st).decode()}: {L.kc_last_error(ctxs[0]._h).decode()}")
 

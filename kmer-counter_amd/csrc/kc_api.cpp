@@ -107,6 +107,11 @@ struct kc_ctx {
     // host staging (kc_stage.h), created on the first host-pointer input or output
     kc::Pool* pool = nullptr;
     kc::PinnedRing* ring = nullptr;
+    std::vector<char*> file_bufs;  // pinned blocks of kc_count_file's reader (kept: pinning is slow)
+    size_t file_buf_bytes = 0;
+    hipStream_t copy_stream = nullptr;  // kc_count_file: block i+1 uploads while block i is decoded
+    hipEvent_t file_ev[2] = {nullptr, nullptr};
+    DevBuf file_stage[2];
 
     // Pending batch: reads already indexed and 2-bit encoded into part_codes /
     // part_inval (/ part_rlen) by kc_count_* calls, counted together at the
@@ -128,6 +133,7 @@ struct kc_ctx {
     // only when HBM is short, as c->runs), merged on the device by kc_finish
     std::vector<DevBuf> dev_runs;
     std::vector<uint64_t> dev_run_n;
+    std::vector<DevBuf> run_pool;  // run buffers of earlier counts, reused (allocations are kept like all others)
     uint64_t runs_cut = 0;
     uint64_t batches_cut = 0;  // batches of the records already cut into runs
 
@@ -144,7 +150,7 @@ struct kc_ctx {
 static kc_status cut_run(kc_ctx* c);
 static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
 static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
-static void release_dev_runs(kc_ctx* c);
+static void release_dev_runs(kc_ctx* c, bool free_pool);
 
 static kc_status fail(kc_ctx* c, kc_status s, const char* fmt, ...) {
     if (c) {
@@ -249,6 +255,31 @@ static kc_status sort_records(kc_ctx* c, uint64_t* ka, uint64_t* kb, uint32_t* v
 // spill runs: sort the spill buffer, run-length reduce, pack, move to host
 // ---------------------------------------------------------------------------
 
+// A sorted packed run of n records (device memory, rewritten later) kept as a
+// device run when HBM has room for it plus a margin; false: the caller keeps
+// it on the host.
+static bool keep_run_on_device(kc_ctx* c, const void* packed, uint64_t n) {
+    const size_t bytes = (size_t)n * c->rs;
+    size_t mfree = 0, mtotal = 0;
+    DevBuf run;
+    if (hipMemGetInfo(&mfree, &mtotal) != hipSuccess || mfree < bytes + ((size_t)4 << 30) ||
+        hipMalloc(&run.p, bytes ? bytes : 16) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    run.bytes = bytes;
+    if (hipMemcpyAsync(run.p, packed, bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        (void)hipFree(run.p);
+        (void)hipGetLastError();
+        return false;
+    }
+    c->dev_runs.push_back(run);
+    c->dev_run_n.push_back(n);
+    c->runs_cut++;
+    return true;
+}
+
 // Sorts n spilled keys (SoA at `stride` in `keys`, `scratch` of the same
 // shape), run-length reduces them and stores the run (host memory or a temp
 // file).
@@ -276,12 +307,15 @@ static kc_status flush_keys(kc_ctx* c, uint64_t* keys, uint64_t stride, uint64_t
     size_t bytes = (size_t)m * c->rs;
     if ((s = ensure(c, c->run_packed, bytes))) return s;
     HIPCHK(c, launch_pack(W, (uint64_t*)c->run_keys.p, n, (uint32_t*)c->run_cnts.p, m, c->run_packed.p, c->stream));
+    c->spilled_flushed += n;
+    // the run stays in HBM (merged on the device by kc_finish) unless HBM is
+    // short: then host memory, or a file in tempFileLocation
+    if (keep_run_on_device(c, c->run_packed.p, m)) return KC_OK;
     HostRun run;
     run.records = m;
     run.mem.resize(bytes);
     HIPCHK(c, hipMemcpyAsync(run.mem.data(), c->run_packed.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->spilled_flushed += n;
     if (!c->temp_dir.empty()) {
         char name[128];
         snprintf(name, sizeof(name), "/kc.%d.%llu.%zu", (int)getpid(), (unsigned long long)c->id, c->runs.size());
@@ -1273,7 +1307,13 @@ void kc_destroy(kc_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     delete c->ring;  // waits for its DMAs
     delete c->pool;
-    release_dev_runs(c);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    for (char* b : c->file_bufs) (void)hipHostFree(b);
+    for (auto& b : c->file_stage) release(b);
+    for (auto& e : c->file_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    release_dev_runs(c, true);
     for (auto& r : c->runs)
         if (!r.path.empty()) unlink(r.path.c_str());
     DevBuf* bufs[] = {&c->in_stage, &c->fq_counts, &c->fq_base, &c->fq_tmp, &c->seq_off, &c->seq_end,
@@ -1341,7 +1381,7 @@ kc_status kc_reset(kc_ctx* c) {
         if (!r.path.empty()) unlink(r.path.c_str());
     c->runs.clear();
     c->spilled_flushed = 0;
-    release_dev_runs(c);
+    release_dev_runs(c, false);
     c->runs_cut = 0;
     c->batches_cut = 0;
     c->pend_reads = 0;
@@ -1468,14 +1508,25 @@ static size_t file_block_bytes() {
     return kFileBlock;
 }
 
-// A block of the file reader (pinned): DMA straight into the staging buffer,
-// then the GPU decode (which waits for its checks, so the reader may refill
-// the block when this returns).
-static kc_status file_block(kc_ctx* c, const char* p, size_t n, int64_t L, bool count, uint64_t* got) {
+// Uploads a block of the file reader (pinned) into staging buffer `slot` on
+// the ctx's copy stream; the decode waits for it through file_ev[slot].
+static kc_status file_upload(kc_ctx* c, int slot, const char* p, size_t n) {
     kc_status s;
-    if ((s = ensure(c, c->in_stage, n + 64))) return s;
-    HIPCHK(c, hipMemcpyAsync(c->in_stage.p, p, n, hipMemcpyHostToDevice, c->stream));
-    return fastq_device(c, c->in_stage.p, n, L, got, count);
+    if (!c->copy_stream) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        for (auto& e : c->file_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if ((s = ensure(c, c->file_stage[slot], n + 64))) return s;
+    HIPCHK(c, hipMemcpyAsync(c->file_stage[slot].p, p, n, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(c, hipEventRecord(c->file_ev[slot], c->copy_stream));
+    return KC_OK;
+}
+
+// The GPU decode of an uploaded block (waits for its checks, hence for the
+// upload: the reader may refill the block when this returns).
+static kc_status file_decode(kc_ctx* c, int slot, size_t n, int64_t L, bool count, uint64_t* got) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->file_ev[slot], 0));
+    return fastq_device(c, c->file_stage[slot].p, n, L, got, count);
 }
 
 // Streams the file's blocks to the contexts (each block to whichever context
@@ -1483,13 +1534,32 @@ static kc_status file_block(kc_ctx* c, const char* p, size_t n, int64_t L, bool 
 // context stops; *failed names the context that reported it.
 static kc_status file_blocks(kc_ctx* const* ctxs, uint32_t n_ctx, const char* path, int64_t L, bool count,
                              uint64_t* reads, kc_ctx** failed) {
-    kc::FastqFileReader rd(file_block_bytes(), (int)n_ctx + 2, 8);
+    // the reader's pinned buffers live in ctxs[0] (2 n_ctx + 2 of them: two per
+    // context in flight, one filling, one holding the carried tail)
+    kc_ctx* c0 = ctxs[0];
+    const size_t block = file_block_bytes();
+    const size_t want = block + kc::FastqFileReader::carry_bytes();
+    if (c0->file_buf_bytes != want) {
+        for (char* b : c0->file_bufs) (void)hipHostFree(b);
+        c0->file_bufs.clear();
+        c0->file_buf_bytes = want;
+    }
+    HIPCHK(c0, hipSetDevice(c0->cfg.device));
+    while (c0->file_bufs.size() < 2 * (size_t)n_ctx + 2) {
+        char* b = nullptr;
+        HIPCHK(c0, hipHostMalloc((void**)&b, want, 0));
+        c0->file_bufs.push_back(b);
+    }
+    std::vector<char*> bufs(c0->file_bufs.begin(), c0->file_bufs.begin() + 2 * n_ctx + 2);
+    kc::FastqFileReader rd(block, bufs, 8);
     std::string err;
     *failed = ctxs[0];
     if (!rd.open(path, &err)) return fail(ctxs[0], KC_ERR_IO, "%s", err.c_str());
     std::atomic<bool> stop(false);
     std::vector<kc_status> st(n_ctx, KC_OK);
     std::vector<uint64_t> nr(n_ctx, 0);
+    // per context: block i + 1 is uploaded (copy stream) while block i is
+    // decoded (ctx stream)
     auto work = [&](uint32_t g) {
         kc_ctx* c = ctxs[g];
         if (hipSetDevice(c->cfg.device) != hipSuccess) {
@@ -1497,20 +1567,37 @@ static kc_status file_blocks(kc_ctx* const* ctxs, uint32_t n_ctx, const char* pa
             stop = true;
             return;
         }
-        kc::FastqFileReader::Block b;
-        while (!stop && rd.next(&b)) {
+        kc::FastqFileReader::Block cur, nxt;
+        bool have = !stop && rd.next(&cur);
+        int slot = 0;
+        kc_status s = have ? file_upload(c, slot, cur.p, cur.n) : KC_OK;
+        while (have && !s) {
+            const bool have_nxt = !stop && rd.next(&nxt);
+            if (have_nxt && (s = file_upload(c, slot ^ 1, nxt.p, nxt.n))) {
+                rd.release(nxt);
+                break;
+            }
             uint64_t got = 0;
             const double t0 = kc::trace_on() ? kc::now_s() : 0;
-            kc_status s = file_block(c, b.p, b.n, L, count, &got);
-            if (kc::trace_on()) kc::trace("ctx %u block %llu: %zu bytes, upload + decode %.3f ms", g,
-                                          (unsigned long long)b.index, b.n, (kc::now_s() - t0) * 1e3);
-            rd.release(b);
-            if (s) {
-                st[g] = s;
-                stop = true;
-                return;
-            }
+            s = file_decode(c, slot, cur.n, L, count, &got);
+            if (kc::trace_on()) kc::trace("ctx %u block %llu: %zu bytes, decode (+ upload wait) %.3f ms", g,
+                                          (unsigned long long)cur.index, cur.n, (kc::now_s() - t0) * 1e3);
+            rd.release(cur);
             nr[g] += got;
+            if (s) {
+                if (have_nxt) {
+                    (void)hipStreamSynchronize(c->copy_stream);
+                    rd.release(nxt);
+                }
+                break;
+            }
+            cur = nxt;
+            have = have_nxt;
+            slot ^= 1;
+        }
+        if (s) {
+            st[g] = s;
+            stop = true;
         }
     };
     if (n_ctx == 1) {
@@ -1911,7 +1998,7 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
         std::vector<std::pair<const void*, uint64_t>> runs;
         for (size_t r = 0; r < c->dev_runs.size(); r++) runs.push_back({c->dev_runs[r].p, c->dev_run_n[r]});
         s = merge_runs_packed(c, runs);
-        release_dev_runs(c);
+        release_dev_runs(c, false);
         if (s) return s;
         c->st.table_used = 0;
         if (n_records) *n_records = c->n_records;
@@ -2011,15 +2098,20 @@ static kc_status table_run_to_host(kc_ctx* c, std::vector<uint8_t>* mem) {
     return KC_OK;
 }
 
-// The finished table run into a file at byte `at` (a new file, truncated,
-// when `truncate`): device -> pinned slot DMAs overlap the writes of the
-// previous slot.
-static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0, bool truncate = true) {
+// The finished table run into a file at byte `at` (`whole`: the file is
+// exactly the run, as after truncating it — the reference appends,
+// KMerFileMerger.cpp:129): device -> pinned slot DMAs overlap the writes of
+// the previous slot. An existing file is not truncated first but overwritten
+// in place and cut to size at the end (truncating a cached file frees its
+// pages, ~60 ms per GB, and the writes then allocate them again); the range
+// is allocated up front (fallocate), the writes go out in 8 MiB pieces.
+static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0, bool whole = true) {
     const uint64_t bytes = c->n_records * c->rs;
     const double t0 = kc::trace_on() ? kc::now_s() : 0;
-    int fd = open(path, O_CREAT | O_WRONLY | (truncate ? O_TRUNC : 0), 0644);
-    if (kc::trace_on()) kc::trace("output open%s %.3f ms", truncate ? " (truncate)" : "", (kc::now_s() - t0) * 1e3);
+    int fd = open(path, O_CREAT | O_WRONLY, 0644);
     if (fd < 0) return fail(c, KC_ERR_IO, "cannot open output file %s", path);
+    if (bytes) (void)fallocate(fd, 0, (off_t)at, (off_t)bytes);  // a hint: filesystems without it just write
+    if (kc::trace_on()) kc::trace("output open + fallocate %.3f ms", (kc::now_s() - t0) * 1e3);
     kc_status s = KC_OK;
     if (bytes) {
         HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -2030,7 +2122,8 @@ static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0,
         hipError_t e = c->ring->download(c->fin_packed.p, bytes, c->stream, [&](const char* p, size_t n, size_t off) {
             size_t done = 0;
             while (done < n) {
-                ssize_t w = pwrite(fd, p + done, n - done, (off_t)(at + off + done));
+                const size_t piece = std::min((size_t)8 << 20, n - done);
+                ssize_t w = pwrite(fd, p + done, piece, (off_t)(at + off + done));
                 if (w <= 0) return false;
                 done += (size_t)w;
             }
@@ -2039,6 +2132,7 @@ static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0,
         if (e == hipErrorUnknown) s = fail(c, KC_ERR_IO, "short write to %s", path);
         else if (e != hipSuccess) s = fail(c, KC_ERR_HIP, "output copy: %s", hipGetErrorString(e));
     }
+    if (!s && whole && ftruncate(fd, (off_t)(at + bytes)) != 0) s = fail(c, KC_ERR_IO, "cannot size %s", path);
     if (close(fd) != 0 && !s) s = fail(c, KC_ERR_IO, "cannot close %s", path);
     if (kc::trace_on()) kc::trace("output %llu bytes in %.3f ms", (unsigned long long)bytes, (kc::now_s() - t0) * 1e3);
     return s;
@@ -2404,18 +2498,20 @@ static kc_status cut_run(kc_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const size_t bytes = (size_t)n * c->rs;
     if (n) {
+        // the run takes over fin_packed's buffer (no copy); fin_packed gets a
+        // pooled buffer back (grown by the next finish if it is short)
         size_t mfree = 0, mtotal = 0;
-        DevBuf run;
-        if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > bytes + ((size_t)4 << 30) &&
-            hipMalloc(&run.p, bytes) == hipSuccess) {
-            run.bytes = bytes;
-            HIPCHK(c, hipMemcpyAsync(run.p, c->fin_packed.p, bytes, hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > ((size_t)4 << 30)) {
+            DevBuf run = c->fin_packed;
+            c->fin_packed = DevBuf();
+            if (!c->run_pool.empty()) {
+                c->fin_packed = c->run_pool.back();
+                c->run_pool.pop_back();
+            }
             c->dev_runs.push_back(run);
             c->dev_run_n.push_back(n);
             c->runs_cut++;
         } else {
-            (void)hipGetLastError();
             HostRun hr;
             hr.records = n;
             hr.mem.resize(bytes);
@@ -2445,10 +2541,14 @@ static kc_status cut_run_if_full(kc_ctx* c) {
     return cut_run(c);
 }
 
-static void release_dev_runs(kc_ctx* c) {
-    for (auto& r : c->dev_runs) release(r);
+static void release_dev_runs(kc_ctx* c, bool free_pool) {
+    for (auto& r : c->dev_runs) c->run_pool.push_back(r);
     c->dev_runs.clear();
     c->dev_run_n.clear();
+    if (free_pool) {
+        for (auto& r : c->run_pool) release(r);
+        c->run_pool.clear();
+    }
 }
 
 extern "C" {
@@ -2533,6 +2633,40 @@ kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n) {
     }
     release();
     return KC_OK;
+}
+
+kc_status kc_gather_contexts(kc_ctx* const* ctxs, uint32_t n) {
+    if (!ctxs || n == 0) return KC_ERR_ARG;
+    for (uint32_t r = 0; r < n; r++) {
+        if (!ctxs[r] || ctxs[r]->W != ctxs[0]->W) return KC_ERR_ARG;
+        if (!ctxs[r]->finished) return fail(ctxs[r], KC_ERR_STATE, "call kc_finish first");
+        if (!ctxs[r]->runs.empty()) return fail(ctxs[r], KC_ERR_STATE, "host spill runs exist: merge on the host");
+    }
+    kc_ctx* c0 = ctxs[0];
+    const uint64_t rs = (uint64_t)c0->rs;
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < n; r++) total += ctxs[r]->n_records;
+    HIPCHK(c0, hipSetDevice(c0->cfg.device));
+    void* recv = nullptr;
+    HIPCHK(c0, hipMalloc(&recv, total * rs + 16));
+    std::vector<std::pair<const void*, uint64_t>> runs;
+    uint64_t off = 0;
+    for (uint32_t r = 0; r < n; r++) {
+        const uint64_t bytes = ctxs[r]->n_records * rs;
+        hipError_t e = bytes ? hipMemcpyPeerAsync((uint8_t*)recv + off * rs, c0->cfg.device, ctxs[r]->fin_packed.p,
+                                                  ctxs[r]->cfg.device, bytes, c0->stream)
+                             : hipSuccess;
+        if (e != hipSuccess) {
+            (void)hipFree(recv);
+            return fail(c0, KC_ERR_HIP, "gather: %s", hipGetErrorString(e));
+        }
+        runs.push_back({(uint8_t*)recv + off * rs, ctxs[r]->n_records});
+        off += ctxs[r]->n_records;
+    }
+    hipError_t e = hipStreamSynchronize(c0->stream);
+    kc_status s = e == hipSuccess ? merge_runs_packed(c0, runs) : fail(c0, KC_ERR_HIP, "gather: %s", hipGetErrorString(e));
+    (void)hipFree(recv);
+    return s;
 }
 
 kc_status kc_copy_device(kc_ctx* c, void* d_dst, const void* d_src, uint64_t n) {

@@ -385,20 +385,32 @@ int main(int argc, char** argv) {
         }
         if (fclose(out)) die(nullptr, KC_ERR_IO, o.output_file.c_str());
     } else {
-        std::vector<std::string> all;
-        for (auto& w : gw) {
-            std::string prefix = o.temp_dir + "/kc_gpu" + std::to_string(w.gpu) + "." + std::to_string(getpid());
-            uint32_t nr = 0;
-            kc_status s = kc_write_runs(w.ctx, prefix.c_str(), &nr);
-            if (s) die(w.ctx, s, "write runs");
-            for (uint32_t i = 0; i < nr; i++) all.push_back(prefix + "." + std::to_string(i));
+        // read-shard: the contexts' runs merged on the first context's GPU
+        // (kc_gather_contexts); contexts with spill runs in host memory take
+        // the host k-way merge (KMerFileMergeHandler semantics)
+        std::vector<kc_ctx*> cs;
+        for (auto& w : gw) cs.push_back(w.ctx);
+        kc_status s = kc_gather_contexts(cs.data(), (uint32_t)cs.size());
+        if (s == KC_OK) {
+            if ((s = kc_write_output(gw[0].ctx, o.output_file.c_str(), o.mergers_at_once, o.merge_threads)))
+                die(gw[0].ctx, s, "write output");
+        } else if (s == KC_ERR_STATE) {
+            std::vector<std::string> all;
+            for (auto& w : gw) {
+                std::string prefix = o.temp_dir + "/kc_gpu" + std::to_string(w.gpu) + "." + std::to_string(getpid());
+                uint32_t nr = 0;
+                if ((s = kc_write_runs(w.ctx, prefix.c_str(), &nr))) die(w.ctx, s, "write runs");
+                for (uint32_t i = 0; i < nr; i++) all.push_back(prefix + "." + std::to_string(i));
+            }
+            std::vector<const char*> ptrs;
+            for (auto& p : all) ptrs.push_back(p.c_str());
+            s = kc_merge_files(ptrs.data(), (uint32_t)ptrs.size(), o.output_file.c_str(), o.kmer_length,
+                               o.mergers_at_once, o.merge_threads);
+            for (auto& p : all) unlink(p.c_str());
+            if (s) die(nullptr, s, "merge");
+        } else {
+            die(cs[0], s, "gather");
         }
-        std::vector<const char*> ptrs;
-        for (auto& s : all) ptrs.push_back(s.c_str());
-        kc_status s = kc_merge_files(ptrs.data(), (uint32_t)ptrs.size(), o.output_file.c_str(), o.kmer_length,
-                                     o.mergers_at_once, o.merge_threads);
-        for (auto& p : all) unlink(p.c_str());
-        if (s) die(nullptr, s, "merge");
     }
     if (o.dump && !to_dump_format(o.output_file, (int)((o.kmer_length + 31) / 32)))
         die(nullptr, KC_ERR_IO, o.output_file.c_str());

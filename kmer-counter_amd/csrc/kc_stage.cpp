@@ -264,10 +264,10 @@ size_t fastq_cut(const char* p, size_t n) {
 
 static const size_t kCarryMax = (size_t)64 << 20;  // longest record carried between blocks
 
-FastqFileReader::FastqFileReader(size_t block_bytes, int nbuf, int read_threads)
-    : pool_(read_threads), block_(block_bytes) {
-    buf_.assign((size_t)(nbuf < 2 ? 2 : nbuf), nullptr);
-}
+size_t FastqFileReader::carry_bytes() { return kCarryMax; }
+
+FastqFileReader::FastqFileReader(size_t block_bytes, const std::vector<char*>& bufs, int read_threads)
+    : pool_(read_threads), block_(block_bytes), buf_(bufs) {}
 
 FastqFileReader::~FastqFileReader() {
     {
@@ -276,8 +276,6 @@ FastqFileReader::~FastqFileReader() {
     }
     cv_.notify_all();
     if (th_.joinable()) th_.join();
-    for (char* b : buf_)
-        if (b) (void)hipHostFree(b);
     if (fd_ >= 0) close(fd_);
 }
 
@@ -301,9 +299,9 @@ bool FastqFileReader::open(const std::string& path, std::string* err) {
     block_ = (size_t)std::min<uint64_t>(block_, size_);
     // a file of one block needs one buffer
     if (block_ >= size_) buf_.resize(1);
-    for (char*& b : buf_)
-        if (hipHostMalloc((void**)&b, block_ + kCarryMax, 0) != hipSuccess) {
-            *err = "cannot allocate pinned read buffers";
+    for (char* b : buf_)
+        if (!b) {
+            *err = "no pinned read buffers";
             return false;
         }
     len_.assign(buf_.size(), 0);

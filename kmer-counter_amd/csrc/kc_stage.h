@@ -108,8 +108,11 @@ class FastqFileReader {
         size_t n = 0;
         uint64_t index = 0;  // block number in the file
     };
-    FastqFileReader(size_t block_bytes, int nbuf, int read_threads);
+    // bufs: `nbuf` pinned buffers of block_bytes + carry_bytes() each, owned by
+    // the caller (pinning costs ~50 ms per GB: a context keeps them)
+    FastqFileReader(size_t block_bytes, const std::vector<char*>& bufs, int read_threads);
     ~FastqFileReader();
+    static size_t carry_bytes();
     bool open(const std::string& path, std::string* err);
     // next block in file order; false at the end of the file or on a read error
     bool next(Block* b);

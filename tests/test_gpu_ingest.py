@@ -256,3 +256,22 @@ def test_write_output_at_offsets_after_exchange(kca, orc, tmp_path):
         for c in ctxs:
             c.close()
     assert out.read_bytes() == orc.count_fastq(b"".join(shards), 31)
+
+
+@pytest.mark.parametrize("k,mem", [(31, 100_000_000), (55, 1 << 20)])
+def test_gather_contexts_merges_on_first_device(kca, orc, k, mem):
+    """kc_gather_contexts (read-shard merge on one GPU): three contexts count
+    shards (with a 1 MiB working set they also cut runs and spill), their runs
+    are merged by merge path on the first context's device."""
+    shards = [kca.synth_fastq(3000, 150, 70 + r, n_rate=0.001, genome_length=120_000) for r in range(3)]
+    ctxs = [kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=mem) for _ in shards]
+    try:
+        for c, fq in zip(ctxs, shards):
+            c.count_fastq(fq)
+            c.finish()
+        kca.gather_contexts(ctxs)
+        got = ctxs[0].records()
+    finally:
+        for c in ctxs:
+            c.close()
+    assert got == orc.count_fastq(b"".join(shards), k)
