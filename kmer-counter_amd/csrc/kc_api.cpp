@@ -79,6 +79,7 @@ struct kc_ctx {
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_dedup;  // skm P5a: per-bucket list starts (u64) and lengths (u32), list cursor
+    DevBuf p3b_buf, sub_starts;  // key-prefix engine, high cardinality: P3b tile positions, sub-bucket starts
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
     DevBuf part_rlen;               // KC_FLAG_VARLEN: each read's own length (u16)
     const uint16_t* var_rlen = nullptr;  // set while a variable-length block is counted
@@ -111,7 +112,9 @@ struct kc_ctx {
     size_t file_buf_bytes = 0;
     hipStream_t copy_stream = nullptr;  // kc_count_file: block i+1 uploads while block i is decoded
     hipEvent_t file_ev[2] = {nullptr, nullptr};
+    hipEvent_t stage_free[2] = {nullptr, nullptr};  // kc_count_chunk: the encode of the staged chunk is done
     DevBuf file_stage[2];
+    int chunk_slot = 0;
 
     // Pending batch: reads already indexed and 2-bit encoded into part_codes /
     // part_inval (/ part_rlen) by kc_count_* calls, counted together at the
@@ -562,6 +565,52 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
             c->part_ms[3] += t;
 
+            // P3b (high cardinality: most keys distinct): every bucket split
+            // once more by key bits 40..47 (a regional radix pass keys_b ->
+            // keys_a over the 65536 buckets), so P5 counts runs of
+            // consecutive sub-buckets in one pass each and reads every key
+            // once instead of once per sub-range pass
+            uint64_t* p5_keys = c->keys_b;
+            uint64_t* p5_spill = c->keys_a;
+            const uint64_t* sub_starts = nullptr;
+            // (KC_P3B_MIN: path selector for tests, same counts either way)
+            uint64_t p3b_min = 1ull << 22;
+            if (const char* e = getenv("KC_P3B_MIN")) p3b_min = strtoull(e, nullptr, 10);
+            if (c->hc_hint && n >= p3b_min && !getenv("KC_NO_P3B")) {
+                std::vector<uint64_t> rs((size_t)nb + 1);
+                HIPCHK(c, hipMemcpyAsync(rs.data(), c->part_starts.p, rs.size() * 8, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                const uint64_t tile = (uint64_t)rp_tile(W, false);
+                std::vector<uint64_t> rt(2 * ((size_t)nb + 1));
+                for (uint32_t r = 0; r <= nb; r++) rt[r] = rs[r];
+                uint64_t* tp = rt.data() + nb + 1;
+                tp[0] = 0;
+                for (uint32_t r = 0; r < nb; r++) tp[r + 1] = tp[r] + (rs[r + 1] - rs[r] + tile - 1) / tile;
+                const uint64_t nt = tp[nb];
+                const size_t pos_n = 256 * nt, cnt_n = (256 * nt + 1) / 2;
+                if ((s = ensure(c, c->p3b_buf, (pos_n + cnt_n + rt.size()) * 8)) ||
+                    (s = ensure(c, c->sub_starts, (((size_t)nb << 8) + 1) * 8)))
+                    return s;
+                uint64_t* pos = (uint64_t*)c->p3b_buf.p;
+                uint32_t* cnt_t = (uint32_t*)(pos + pos_n);
+                uint64_t* rtd = pos + pos_n + cnt_n;
+                HIPCHK(c, hipMemcpyAsync(rtd, rt.data(), rt.size() * 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                HIPCHK(c, launch_rp_hist_regional(c->keys_b, 40, rtd, rtd + nb + 1, (int)nb, nt, (uint32_t)tile, pos,
+                                                  cnt_t, 2 * c->n_cu, c->stream));
+                HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, c->key_cap, c->keys_a, c->key_cap, nullptr, nullptr,
+                                            rtd, rtd + nb + 1, (int)nb, nt, pos, 40, nullptr, 0, 2 * c->n_cu,
+                                            c->stream));
+                HIPCHK(c, launch_sub_starts(rtd, rtd + nb + 1, pos, nb, n, (uint64_t*)c->sub_starts.p, c->stream));
+                HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                HIPCHK(c, hipEventSynchronize(c->ev1));
+                HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                c->part_ms[2] += t;
+                p5_keys = c->keys_a;
+                p5_spill = c->keys_b;
+                sub_starts = (const uint64_t*)c->sub_starts.p;
+            }
+
             // Records: at most one LDS table per bucket unless buckets were
             // split into sub-range passes (high cardinality); on overflow P5
             // reruns with a bigger buffer (safe while nothing went to the
@@ -579,11 +628,11 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 if ((s = grow_records(c, rec0 + bound))) return s;
                 // keys_a is free after P3: it takes P5's spills (capacity >= n)
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-                HIPCHK(c, launch_count_buckets(W, c->keys_b, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
+                HIPCHK(c, launch_count_buckets(W, p5_keys, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
                                                c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
-                                               c->keys_a, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
+                                               p5_spill, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
                                                c->n_cu, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,
-                                               (uint32_t*)c->desc_len.p, kDescCap, c->stream, c->hc_hint));
+                                               (uint32_t*)c->desc_len.p, kDescCap, c->stream, c->hc_hint, sub_starts));
                 HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                 HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
                 if ((s = sync_stats(c))) return s;
@@ -613,7 +662,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
             uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
             if (n2) {
-                if ((s = flush_keys(c, c->keys_a, c->key_cap, n2, c->keys_b))) return s;
+                if ((s = flush_keys(c, p5_spill, c->key_cap, n2, p5_keys))) return s;
                 HIPCHK(c, hipMemsetAsync(c->stats + ST_SPILL2_FILL, 0, 8, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
                 c->stats_h[ST_SPILL2_FILL] = 0;
@@ -921,9 +970,66 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
     return KC_OK;
 }
 
+// Engine choice before the super-k-mer engine's first large batch: the
+// coverage sketch of the encoded reads (sketch_k). When most sampled k-mers
+// are distinct (low coverage: iid reads, SURVEY cfg5) the key-prefix engine
+// counts this batch and the rest of the context's input, and P5 splits its
+// buckets up front; the super-k-mer engine's bucket sample (count_reads_skm)
+// stays as the second check. Saves the skm engine's F and S passes over a
+// batch it would give up.
+static const double kSketchDistinctMax = 0.7;
+
+static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre0) {
+    kc_status s;
+    const uint64_t G = (uint64_t)groups_per_read((int)L);
+    const uint64_t cap = n_reads * G / 128 + 1024;  // ~1/256 of the aligned k-mers are kept
+    if ((s = ensure(c, c->fin_keys[0], cap * 8 + 64)) || (s = ensure(c, c->fin_keys[1], cap * 8 + 64)) ||
+        (s = ensure(c, c->fin_misc, 64)))
+        return s;
+    uint64_t* fp = (uint64_t*)c->fin_keys[0].p;
+    uint64_t* counter = (uint64_t*)c->fin_misc.p;
+    HIPCHK(c, hipMemsetAsync(counter, 0, 8, c->stream));
+    HIPCHK(c, launch_sketch((const uint32_t*)c->part_codes.p + (uint64_t)pre0 * G,
+                            (const uint16_t*)c->part_inval.p + (uint64_t)pre0 * G, n_reads, (int)L, (int)c->k, fp, cap,
+                            counter, c->stream));
+    uint64_t m = 0;
+    HIPCHK(c, hipMemcpyAsync(&m, counter, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (m > cap) m = cap;
+    if (m < 4096) return KC_OK;  // too few samples to tell: the skm engine's own sample decides
+    int which = 0;
+    if ((s = sort_records(c, fp, (uint64_t*)c->fin_keys[1].p, nullptr, nullptr, cap, m, &which, 1))) return s;
+    const uint64_t* sorted = (const uint64_t*)c->fin_keys[which].p;
+    if ((s = ensure(c, c->rle_flags, m * 4)) || (s = ensure(c, c->rle_pos, m * 4)) ||
+        (s = ensure(c, c->rle_tmp, scan_tmp_elems(m) * 4)))
+        return s;
+    HIPCHK(c, launch_rle_heads(1, sorted, cap, m, (uint32_t*)c->rle_flags.p, c->stream));
+    HIPCHK(c, launch_scan_u32((uint32_t*)c->rle_flags.p, (uint32_t*)c->rle_pos.p, m, (uint32_t*)c->rle_tmp.p,
+                              c->stream));
+    uint32_t last[2];
+    HIPCHK(c, hipMemcpyAsync(&last[0], (uint32_t*)c->rle_pos.p + (m - 1), 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&last[1], (uint32_t*)c->rle_flags.p + (m - 1), 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t distinct = (uint64_t)last[0] + last[1];
+    if (getenv("KC_DEBUG"))
+        fprintf(stderr, "kc: sketch %llu distinct / %llu sampled k-mers\n", (unsigned long long)distinct,
+                (unsigned long long)m);
+    if ((double)distinct > kSketchDistinctMax * (double)m) {
+        c->skm_hc = true;
+        c->hc_hint = true;
+        c->skm_checked = true;
+    }
+    return KC_OK;
+}
+
 // pre0 >= 0: the reads are pre-encoded in part_codes / part_inval from read pre0
 static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L,
                              int64_t pre0 = -1) {
+    if (c->skm && !c->skm_hc && !c->skm_force && !c->skm_checked && pre0 >= 0 && !getenv("KC_NO_SKETCH") &&
+        n_reads * (uint64_t)(L - c->k + 1) >= kSkmSampleMinKeys && skm_geometry((int)L, (int)c->k).ok) {
+        kc_status s = sketch_engine(c, n_reads, L, pre0);
+        if (s) return s;
+    }
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
     if (c->skm && !c->skm_hc) {
@@ -1312,6 +1418,8 @@ void kc_destroy(kc_ctx* c) {
     for (auto& b : c->file_stage) release(b);
     for (auto& e : c->file_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->stage_free)
+        if (e) (void)hipEventDestroy(e);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     release_dev_runs(c, true);
     for (auto& r : c->runs)
@@ -1331,6 +1439,8 @@ void kc_destroy(kc_ctx* c) {
     if (c->rec_cursor) (void)hipFree(c->rec_cursor);
     if (c->pool_cursor) (void)hipFree(c->pool_cursor);
     release(c->part_hist);
+    release(c->p3b_buf);
+    release(c->sub_starts);
     release(c->part_codes);
     release(c->part_inval);
     release(c->part_rlen);
@@ -1434,9 +1544,18 @@ kc_status kc_count_chunk_device(kc_ctx* c, const void* d_chunk, int64_t size, in
     return KC_OK;
 }
 
-// Host chunk: its whole reads go through the pinned ring into the staging
-// buffer; the encode is queued behind the upload on the ctx stream and the
-// call returns as soon as the caller's bytes are in pinned memory, so
+static kc_status copy_stream_init(kc_ctx* c) {
+    if (c->copy_stream) return KC_OK;
+    HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (auto& e : c->file_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : c->stage_free) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return KC_OK;
+}
+
+// Host chunk: its whole reads go through the pinned ring into one of two
+// staging buffers on the copy stream, the encode waits for that upload on
+// the ctx stream; the call returns as soon as the caller's bytes are in
+// pinned memory. Chunk i + 1 therefore uploads while chunk i is encoded, and
 // consecutive chunks (the reference's ~7.8 MB at gpuMemoryLimit=1e8,
 // KMerCounter.cpp:193-212) stream at the PCIe rate.
 kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) {
@@ -1447,11 +1566,23 @@ kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) 
     if (n == 0) return KC_OK;
     if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if ((s = stage_init(c))) return s;
+    if ((s = stage_init(c)) || (s = copy_stream_init(c))) return s;
     const size_t bytes = (size_t)(n * (uint64_t)L);
-    if ((s = ensure(c, c->in_stage, bytes + 64))) return s;
-    HIPCHK(c, c->ring->upload(c->in_stage.p, chunk, bytes, c->stream, c->pool));
-    return chunk_device(c, (const uint8_t*)c->in_stage.p, (int64_t)bytes, L);
+    const int slot = c->chunk_slot;
+    c->chunk_slot ^= 1;
+    DevBuf& st = c->file_stage[slot];
+    if (st.bytes < bytes + 64) {
+        // growing: nothing may still read or write the old buffer
+        HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+        if ((s = ensure(c, st, bytes + 64))) return s;
+    }
+    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->stage_free[slot], 0));
+    HIPCHK(c, c->ring->upload(st.p, chunk, bytes, c->copy_stream, c->pool));
+    HIPCHK(c, hipEventRecord(c->file_ev[slot], c->copy_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->file_ev[slot], 0));
+    if ((s = chunk_device(c, (const uint8_t*)st.p, (int64_t)bytes, L))) return s;
+    HIPCHK(c, hipEventRecord(c->stage_free[slot], c->stream));
+    return KC_OK;
 }
 
 static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_t L, uint64_t* n_reads,
@@ -1512,11 +1643,12 @@ static size_t file_block_bytes() {
 // the ctx's copy stream; the decode waits for it through file_ev[slot].
 static kc_status file_upload(kc_ctx* c, int slot, const char* p, size_t n) {
     kc_status s;
-    if (!c->copy_stream) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-        for (auto& e : c->file_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if ((s = copy_stream_init(c))) return s;
+    if (c->file_stage[slot].bytes < n + 64) {
+        HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+        if ((s = ensure(c, c->file_stage[slot], n + 64))) return s;
     }
-    if ((s = ensure(c, c->file_stage[slot], n + 64))) return s;
+    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->stage_free[slot], 0));  // a chunk encode may still read it
     HIPCHK(c, hipMemcpyAsync(c->file_stage[slot].p, p, n, hipMemcpyHostToDevice, c->copy_stream));
     HIPCHK(c, hipEventRecord(c->file_ev[slot], c->copy_stream));
     return KC_OK;
@@ -1980,48 +2112,12 @@ static kc_status reduce_pack(kc_ctx* c, uint64_t out_cap, uint64_t n, int which,
     return KC_OK;
 }
 
-kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
-    if (!c) return KC_ERR_ARG;
-    if (c->finished) {
-        if (n_records) *n_records = c->n_records;
-        return KC_OK;
-    }
-    HIPCHK(c, hipSetDevice(c->cfg.device));
+// Table engine: the global table compacted, radix-sorted and packed into
+// fin_packed (key 0 first when present).
+static kc_status finish_table(kc_ctx* c, uint64_t* n_out) {
     kc_status s;
-    c->ckpt = false;
-    if ((s = pend_flush(c))) return s;
-    if ((s = sync_stats(c))) return s;
-    if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;
-    if (!c->dev_runs.empty()) {
-        // the rest of the records as the last run, then one merge of all runs
-        if ((s = cut_run(c))) return s;
-        std::vector<std::pair<const void*, uint64_t>> runs;
-        for (size_t r = 0; r < c->dev_runs.size(); r++) runs.push_back({c->dev_runs[r].p, c->dev_run_n[r]});
-        s = merge_runs_packed(c, runs);
-        release_dev_runs(c, false);
-        if (s) return s;
-        c->st.table_used = 0;
-        if (n_records) *n_records = c->n_records;
-        return KC_OK;
-    }
     const int W = c->W;
     uint64_t out_cap = c->stats_h[ST_CLAIMED] + 1;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if (c->part) {
-        uint64_t n = 0;
-        if ((s = finish_part(c, &n))) return s;
-        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        float tf = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&tf, c->ev0, c->ev1));
-        c->st.finish_ms += tf;
-        c->n_records = n;
-        c->finished = true;
-        c->st.table_used = c->stats_h[ST_CLAIMED];
-        c->st.output_records = n;
-        if (n_records) *n_records = n;
-        return KC_OK;
-    }
     for (int i = 0; i < 2; i++) {
         if ((s = ensure(c, c->fin_keys[i], (size_t)W * out_cap * 8)) || (s = ensure(c, c->fin_cnts[i], out_cap * 4)))
             return s;
@@ -2045,14 +2141,56 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
     HIPCHK(c, launch_pack(W, (uint64_t*)c->fin_keys[which].p, out_cap, (uint32_t*)c->fin_cnts[which].p, n,
                           c->fin_packed.p, c->stream));
+    *n_out = n;
+    return KC_OK;
+}
+
+kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
+    if (!c) return KC_ERR_ARG;
+    if (c->finished) {
+        if (n_records) *n_records = c->n_records;
+        return KC_OK;
+    }
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    kc_status s;
+    c->ckpt = false;
+    if ((s = pend_flush(c))) return s;
+    if ((s = sync_stats(c))) return s;
+    if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;
+    // the table run: the engines' records (or the global table) sorted into fin_packed
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    uint64_t n = 0;
+    if ((s = c->part ? finish_part(c, &n) : finish_table(c, &n))) return s;
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    float t = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-    c->st.finish_ms += t;
+    float tf = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&tf, c->ev0, c->ev1));
+    c->st.finish_ms += tf;
+    c->st.table_used = c->stats_h[ST_CLAIMED];
+    if (!c->dev_runs.empty()) {
+        // sorted runs in HBM (cut runs, spill runs): the table run joins them
+        // (taking over fin_packed's buffer), one merge of all
+        std::vector<std::pair<const void*, uint64_t>> runs;
+        for (size_t r = 0; r < c->dev_runs.size(); r++) runs.push_back({c->dev_runs[r].p, c->dev_run_n[r]});
+        DevBuf table_run;
+        if (n) {
+            table_run = c->fin_packed;
+            c->fin_packed = DevBuf();
+            if (!c->run_pool.empty()) {
+                c->fin_packed = c->run_pool.back();
+                c->run_pool.pop_back();
+            }
+            runs.push_back({table_run.p, n});
+        }
+        s = merge_runs_packed(c, runs);
+        if (table_run.p) c->run_pool.push_back(table_run);
+        release_dev_runs(c, false);
+        if (s) return s;
+        if (n_records) *n_records = c->n_records;
+        return KC_OK;
+    }
     c->n_records = n;
     c->finished = true;
-    c->st.table_used = c->stats_h[ST_CLAIMED];
     c->st.output_records = n;
     if (n_records) *n_records = n;
     return KC_OK;

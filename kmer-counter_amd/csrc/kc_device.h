@@ -143,7 +143,11 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
-                                hipStream_t s, bool distinct = false);
+                                hipStream_t s, bool distinct = false, const uint64_t* sub_starts = nullptr);
+// Starts of the 256 sub-buckets per region after a regional radix pass by key
+// bits 40..47 (rp_hist/rp_scatter over nreg regions): nreg * 256 + 1 entries
+hipError_t launch_sub_starts(const uint64_t* rstart, const uint64_t* tpre, const uint64_t* pos, uint32_t nreg,
+                             uint64_t n, uint64_t* sub, hipStream_t s);
 // Finish without a global sort (see kc_kernels.hip): lens_sorted[i] = len[order[i]];
 // seg_sort writes each descriptor's records sorted at out_off[i].
 hipError_t launch_desc_prep(const uint32_t* order, const uint32_t* len, uint64_t n, uint64_t* lens_sorted,
@@ -268,6 +272,12 @@ uint64_t* rp_digit_base(uint64_t* tmp, uint64_t ntiles);  // exclusive digit bas
 hipError_t launch_rp_hist(const uint8_t* digs, const uint64_t* w0, int shift, const uint64_t* rstart,
                           const uint64_t* tpre, int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos,
                           uint64_t* tmp, int grid, hipStream_t s);
+// MSD regional histogram: digit (w0[i] >> shift) & 255, runs placed inside
+// their region (regions stay in order, each sorted by the digit); cnt_t:
+// 256 * ntiles u32 scratch, pos: 256 * ntiles run starts
+hipError_t launch_rp_hist_regional(const uint64_t* w0, int shift, const uint64_t* rstart, const uint64_t* tpre,
+                                   int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos, uint32_t* cnt_t, int grid,
+                                   hipStream_t s);
 hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t istride, uint64_t* kout,
                              uint64_t ostride, const uint32_t* pin, uint32_t* pout, const uint64_t* rstart,
                              const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,
@@ -302,6 +312,10 @@ struct SynthArgs {
     int64_t Lmin = 0;  // variable read lengths in [Lmin, L] (0: fixed)
     int layout = 0;    // 1: concatenated sequences (reference chunk layout)
 };
+// Coverage sketch of encoded reads (kc_kernels.hip sketch_k): fingerprints of
+// ~1/256 of the group-aligned k-mers appended to out (cap), count in *counter
+hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, uint64_t* out,
+                         uint64_t cap, uint64_t* counter, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s);
 void synth_host(const SynthArgs& a, char* out);
 uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L, int layout);

@@ -1744,6 +1744,8 @@ struct BucketArgs {
     int skip;         // timing experiments only (KC_P5_SKIP): 1 = no LDS inserts
     int distinct;     // input where most keys are distinct (high cardinality): a bucket's
                       // first split m is taken from its key count (no aborted first pass)
+    const u64* sub_starts;  // pre-split buckets (high cardinality): 256 sub-buckets per bucket by key bits
+                            // 40..47, sub_starts[b * 256 + d] (2^24 + 1 entries); nullptr: plain buckets
 };
 
 // 48-bit slot fraction of a key for the P5 LDS table: multiply-shift (the
@@ -1902,16 +1904,47 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         const bool stop = *lnext != 0u;
         __syncthreads();
         if (stop) return;
-        const u64 lo = a.starts[b], hi = a.starts[b + 1];
+        // Pre-split buckets: runs of consecutive sub-buckets holding at most
+        // `per` keys are counted in one pass each (distinct <= keys: the
+        // table never fills, every key is read once); a sub-bucket with more
+        // keys is split by the bits below it (fshift = 40) as plain buckets
+        // are by the bits below the bucket (fshift = 48).
+        const u64 per = (u64)limit * 7 / 8;
+        u32 sb = 0;
+        bool once = false;
+        for (;;) {
+        u64 lo, hi;
+        u32 fshift = 48;
+        bool multi = false;
+        u64 dbase = (u64)b << 48;
+        if (a.sub_starts) {
+            if (sb >= 256u) break;
+            const u64* ss = a.sub_starts + (u64)b * 256u;
+            const u32 s0 = sb;
+            lo = ss[s0];
+            u32 e = s0 + 1;
+            while (e < 256u && ss[e + 1] - lo <= per) e++;
+            hi = ss[e];
+            sb = e;
+            multi = hi - lo <= per;
+            fshift = multi ? 48u : 40u;
+            dbase |= (u64)s0 << 40;
+            if (hi == lo) continue;
+        } else {
+            if (once) break;
+            once = true;
+            lo = a.starts[b];
+            hi = a.starts[b + 1];
+        }
+        const u64 FM = (1ull << fshift) - 1;
         u32 m = 1, sub = 0;
-        if (a.distinct) {
+        if (a.distinct && !multi) {
             // every key may be distinct: enough passes that each fills the
             // table to at most 7/8 of its abort limit
-            const u64 per = (u64)limit * 7 / 8;
             while (m < mmax && (u64)m * per < hi - lo) m *= 2;
         }
         while (sub < m) {
-            const bool last = m >= mmax;
+            const bool last = m >= mmax || multi;
             u64 scanned = 0;
             u32 qn = 0;  // entries in this wave's queue (wave-uniform)
             // slow path for the first c queued keys: full probing insert, fill
@@ -2000,7 +2033,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                 for (int u = 0; u < U; u++) {
                     const u64 gi = base + (u64)u * kBucketBlock + tid;
                     const bool want =
-                        live[u] && !a.skip && (u32)(((key[u][0] & M48) * (u64)m) >> 48) == sub;
+                        live[u] && !a.skip && (u32)(((key[u][0] & FM) * (u64)m) >> fshift) == sub;
                     bool found = false;
                     const u64 fr = slot_frac<W>(key[u]);
                     if constexpr (W == 1) {
@@ -2109,9 +2142,12 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                         // log2(m) bits equal sub: one key-ordered segment
                         const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
                         if (di < a.desc_cap) {
-                            a.desc_key[di] = ((u64)b << 48) | ((u64)sub << (48 - __builtin_ctz(m)));
+                            // segment: the keys of [dbase, ...) whose next log2(m)
+                            // bits below fshift equal sub; len | shared bits below
+                            // the 16-bit bucket << 24 (the segment sort's digit)
+                            a.desc_key[di] = dbase | ((u64)sub << (fshift - __builtin_ctz(m)));
                             a.desc_start[di] = rbase;
-                            a.desc_len[di] = total | ((u32)__builtin_ctz(m) << 24);  // len | log2(m) << 24
+                            a.desc_len[di] = total | ((48u - fshift + (u32)__builtin_ctz(m)) << 24);
                         }
                     }
                 }
@@ -2142,7 +2178,33 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             __syncthreads();
             ++sub;
         }
+        }
     }
+}
+
+// Sub-bucket starts of a pre-split partition: the regional radix pass over
+// the 65536 buckets (regions) by key bits 40..47 wrote digit d of region r at
+// pos[first tile of r][d], so sub-bucket r * 256 + d starts there (an empty
+// region's sub-buckets start at the region's start).
+__global__ __launch_bounds__(kBlock) void sub_starts_k(const u64* __restrict__ rstart, const u64* __restrict__ tpre,
+                                                       const u64* __restrict__ pos, u32 nreg, u64 n,
+                                                       u64* __restrict__ sub) {
+    const u64 total = (u64)nreg * 256u;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i <= total; i += (u64)gridDim.x * kBlock) {
+        if (i == total) {
+            sub[i] = n;
+            continue;
+        }
+        const u32 r = (u32)(i >> 8), d = (u32)(i & 255u);
+        sub[i] = tpre[r + 1] > tpre[r] ? pos[tpre[r] * 256u + d] : rstart[r];
+    }
+}
+
+hipError_t launch_sub_starts(const uint64_t* rstart, const uint64_t* tpre, const uint64_t* pos, uint32_t nreg,
+                             uint64_t n, uint64_t* sub, hipStream_t s) {
+    const u64 total = (u64)nreg * 256u + 1;
+    hipLaunchKernelGGL(sub_starts_k, dim3(grid_for(total)), dim3(kBlock), 0, s, rstart, tpre, pos, nreg, n, sub);
+    return hipGetLastError();
 }
 
 size_t bucket_lds_bytes(int W) {
@@ -2155,10 +2217,11 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
-                                hipStream_t s, bool distinct) {
+                                hipStream_t s, bool distinct, const uint64_t* sub_starts) {
     BucketArgs a;
     a.skip = experiment_knob("KC_P5_SKIP");
     a.distinct = distinct ? 1 : 0;
+    a.sub_starts = sub_starts;
     a.desc_key = desc_key;
     a.desc_start = desc_start;
     a.desc_len = desc_len;
@@ -3900,6 +3963,59 @@ hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, 
     if (n_rec == 0) return hipSuccess;
     hipLaunchKernelGGL(fq_validate_k, dim3(grid_for(n_rec)), dim3(kBlock), 0, s, seq_off, seq_end, n_rec, L, stats,
                        at_most ? 1 : 0);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Coverage sketch (engine choice): one k-mer per read and 16-base group, the
+// one starting at the group (aligned to the read, not to the genome), kept
+// when its hash falls in 1/256 of the hash space; its 56-bit fingerprint is
+// appended to `out`. Reads from a genome at coverage c repeat such a k-mer in
+// ~c/16 reads (a read starting at the same position mod 16), so the share of
+// distinct fingerprints estimates the coverage: iid reads ~1, cfg2's 30x
+// ~0.45. The k-mer's bases are taken from the 2-bit codes (first base
+// highest in each u32 of 16 bases); k-mers with a not-ACGT base are skipped.
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void sketch_k(const u32* __restrict__ codes, const unsigned short* __restrict__ inval,
+                                                  u64 n_reads, int G, int k, u64* __restrict__ out, u64 cap,
+                                                  u64* __restrict__ counter) {
+    const int ng = (k + 15) >> 4;  // groups a k-mer spans from a group start
+    const int per = G - ng + 1;    // aligned k-mers per read
+    const u64 total = per > 0 ? n_reads * (u64)per : 0;
+    for (u64 it = (u64)blockIdx.x * kBlock + threadIdx.x; it < total; it += (u64)gridDim.x * kBlock) {
+        const u64 r = it / (u64)per;
+        const int g = (int)(it - r * (u64)per);
+        const u64 base = r * (u64)G + (u64)g;
+        u64 h = 0x243f6a8885a308d3ull ^ (u64)k;
+        bool ok = true;
+        for (int j = 0; j < ng; j++) {
+            const int nb = min(16, k - 16 * j);  // bases of this group inside the k-mer
+            const u32 keep = nb == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb));
+            const unsigned short bad = (unsigned short)(inval[base + j] & (nb == 16 ? 0xffffu : ~(0xffffu >> nb)));
+            ok = ok && bad == 0;
+            h = mix64(h ^ (u64)(codes[base + j] & keep) ^ ((u64)j << 40));
+        }
+        const bool take = ok && (h & 255u) == 0;
+        const u64 m = __ballot(take);
+        if (!m) continue;
+        u64 at = 0;
+        const int lead = __ffsll((long long)m) - 1;
+        if (lane_id() == lead) at = atomicAdd((unsigned long long*)counter, (unsigned long long)__popcll(m));
+        at = __shfl(at, lead);
+        if (take) {
+            const u64 q = at + (u64)__popcll(m & lanemask_lt());
+            if (q < cap) out[q] = h >> 8;
+        }
+    }
+}
+
+hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, uint64_t* out,
+                         uint64_t cap, uint64_t* counter, hipStream_t s) {
+    const int G = groups_per_read(L);
+    const u64 total = n_reads * (u64)(G > 0 ? G : 1);
+    hipLaunchKernelGGL(sketch_k, dim3(grid_for(total)), dim3(kBlock), 0, s, codes, (const unsigned short*)inval,
+                       n_reads, G, k, out, cap, counter);
     return hipGetLastError();
 }
 

@@ -1787,6 +1787,49 @@ hipError_t launch_rp_hist(const uint8_t* digs, const uint64_t* w0, int shift, co
     return hipGetLastError();
 }
 
+// MSD form of the regional histogram: digit runs are placed inside their
+// region (region start + the region's smaller digits + the region's earlier
+// tiles), so a pass sorts every region by the digit and regions stay in
+// order (the rp_hist passes above are LSD: digit-major over all regions).
+// One 256-thread workgroup (one thread per digit) per region.
+__global__ __launch_bounds__(256) void rp_region_pos_k(const u32* __restrict__ cnt_t, const u64* __restrict__ rstart,
+                                                       const u64* __restrict__ tpre, u32 nreg, u64* __restrict__ pos) {
+    __shared__ u64 part[256];
+    const int d = threadIdx.x;
+    for (u32 r = blockIdx.x; r < nreg; r += gridDim.x) {
+        const u64 t0 = tpre[r], t1 = tpre[r + 1];
+        u64 sum = 0;
+        for (u64 t = t0; t < t1; t++) sum += cnt_t[t * 256 + d];
+        part[d] = sum;
+        __syncthreads();
+        // exclusive scan over the 256 digits (Hillis-Steele in LDS)
+        for (int o = 1; o < 256; o <<= 1) {
+            const u64 y = d >= o ? part[d - o] : 0ull;
+            __syncthreads();
+            part[d] += y;
+            __syncthreads();
+        }
+        u64 run = rstart[r] + part[d] - sum;
+        for (u64 t = t0; t < t1; t++) {
+            pos[t * 256 + d] = run;
+            run += cnt_t[t * 256 + d];
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_rp_hist_regional(const uint64_t* w0, int shift, const uint64_t* rstart, const uint64_t* tpre,
+                                   int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos, uint32_t* cnt_t, int grid,
+                                   hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    const int gu = (int)hmin(ntiles, (u64)grid * 4);
+    hipLaunchKernelGGL(rp_upsweep_k, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)nullptr, w0, shift, rstart,
+                       tpre, nreg, ntiles, tile, cnt_t);
+    hipLaunchKernelGGL(rp_region_pos_k, dim3((u32)hmin((u64)nreg, 65536)), dim3(256), 0, s, (const u32*)cnt_t, rstart,
+                       tpre, (u32)nreg, pos);
+    return hipGetLastError();
+}
+
 hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t istride, uint64_t* kout,
                              uint64_t ostride, const uint32_t* pin, uint32_t* pout, const uint64_t* rstart,
                              const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,

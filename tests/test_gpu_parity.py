@@ -471,6 +471,28 @@ def test_partition_subrange_passes(kca, orc, k, slots):
     assert st["spilled_kmers"] == 0 and st["table_used"] == 0
 
 
+@pytest.mark.parametrize("k", [31, 55, 100])
+def test_presplit_buckets_high_cardinality(kca, orc, monkeypatch, k):
+    """High cardinality on the key-prefix engine: after a batch whose keys
+    were mostly distinct, the next batches split every bucket once more by key
+    bits 40..47 (P3b, an MSD regional radix pass) and P5 counts runs of
+    consecutive sub-buckets in one pass each; the runs cut from the records
+    merge on the device. Same bytes as the oracle; the pass can be disabled
+    (KC_NO_P3B) with the same result."""
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    fq = kca.synth_fastq(30000, 150, seed=k + 3, n_rate=0.0005)
+    outs = []
+    for env in ((), ("KC_NO_P3B",)):
+        for v in env:
+            monkeypatch.setenv(v, "1")
+        with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=24 << 20, engine="partition") as ctx:
+            ctx.count_fastq(fq)
+            outs.append(ctx.records())
+            st = ctx.stats()
+        assert st["batches"] >= 3
+    assert outs[0] == outs[1] == orc.count_fastq(fq, k)
+
+
 def _u64_sortable(lo32, hi32):
     """(hi << 32 | lo) as int64 whose signed order is the unsigned order."""
     import torch
