@@ -617,7 +617,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             // fallback table or the spill, whose inserts are not idempotent).
             uint64_t lslots = (uint64_t)bucket_lds_slots(W);
             uint64_t bound = (uint64_t)nb * lslots;
-            if (bound > n) bound = n;
+            if (bound > n || c->hc_hint) bound = n;  // high cardinality: about one record per key
             const uint64_t rec0 = c->rec_n;
             const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
             const uint64_t desc0 = c->stats_h[ST_DESC_FILL];
@@ -1025,10 +1025,15 @@ static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t p
 // pre0 >= 0: the reads are pre-encoded in part_codes / part_inval from read pre0
 static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L,
                              int64_t pre0 = -1) {
-    if (c->skm && !c->skm_hc && !c->skm_force && !c->skm_checked && pre0 >= 0 && !getenv("KC_NO_SKETCH") &&
-        n_reads * (uint64_t)(L - c->k + 1) >= kSkmSampleMinKeys && skm_geometry((int)L, (int)c->k).ok) {
+    // the coverage sketch picks the engine (auto) or, for the partition engine,
+    // sets the high-cardinality hint before its first batch
+    const bool sketch_skm = c->skm && !c->skm_hc && !c->skm_force && skm_geometry((int)L, (int)c->k).ok;
+    const bool sketch_part = !c->skm && c->part && !c->hc_hint;
+    if ((sketch_skm || sketch_part) && !c->skm_checked && pre0 >= 0 && !getenv("KC_NO_SKETCH") &&
+        n_reads * (uint64_t)(L - c->k + 1) >= kSkmSampleMinKeys) {
         kc_status s = sketch_engine(c, n_reads, L, pre0);
         if (s) return s;
+        if (sketch_part) c->skm_checked = true;  // once per reset
     }
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
@@ -1901,11 +1906,22 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
             (s = ensure(c, c->desc_v2, ndesc * 4)) || (s = ensure(c, c->desc_lens, ndesc * 8)) ||
             (s = ensure(c, c->desc_offs, ndesc * 8)) || (s = ensure(c, c->rle_tmp, scan_tmp_elems(ndesc) * 8)))
             return s;
+        // KC_TRACE: each phase synchronised and timed
+        double tp = kc::trace_on() ? kc::now_s() : 0;
+        auto phase = [&](const char* what) {
+            if (!kc::trace_on()) return;
+            if (hipStreamSynchronize(c->stream) != hipSuccess) return;
+            const double t = kc::now_s();
+            kc::trace("finish_part_sorted %s: %.3f ms", what, (t - tp) * 1e3);
+            tp = t;
+        };
+        phase("buffers");
         HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, ndesc, c->stream));
         int which = 0;
         if ((s = sort_records(c, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_k2.p, (uint32_t*)c->desc_v.p,
                               (uint32_t*)c->desc_v2.p, ndesc, ndesc, &which, 1)))
             return s;
+        phase("descriptor sort");
         const uint32_t* order = (const uint32_t*)(which ? c->desc_v2.p : c->desc_v.p);
         HIPCHK(c, launch_desc_prep(order, (const uint32_t*)c->desc_len.p, ndesc, (uint64_t*)c->desc_lens.p,
                                    c->stream));
@@ -1918,10 +1934,13 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
         fb = (uint32_t*)c->desc_fb.p;
         // sorted straight into the packed output, after the key-0 record
         if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
+        phase("descriptor scan");
         HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, order, (const uint64_t*)c->desc_start.p,
                                   (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, k0 + off0,
                                   c0 + off0, out_cap, c->stats, fb, fb_n, c->n_cu, c->stream,
-                                  (char*)c->fin_packed.p + off0 * c->rs));
+                                  (char*)c->fin_packed.p + off0 * c->rs,
+                                  (const uint64_t*)(which ? c->desc_k2.p : c->desc_key.p)));
+        phase("segment sort");
     }
     if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
     // record 0: key 0^W (all-zero words) and its count (kept alive until the
@@ -1995,7 +2014,8 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
             (s = ensure(c, c->desc_fb, (size_t)nb * 4 + 16)))
             return s;
         std::vector<uint32_t> lens(nb);
-        for (uint32_t b = 0; b < nb; b++) lens[b] = (uint32_t)(st[b + 1] - st[b]);  // log2(m) = 0: 16-bit prefix
+        // digit: word0 bits 36..47 (the 12 bits below the 16-bit group prefix)
+        for (uint32_t b = 0; b < nb; b++) lens[b] = (uint32_t)(st[b + 1] - st[b]) | (36u << 24);
         HIPCHK(c, hipMemcpyAsync(c->desc_len.p, lens.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, nb, c->stream));
         uint64_t* fb_n = (uint64_t*)((char*)c->desc_fb.p + (size_t)nb * 4);
@@ -2033,6 +2053,9 @@ static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
     const uint64_t nrec = c->rec_n;
     const uint64_t claimed = c->stats_h[ST_CLAIMED];
     const uint64_t ndesc = c->stats_h[ST_DESC_FILL];
+    kc::trace("finish_part: %llu records, %llu batches, %llu claimed, %zu host runs, %llu descriptors",
+              (unsigned long long)nrec, (unsigned long long)c->batches, (unsigned long long)claimed, c->runs.size(),
+              (unsigned long long)ndesc);
     if (c->batches <= 1 && claimed == 0 && c->runs.empty() && ndesc <= kDescCap && !getenv("KC_NO_SEGSORT"))
         return finish_part_sorted(c, ndesc, n_out);
     const uint64_t out_cap = nrec + claimed + 1;
@@ -2182,7 +2205,9 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
             }
             runs.push_back({table_run.p, n});
         }
+        const double tm = kc::trace_on() ? kc::now_s() : 0;
         s = merge_runs_packed(c, runs);
+        kc::trace("merge of %zu runs: %.3f ms", runs.size(), (kc::now_s() - tm) * 1e3);
         if (table_run.p) c->run_pool.push_back(table_run);
         release_dev_runs(c, false);
         if (s) return s;
@@ -2632,8 +2657,10 @@ static kc_status cut_run(kc_ctx* c) {
     kc_status s;
     if ((s = sync_stats(c))) return s;
     uint64_t n = 0;
+    const double t0 = kc::trace_on() ? kc::now_s() : 0;
     if ((s = finish_part(c, &n))) return s;  // fin_packed
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    kc::trace("cut_run: %llu records finished in %.3f ms", (unsigned long long)n, (kc::now_s() - t0) * 1e3);
     const size_t bytes = (size_t)n * c->rs;
     if (n) {
         // the run takes over fin_packed's buffer (no copy); fin_packed gets a

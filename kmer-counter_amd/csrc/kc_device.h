@@ -160,7 +160,8 @@ hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s);
 hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, uint64_t rstride, const uint32_t* order,
                            const uint64_t* dstart, const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc,
                            uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, uint32_t* fb,
-                           uint64_t* fb_n, int grid, hipStream_t s, void* packed = nullptr);
+                           uint64_t* fb_n, int grid, hipStream_t s, void* packed,
+                           const uint64_t* dkey = nullptr);
 // segmented sum of sorted records (out_cnts zeroed by the caller)
 hipError_t launch_reduce_add(int W, const uint64_t* keys, uint64_t stride, const uint32_t* cnts, uint64_t n,
                              const uint32_t* flags, const uint32_t* pos, uint64_t* out_keys, uint64_t ostride,

@@ -1893,7 +1893,6 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
     __syncthreads();
     const u32 limit = (a.lcap * 13u) >> 4;
     const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;  // tiny test tables: global fallback only
-    constexpr u64 M48 = 0xffffffffffffull;
     for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         // a full record buffer ends the launch early (the host reruns P5)
         if (tid == 0)
@@ -1916,6 +1915,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         u64 lo, hi;
         u32 fshift = 48;
         bool multi = false;
+        u32 nsub_l2 = 0;  // multi: ceil(log2(sub-buckets in the run))
         u64 dbase = (u64)b << 48;
         if (a.sub_starts) {
             if (sb >= 256u) break;
@@ -1928,6 +1928,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             sb = e;
             multi = hi - lo <= per;
             fshift = multi ? 48u : 40u;
+            while ((1u << nsub_l2) < e - s0) nsub_l2++;
             dbase |= (u64)s0 << 40;
             if (hi == lo) continue;
         } else {
@@ -2036,7 +2037,13 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                         live[u] && !a.skip && (u32)(((key[u][0] & FM) * (u64)m) >> fshift) == sub;
                     bool found = false;
                     const u64 fr = slot_frac<W>(key[u]);
-                    if constexpr (W == 1) {
+                    if (multi) {
+                        // a run of sub-buckets (<= per keys, mostly distinct):
+                        // insert in place with full probing; the queue keeps
+                        // only what misses the table (none while keys <= per)
+                        bool lclaim = false;
+                        found = want && lds_insert<W>(key[u], fr, lkeys, lcnt, lstate, a.lcap, a.lcap, &lclaim);
+                    } else if constexpr (W == 1) {
                         if ((a.lcap & 3u) == 0) {
                             const u32 g = (u32)((fr * (u64)(a.lcap >> 2)) >> 48);
                             const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
@@ -2143,11 +2150,14 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                         const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
                         if (di < a.desc_cap) {
                             // segment: the keys of [dbase, ...) whose next log2(m)
-                            // bits below fshift equal sub; len | shared bits below
-                            // the 16-bit bucket << 24 (the segment sort's digit)
+                            // bits below fshift equal sub (a run of sub-buckets:
+                            // [dbase, dbase + run << 40)); len | the segment
+                            // sort's digit shift << 24: digit = (key bits below
+                            // 48 - the descriptor's) >> shift spans the 4096 bins
                             a.desc_key[di] = dbase | ((u64)sub << (fshift - __builtin_ctz(m)));
                             a.desc_start[di] = rbase;
-                            a.desc_len[di] = total | ((48u - fshift + (u32)__builtin_ctz(m)) << 24);
+                            const u32 dsh = multi ? 28u + nsub_l2 : fshift - 12u - (u32)__builtin_ctz(m);
+                            a.desc_len[di] = total | (dsh << 24);
                         }
                     }
                 }
@@ -2653,6 +2663,12 @@ __device__ __forceinline__ void seg_put(u64* __restrict__ okeys, u32* __restrict
     }
 }
 
+constexpr u64 kM48 = 0xffffffffffffull;
+
+__device__ __forceinline__ u32 seg_digit(u64 w0, u64 base, int sh) {
+    return (u32)(((w0 & kM48) - base) >> sh) & 4095u;
+}
+
 // MSD segment sort: the bits just below the bucket prefix and the pass's
 // sub-range bits (known from the descriptor) give a 12-bit digit; a counting
 // pass and a scatter pass stream the segment from global memory (L2-resident
@@ -2667,7 +2683,8 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
                                                         u64* __restrict__ okeys, u32* __restrict__ ocnts,
                                                         u64 ostride, u32* __restrict__ packed,
                                                         u64* __restrict__ stats, u32* __restrict__ fb,
-                                                        u64* __restrict__ fb_n, int skip) {
+                                                        u64* __restrict__ fb_n, int skip,
+                                                        const u64* __restrict__ dkey) {
     constexpr int CAP = SegCfg<W>::CAP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* skey = (u64*)smem;                      // W x CAP
@@ -2707,9 +2724,11 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         const u64 st = dstart[o];
         const u32 lw = dlen[o];
         const u32 len = lw & 0xffffffu;
-        const int l2m = (int)(lw >> 24);
         const u64 obase = out_off[di];
-        const int sh = 36 - l2m;  // digit = word0 bits [sh, sh + 12)
+        // digit = ((word0 & M48) - base) >> sh: the segment's key range over
+        // the 4096 bins (base: the sorted descriptor key's bits below 48)
+        const int sh = (int)(lw >> 24);
+        const u64 dbase = dkey ? (dkey[di] & kM48) : 0ull;
         u64 ck[PI][W];
         u32 cc[PI];
 #pragma unroll
@@ -2729,9 +2748,9 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         }
 #pragma unroll
         for (int i = 0; i < PI; i++)
-            if ((u32)tid + (u32)i * kSegBlock < len) atomicAdd(&bcnt[(u32)(ck[i][0] >> sh) & 4095u], 1u);
+            if ((u32)tid + (u32)i * kSegBlock < len) atomicAdd(&bcnt[seg_digit(ck[i][0], dbase, sh)], 1u);
         for (u32 p = tid + PI * kSegBlock; p < len; p += kSegBlock)
-            atomicAdd(&bcnt[(u32)(rkeys[st + p] >> sh) & 4095u], 1u);
+            atomicAdd(&bcnt[seg_digit(rkeys[st + p], dbase, sh)], 1u);
         __syncthreads();
         // bin starts: 4 bins per thread, block-wide exclusive scan; skew check
         const u32 c0 = bcnt[4 * tid], c1 = bcnt[4 * tid + 1], c2 = bcnt[4 * tid + 2], c3 = bcnt[4 * tid + 3];
@@ -2765,7 +2784,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
 #pragma unroll
         for (int i = 0; i < PI; i++) {
             if ((u32)tid + (u32)i * kSegBlock >= len) continue;
-            const u32 q = atomicAdd(&bcnt[(u32)(ck[i][0] >> sh) & 4095u], 1u);
+            const u32 q = atomicAdd(&bcnt[seg_digit(ck[i][0], dbase, sh)], 1u);
 #pragma unroll
             for (int j = 0; j < W; j++) skey[(size_t)j * CAP + q] = ck[i][j];
             scnt[q] = cc[i];
@@ -2774,7 +2793,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             u64 k[W];
 #pragma unroll
             for (int j = 0; j < W; j++) k[j] = rkeys[(u64)j * rstride + st + p];
-            const u32 q = atomicAdd(&bcnt[(u32)(k[0] >> sh) & 4095u], 1u);
+            const u32 q = atomicAdd(&bcnt[seg_digit(k[0], dbase, sh)], 1u);
 #pragma unroll
             for (int j = 0; j < W; j++) skey[(size_t)j * CAP + q] = k[j];
             scnt[q] = rcnts[st + p];
@@ -2787,7 +2806,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             // is its place: written straight there
             for (u32 p = tid; p < ((skip & 1) ? 0u : len); p += kSegBlock) {
                 const u64 kp = skey[p];
-                const u32 d = (u32)(kp >> sh) & 4095u;
+                const u32 d = seg_digit(kp, dbase, sh);
                 const u32 b0 = d ? bcnt[d - 1] : 0u, b1 = bcnt[d];
                 u32 r = 0;
                 for (u32 q = b0; q < ((skip & 2) ? b0 : b1); q++) {
@@ -3025,7 +3044,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_lsd_k(const u64* __restric
 hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, uint64_t rstride, const uint32_t* order,
                            const uint64_t* dstart, const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc,
                            uint64_t* okeys, uint32_t* ocnts, uint64_t ostride, uint64_t* stats, uint32_t* fb,
-                           uint64_t* fb_n, int grid, hipStream_t s, void* packed) {
+                           uint64_t* fb_n, int grid, hipStream_t s, void* packed, const uint64_t* dkey) {
     if (ndesc == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(fb_n, 0, 8, s);
     if (e != hipSuccess) return e;
@@ -3034,7 +3053,8 @@ hipError_t launch_seg_sort(int W, const uint64_t* rkeys, const uint32_t* rcnts, 
     const int skip = experiment_knob("KC_SEG_SKIP");  // 1 output stores, 2 insertion sort
 #define KC_SEG(WW)                                                                                                  \
     hipLaunchKernelGGL(seg_sort_k<WW>, dim3(grid), dim3(kSegBlock), lds_msd, s, rkeys, rcnts, rstride, order,       \
-                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, fb, fb_n, skip); \
+                       dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, fb, fb_n, skip,  \
+                       dkey);                                                                                      \
     hipLaunchKernelGGL(seg_sort_lsd_k<WW>, dim3(grid), dim3(kSegBlock), lds, s, rkeys, rcnts, rstride, order,       \
                        dstart, dlen, out_off, ndesc, okeys, ocnts, ostride, (u32*)packed, stats, (const u32*)fb,   \
                        (const u64*)fb_n)
@@ -3291,8 +3311,26 @@ __global__ __launch_bounds__(kBlock) void merge_tile_packed_k(const u32* __restr
         const u64 i0 = split[t], i1 = split[t + 1];
         const u64 j0 = d0 - i0, j1 = d1 - i1;
         const u32 la = (u32)(i1 - i0), lb = (u32)(j1 - j0), n = la + lb;
-        for (u32 x = tid; x < la * RW; x += kBlock) sin[x] = __builtin_nontemporal_load(A + i0 * RW + x);
-        for (u32 x = tid; x < lb * RW; x += kBlock) sin[la * RW + x] = __builtin_nontemporal_load(B + j0 * RW + x);
+        {
+            // A slice then B slice, LB independent loads in flight per thread
+            constexpr int LB = 10;
+            const u32 ea = la * RW, tot = n * RW;
+            const u32* pa = A + i0 * RW;
+            const u32* pb = B + j0 * RW;
+            for (u32 x0 = 0; x0 < tot; x0 += kBlock * LB) {
+                u32 v[LB];
+#pragma unroll
+                for (int u = 0; u < LB; u++) {
+                    const u32 x = x0 + (u32)u * kBlock + (u32)tid;
+                    v[u] = x < tot ? __builtin_nontemporal_load(x < ea ? pa + x : pb + (x - ea)) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < LB; u++) {
+                    const u32 x = x0 + (u32)u * kBlock + (u32)tid;
+                    if (x < tot) sin[x] = v[u];
+                }
+            }
+        }
         __syncthreads();
         const u32 dl = min((u32)tid * ITEMS, n);
         u32 lo = dl > lb ? dl - lb : 0, hi = dl < la ? dl : la;
