@@ -80,6 +80,7 @@ struct kc_ctx {
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
     DevBuf part_dedup;  // skm P5a: per-bucket list starts (u64) and lengths (u32), list cursor
     DevBuf p3b_buf, sub_starts;  // key-prefix engine, high cardinality: P3b tile positions, sub-bucket starts
+    DevBuf run_flags;            //   P5s: runs left to the LDS hash path
     DevBuf part_codes, part_inval;  // kernel E output: the batch's reads, 2-bit encoded
     DevBuf part_rlen;               // KC_FLAG_VARLEN: each read's own length (u16)
     const uint16_t* var_rlen = nullptr;  // set while a variable-length block is counted
@@ -624,7 +625,47 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             if ((s = ensure(c, c->desc_key, kDescCap * 8)) || (s = ensure(c, c->desc_start, kDescCap * 8)) ||
                 (s = ensure(c, c->desc_len, kDescCap * 4)))
                 return s;
-            for (;;) {
+            // P5s: pre-split runs sorted in LDS (records <= keys, no overflow);
+            // the runs it flags (a sub-bucket too big, clustered keys) take
+            // the LDS hash table (KC_NO_SORT_RUNS: hash table for all runs)
+            const bool sort_runs = sub_starts && !getenv("KC_NO_SORT_RUNS");
+            if (sort_runs) {
+                if ((s = grow_records(c, rec0 + n))) return s;
+                const size_t fl = ((size_t)nb << 8) + nb + 16;
+                if ((s = ensure(c, c->run_flags, fl))) return s;
+                uint8_t* rf = (uint8_t*)c->run_flags.p;
+                uint8_t* bf = rf + ((size_t)nb << 8);
+                uint32_t* nflag = (uint32_t*)(bf + nb);
+                HIPCHK(c, hipMemsetAsync(rf, 0, fl, c->stream));
+                HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                HIPCHK(c, launch_sort_runs(W, p5_keys, c->key_cap, sub_starts, nb, c->rec_keys, c->rec_cnts,
+                                           c->rec_cap, c->rec_cursor, c->stats, (uint64_t*)c->desc_key.p,
+                                           (uint64_t*)c->desc_start.p, (uint32_t*)c->desc_len.p, kDescCap, rf, bf,
+                                           nflag, 2 * c->n_cu, c->stream));
+                uint32_t nf = 0;
+                HIPCHK(c, hipMemcpyAsync(&nf, nflag, 4, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                if (nf)
+                    HIPCHK(c, launch_count_buckets(W, p5_keys, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
+                                                   c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table,
+                                                   c->cap, p5_spill, c->key_cap, c->stats, l.probe_limit,
+                                                   c->cfg.lds_slots, c->n_cu, (uint64_t*)c->desc_key.p,
+                                                   (uint64_t*)c->desc_start.p, (uint32_t*)c->desc_len.p, kDescCap,
+                                                   c->stream, true, sub_starts, rf, bf,
+                                                   (uint32_t)sort_runs_keys(W)));
+                HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+                if ((s = sync_stats(c))) return s;
+                HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                c->part_ms[4] += t;
+                c->p5_launches++;
+                if (getenv("KC_DEBUG"))
+                    fprintf(stderr, "kc: P5s n=%llu runs=%llu flagged=%u records=%llu %.3f ms\n",
+                            (unsigned long long)n, (unsigned long long)c->stats_h[ST_P5_PASSES], nf,
+                            (unsigned long long)c->rec_n, t);
+                if (c->stats_h[ST_ERR] & ERR_REC_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
+            }
+            for (; !sort_runs;) {
                 if ((s = grow_records(c, rec0 + bound))) return s;
                 // keys_a is free after P3: it takes P5's spills (capacity >= n)
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -982,7 +1023,11 @@ static const double kSketchDistinctMax = 0.7;
 static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre0) {
     kc_status s;
     const uint64_t G = (uint64_t)groups_per_read((int)L);
-    const uint64_t cap = n_reads * G / 128 + 1024;  // ~1/256 of the aligned k-mers are kept
+    // sample rate 2^-rb by k-mer hash: about 2^18 samples (at least 1/256)
+    const uint64_t aligned = n_reads * G;
+    int rb = 8;
+    while (rb < 24 && (aligned >> rb) > (1ull << 18)) rb++;
+    const uint64_t cap = (aligned >> rb) * 2 + 4096;  // twice the expected samples
     if ((s = ensure(c, c->fin_keys[0], cap * 8 + 64)) || (s = ensure(c, c->fin_keys[1], cap * 8 + 64)) ||
         (s = ensure(c, c->fin_misc, 64)))
         return s;
@@ -990,8 +1035,8 @@ static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t p
     uint64_t* counter = (uint64_t*)c->fin_misc.p;
     HIPCHK(c, hipMemsetAsync(counter, 0, 8, c->stream));
     HIPCHK(c, launch_sketch((const uint32_t*)c->part_codes.p + (uint64_t)pre0 * G,
-                            (const uint16_t*)c->part_inval.p + (uint64_t)pre0 * G, n_reads, (int)L, (int)c->k, fp, cap,
-                            counter, c->stream));
+                            (const uint16_t*)c->part_inval.p + (uint64_t)pre0 * G, n_reads, (int)L, (int)c->k, rb, fp,
+                            cap, counter, c->stream));
     uint64_t m = 0;
     HIPCHK(c, hipMemcpyAsync(&m, counter, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1445,6 +1490,7 @@ void kc_destroy(kc_ctx* c) {
     if (c->pool_cursor) (void)hipFree(c->pool_cursor);
     release(c->part_hist);
     release(c->p3b_buf);
+    release(c->run_flags);
     release(c->sub_starts);
     release(c->part_codes);
     release(c->part_inval);

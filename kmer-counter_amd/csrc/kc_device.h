@@ -143,7 +143,19 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
-                                hipStream_t s, bool distinct = false, const uint64_t* sub_starts = nullptr);
+                                hipStream_t s, bool distinct = false, const uint64_t* sub_starts = nullptr,
+                                const uint8_t* run_flags = nullptr, const uint8_t* bucket_flags = nullptr,
+                                uint32_t run_per = 0);
+// P5s (pre-split buckets): runs of sub-buckets of at most sort_runs_keys(W)
+// keys sorted in LDS into key-ordered record segments (descriptor bit 31 set);
+// runs it cannot take are flagged (run_flags[b * 256 + s0], bucket_flags[b],
+// *nflag) for launch_count_buckets with the same flags and run_per.
+int sort_runs_keys(int W);
+hipError_t launch_sort_runs(int W, const uint64_t* keys, uint64_t stride, const uint64_t* sub_starts,
+                            uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                            uint64_t* rec_cursor, uint64_t* stats, uint64_t* desc_key, uint64_t* desc_start,
+                            uint32_t* desc_len, uint64_t desc_cap, uint8_t* run_flags, uint8_t* bucket_flags,
+                            uint32_t* nflag, int grid, hipStream_t s);
 // Starts of the 256 sub-buckets per region after a regional radix pass by key
 // bits 40..47 (rp_hist/rp_scatter over nreg regions): nreg * 256 + 1 entries
 hipError_t launch_sub_starts(const uint64_t* rstart, const uint64_t* tpre, const uint64_t* pos, uint32_t nreg,
@@ -314,9 +326,11 @@ struct SynthArgs {
     int layout = 0;    // 1: concatenated sequences (reference chunk layout)
 };
 // Coverage sketch of encoded reads (kc_kernels.hip sketch_k): fingerprints of
-// ~1/256 of the group-aligned k-mers appended to out (cap), count in *counter
-hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, uint64_t* out,
-                         uint64_t cap, uint64_t* counter, hipStream_t s);
+// the group-aligned k-mers whose hash has rate_bits low zero bits (a 2^-rate
+// sample by k-mer, so every copy of a sampled k-mer is kept) appended to out
+// (cap), count in *counter
+hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, int rate_bits,
+                         uint64_t* out, uint64_t cap, uint64_t* counter, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s);
 void synth_host(const SynthArgs& a, char* out);
 uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L, int layout);

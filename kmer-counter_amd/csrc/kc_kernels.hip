@@ -37,6 +37,19 @@ __device__ __forceinline__ u32 lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ u64 lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
+// Block-uniform values read from LDS, made scalar so the branches (and the
+// barriers under them) are uniform to the compiler as well.
+__device__ __forceinline__ u32 uni32(u32 v) { return __builtin_amdgcn_readfirstlane(v); }
+// v <= lim for a 64-bit uniform v as two 32-bit compares: hipcc (ROCm 7.2)
+// lowers a uniform 64-bit unsigned compare to a VALU compare in VCC and can
+// then select on SCC (a stale carry) — seen in sort_runs_k's run length
+__device__ __forceinline__ bool le64_32(u64 v, u32 lim) { return (u32)(v >> 32) == 0u && (u32)v <= lim; }
+__device__ __forceinline__ u64 uni64(u64 v) {
+    return ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(v >> 32)) << 32) |
+           (u64)(u32)__builtin_amdgcn_readfirstlane((u32)v);
+}
+
+
 // Wave-aggregated atomicAdd of `mine` (per lane) to *ctr; returns this lane's
 // exclusive position (ctr_old + prefix of lower active lanes).
 __device__ __forceinline__ u64 wave_reserve(u64* ctr, bool want) {
@@ -1272,11 +1285,10 @@ __global__ __launch_bounds__(kBlock) void sort_downsweep(const u64* __restrict__
         const u64 q0 = t0 + (u64)wave * (64 * ITEMS) + lane;
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
-            u64 i = q0 + (u64)it * 64;
-            bool ok = i < hi;
+            const u64 i = min(q0 + (u64)it * 64, hi - 1);  // unconditional loads (clamped)
 #pragma unroll
-            for (int j = 0; j < W; j++) kreg[it][j] = ok ? kin[(u64)j * stride + i] : 0ull;
-            if constexpr (HAS_VALS) vreg[it] = ok ? vin[i] : 0u;
+            for (int j = 0; j < W; j++) kreg[it][j] = kin[(u64)j * stride + i];
+            if constexpr (HAS_VALS) vreg[it] = vin[i];
         }
 #pragma unroll
         for (int it = 0; it < ITEMS; it++) {
@@ -1746,6 +1758,9 @@ struct BucketArgs {
                       // first split m is taken from its key count (no aborted first pass)
     const u64* sub_starts;  // pre-split buckets (high cardinality): 256 sub-buckets per bucket by key bits
                             // 40..47, sub_starts[b * 256 + d] (2^24 + 1 entries); nullptr: plain buckets
+    const unsigned char* run_flags;     // pre-split, after sort_runs_k: only the runs it flagged
+    const unsigned char* bucket_flags;  //   (run_flags[b * 256 + first sub-bucket], bucket_flags[b])
+    u32 run_per;                        //   packed with sort_runs_k's run size (0: the table's)
 };
 
 // 48-bit slot fraction of a key for the P5 LDS table: multiply-shift (the
@@ -1894,13 +1909,14 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
     const u32 limit = (a.lcap * 13u) >> 4;
     const u32 mmax = a.lcap >= 64 ? kMaxSub : 1u;  // tiny test tables: global fallback only
     for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        if (a.bucket_flags && !a.bucket_flags[b]) continue;  // block-uniform
         // a full record buffer ends the launch early (the host reruns P5)
         if (tid == 0)
             *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT) &
                            ERR_REC_OVERFLOW);
         __syncthreads();
-        const bool stop = *lnext != 0u;
+        const bool stop = uni32(*lnext) != 0u;
         __syncthreads();
         if (stop) return;
         // Pre-split buckets: runs of consecutive sub-buckets holding at most
@@ -1908,7 +1924,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
         // table never fills, every key is read once); a sub-bucket with more
         // keys is split by the bits below it (fshift = 40) as plain buckets
         // are by the bits below the bucket (fshift = 48).
-        const u64 per = (u64)limit * 7 / 8;
+        const u64 per = a.run_per ? (u64)a.run_per : (u64)limit * 7 / 8;
         u32 sb = 0;
         bool once = false;
         for (;;) {
@@ -1931,11 +1947,13 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             while ((1u << nsub_l2) < e - s0) nsub_l2++;
             dbase |= (u64)s0 << 40;
             if (hi == lo) continue;
+            if (a.run_flags && !a.run_flags[(u64)b * 256u + s0]) continue;  // sorted by sort_runs_k
         } else {
             if (once) break;
             once = true;
             lo = a.starts[b];
             hi = a.starts[b + 1];
+            if (hi == lo) continue;
         }
         const u64 FM = (1ull << fshift) - 1;
         u32 m = 1, sub = 0;
@@ -2005,7 +2023,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             for (int u = 0; u < U; u++) {
                 const u64 i = lo + (u64)u * kBucketBlock + tid;
 #pragma unroll
-                for (int j = 0; j < W; j++) nkey[u][j] = i < hi ? a.keys[(u64)j * a.stride + i] : 0ull;
+                for (int j = 0; j < W; j++) nkey[u][j] = a.keys[(u64)j * a.stride + min(i, hi - 1)];
             }
             for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
                 if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
@@ -2024,7 +2042,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                 for (int u = 0; u < U; u++) {
                     const u64 i = nbase + (u64)u * kBucketBlock + tid;
 #pragma unroll
-                    for (int j = 0; j < W; j++) nkey[u][j] = i < hi ? a.keys[(u64)j * a.stride + i] : 0ull;
+                    for (int j = 0; j < W; j++) nkey[u][j] = a.keys[(u64)j * a.stride + min(i, hi - 1)];
                 }
                 // fast path, branch-light: a key already in its home group (W=1)
                 // or home slot (W>=2) is counted in place; every other wanted
@@ -2087,7 +2105,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
             // leftovers (an aborted pass is restarted from scratch instead)
             if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) drain(qn);
             __syncthreads();
-            const bool aborted = *labort != 0u;  // every thread reads before tid 0 resets it
+            const bool aborted = uni32(*labort) != 0u;  // every thread reads before tid 0 resets it
             __syncthreads();
             if (aborted) {
                 // finer split: m' = m * 2^s from the fill rate seen so far
@@ -2108,7 +2126,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     if constexpr (W >= 2) lstate[i] = 0;
                 }
                 __syncthreads();
-                const u32 nm = *lnext;
+                const u32 nm = uni32(*lnext);
                 sub *= nm / m;
                 m = nm;
                 __syncthreads();
@@ -2217,6 +2235,384 @@ hipError_t launch_sub_starts(const uint64_t* rstart, const uint64_t* tpre, const
     return hipGetLastError();
 }
 
+// P5s — pre-split buckets (high cardinality, after P3b): every run of
+// consecutive sub-buckets holding at most SP keys is sorted in LDS and
+// run-length encoded into sorted (key, count) records, one key-ordered segment
+// per run (its descriptor flagged sorted: the finish copies it instead of
+// sorting). The keys of a run lie in [b << 48 | s0 << 40, + (e - s0) << 40):
+// an 11-bit digit over that span bins them (a counting pass and a scatter
+// into LDS), each thread insertion-sorts its 2 bins, equal keys end up
+// adjacent. A run holding one sub-bucket of more than SP keys, or a bin of
+// more than kMaxSortBin keys (clustered keys), is flagged for the LDS hash
+// table path (count_buckets over the flagged runs only).
+constexpr int kSrBlock = 1024;
+constexpr int kSrWaves = kSrBlock / 64;
+constexpr u32 kSrBins = 2048;
+constexpr u32 kMaxSortBin = 48;
+
+template <int W>
+struct SortRunCfg {
+    static constexpr int SP = W == 1 ? 8192 : (W == 2 ? 4096 : (W == 3 ? 2688 : 2048));  // keys per run
+    static constexpr int R = (SP + kSrBlock - 1) / kSrBlock;                             // keys per thread
+};
+
+int sort_runs_keys(int W) { return W == 1 ? 8192 : (W == 2 ? 4096 : (W == 3 ? 2688 : 2048)); }
+
+size_t sort_runs_lds(int W) {
+    return (size_t)sort_runs_keys(W) * 8 * W + kSrBins * 4 + 64 * 4 + 257 * 8;
+}
+
+struct SortRunArgs {
+    const u64* keys;
+    u64 stride;
+    const u64* sub_starts;  // 256 per bucket + 1
+    u32 nbuckets;
+    u64* rec_keys;
+    u32* rec_cnts;
+    u64 rec_cap;
+    u64* rec_cursor;
+    u64* stats;
+    u64* desc_key;
+    u64* desc_start;
+    u32* desc_len;
+    u64 desc_cap;
+    unsigned char* run_flags;     // nbuckets * 256
+    unsigned char* bucket_flags;  // nbuckets
+    u32* nflag;                   // runs flagged
+};
+
+template <int W>
+__global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
+    constexpr int SP = SortRunCfg<W>::SP;
+    constexpr int R = SortRunCfg<W>::R;
+    constexpr u64 M48 = 0xffffffffffffull;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64* skey = (u64*)smem;                      // W x SP
+    u32* bins = (u32*)(skey + (size_t)W * SP);   // kSrBins
+    u32* misc = bins + kSrBins;                  // [0] flag, [1..16] wave sums, [20..21] record base
+    u64* ss = (u64*)(misc + 64);                 // the bucket's 257 sub-bucket starts
+    const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
+#ifdef KC_EXPERIMENTS
+    // KC_EXPERIMENTS builds: block 0 prints its cycles per phase at the end
+    u64 ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    u64 tl = wall_clock64();
+#define SR_MARK(i)                         \
+    do {                                   \
+        const u64 tn = wall_clock64();     \
+        ph[i] += tn - tl;                  \
+        tl = tn;                           \
+    } while (0)
+#else
+#define SR_MARK(i) \
+    do {           \
+    } while (0)
+#endif
+    for (u32 b = blockIdx.x; b < a.nbuckets; b += gridDim.x) {
+        __syncthreads();
+        if (tid <= 256) ss[tid] = a.sub_starts[(u64)b * 256u + tid];
+        __syncthreads();
+        u32 sb = 0;
+        while (sb < 256u) {
+            const u32 s0 = sb;
+            const u64 lo = uni64(ss[s0]);
+            // run end: the last e in [s0 + 1, 256] with ss[e] - lo <= SP (at
+            // least s0 + 1) — count_buckets' greedy walk, by bisection
+            u32 e = s0 + 1;
+            {
+                u32 eh = 256u;
+                while (e < eh) {
+                    const u32 mid = (e + eh + 1) >> 1;
+                    if (le64_32(uni64(ss[mid]) - lo, (u32)SP))
+                        e = mid;
+                    else
+                        eh = mid - 1;
+                }
+            }
+            const u64 hi = uni64(ss[e]);
+            sb = e;
+            const u32 len = le64_32(hi - lo, (u32)SP) ? (u32)(hi - lo) : (u32)SP + 1u;
+            SR_MARK(0);
+            if (len == 0) continue;
+            if (len > (u32)SP) {  // one sub-bucket of more than SP keys: hash path
+                if (tid == 0) {
+                    a.run_flags[(u64)b * 256u + s0] = 1;
+                    a.bucket_flags[b] = 1;
+                    atomicAdd(a.nflag, 1u);
+                }
+                continue;
+            }
+            // keys p = tid + i * kSrBlock (coalesced); positions past the run
+            // load its last key (unconditional loads: no per-element waits)
+            u64 k[R][W];
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const u32 p = min((u32)tid + (u32)i * kSrBlock, len - 1);
+#pragma unroll
+                for (int j = 0; j < W; j++) k[i][j] = a.keys[(u64)j * a.stride + lo + p];
+            }
+            u32 l2 = 0;
+            while ((1u << l2) < e - s0) l2++;
+            const int sh = 29 + (int)l2;  // (e - s0) << 40 over 2^11 bins
+            const u64 base = (u64)s0 << 40;
+            for (u32 i = tid; i < kSrBins; i += kSrBlock) bins[i] = 0;
+            if (tid == 0) {
+                misc[0] = 0;
+                misc[23] = 0;
+            }
+            __syncthreads();
+            SR_MARK(1);
+            u32 dg[R];
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                dg[i] = (u32)(((k[i][0] & M48) - base) >> sh) & (kSrBins - 1);
+                if ((u32)tid + (u32)i * kSrBlock < len) atomicAdd(&bins[dg[i]], 1u);
+            }
+            __syncthreads();
+            SR_MARK(2);
+            // bin starts: 2 bins per thread, block-wide exclusive scan
+            const u32 c0 = bins[2 * tid], c1 = bins[2 * tid + 1];
+            const u32 sum = c0 + c1;
+            u32 inc = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            if (lane == 63) misc[1 + wave] = inc;
+            if (max(c0, c1) > kMaxSortBin) misc[0] = 1u;
+            __syncthreads();
+            if (uni32(misc[0])) {  // clustered keys: hash path
+                if (tid == 0) {
+                    a.run_flags[(u64)b * 256u + s0] = 1;
+                    a.bucket_flags[b] = 1;
+                    atomicAdd(a.nflag, 1u);
+                }
+                __syncthreads();
+                continue;
+            }
+            u32 wpre = 0;
+            for (int w = 0; w < wave; w++) wpre += misc[1 + w];
+            const u32 bs = wpre + inc - sum;
+            bins[2 * tid] = bs;
+            bins[2 * tid + 1] = bs + c0;
+            __syncthreads();
+            SR_MARK(3);
+            u32 qs[R];  // each key's LDS slot (ties between equal keys)
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                qs[i] = 0;
+                if ((u32)tid + (u32)i * kSrBlock >= len) continue;
+                const u32 q = atomicAdd(&bins[dg[i]], 1u);
+                qs[i] = q;
+#pragma unroll
+                for (int j = 0; j < W; j++) skey[(size_t)j * SP + q] = k[i][j];
+            }
+            __syncthreads();
+            SR_MARK(4);
+            // each key's sorted position: its bin's start (bins now hold bin
+            // ends) + the bin's smaller keys + the equal keys in earlier slots
+            u32 pos[R];
+            bool dup = false;
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const bool valid = (u32)tid + (u32)i * kSrBlock < len;
+                const u32 d = dg[i];
+                const u32 b0 = d ? bins[d - 1] : 0u, b1 = bins[d];
+                const u32 nbn = valid ? b1 - b0 : 0u;
+                // common case: word 0 against up to 8 bin entries read at
+                // once (clamped, masked); ties or bigger bins take the loop
+                constexpr int U8 = 8;
+                u64 w0[U8];
+#pragma unroll
+                for (int x = 0; x < U8; x++) w0[x] = skey[min(b0 + (u32)x, (u32)SP - 1)];
+                u32 r = b0;
+                bool slow = nbn > (u32)U8;
+#pragma unroll
+                for (int x = 0; x < U8; x++) {
+                    const bool in = (u32)x < nbn;
+                    r += (in && w0[x] < k[i][0]) ? 1u : 0u;
+                    slow |= in && w0[x] == k[i][0] && b0 + (u32)x != qs[i];
+                }
+                pos[i] = r;
+                if (!slow) continue;
+                r = b0;
+                for (u32 x = b0; x < b1; x++) {
+                    int c = 0;  // key x vs this key: -1 less, 0 equal, 1 greater
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) {
+                        const u64 kx = skey[(size_t)jj * SP + x];
+                        if (c == 0 && kx != k[i][jj]) c = kx < k[i][jj] ? -1 : 1;
+                    }
+                    r += (c < 0 || (c == 0 && x < qs[i])) ? 1u : 0u;
+                    dup |= c == 0 && x != qs[i];
+                }
+                pos[i] = r;
+            }
+            if (dup) misc[23] = 1u;
+            __syncthreads();
+            SR_MARK(5);
+            if (!uni32(misc[23])) {
+                // distinct keys (the high-cardinality case): records are the
+                // keys, each written straight to its sorted place, count 1
+                if (tid == 0) {
+                    const u64 rbase = atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)len);
+                    *(u64*)(misc + 20) = rbase;
+                    if (rbase + len > a.rec_cap)
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                    const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
+                    if (di < a.desc_cap) {
+                        a.desc_key[di] = ((u64)b << 48) | base;
+                        a.desc_start[di] = rbase;
+                        a.desc_len[di] = len | ((u32)(sh + 1) << 24) | (1u << 31);  // sorted
+                    }
+                }
+                __syncthreads();
+                SR_MARK(6);
+                const u64 rbase = *(const u64*)(misc + 20);
+#pragma unroll
+                for (int i = 0; i < R; i++) {
+                    if ((u32)tid + (u32)i * kSrBlock >= len) continue;
+                    const u64 r = rbase + pos[i];
+                    if (r < a.rec_cap) {
+#pragma unroll
+                        for (int jj = 0; jj < W; jj++) a.rec_keys[(u64)jj * a.rec_cap + r] = k[i][jj];
+                        a.rec_cnts[r] = 1u;
+                    }
+                }
+                SR_MARK(8);
+                continue;
+            }
+            // equal keys: the keys are permuted into sorted order in LDS and
+            // run-length encoded
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                if ((u32)tid + (u32)i * kSrBlock >= len) continue;
+#pragma unroll
+                for (int jj = 0; jj < W; jj++) skey[(size_t)jj * SP + pos[i]] = k[i][jj];
+            }
+            __syncthreads();
+            // heads (first of equal keys) in strided order; record rank = heads
+            // before the position (per-i wave ballots, then a scan of the
+            // R x 16 wave totals in position order by wave 0)
+            bool head[R];
+            u32 hb[R];
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const u32 p = (u32)tid + (u32)i * kSrBlock;
+                bool h = p < len;
+                if (h && p > 0) {
+                    bool eq = true;
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) eq = eq && skey[(size_t)jj * SP + p] == skey[(size_t)jj * SP + p - 1];
+                    h = !eq;
+                }
+                head[i] = h;
+                const u64 bm = __ballot(h);
+                hb[i] = (u32)__popcll(bm & lanemask_lt());
+                if (lane == 0) bins[i * kSrWaves + wave] = (u32)__popcll(bm);  // bins are free after the sort
+            }
+            __syncthreads();
+            if (wave == 0) {
+                constexpr u32 NV = R * kSrWaves;  // <= 128: two per lane
+                static_assert(NV <= 128, "wave totals");
+                const u32 x0 = 2u * (u32)lane, x1 = x0 + 1;
+                const u32 v0 = x0 < NV ? bins[x0] : 0u, v1 = x1 < NV ? bins[x1] : 0u;
+                const u32 sum = v0 + v1;
+                u32 inc = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const u32 y = __shfl_up(inc, o);
+                    if (lane >= o) inc += y;
+                }
+                const u32 ex = inc - sum;
+                if (x0 < NV) bins[x0] = ex;
+                if (x1 < NV) bins[x1] = ex + v0;
+                const u32 run = __shfl(inc, 63);
+                if (lane == 0) {
+                    const u64 rbase = atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)run);
+                    *(u64*)(misc + 20) = rbase;
+                    if (rbase + run > a.rec_cap)
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                    const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
+                    if (di < a.desc_cap) {
+                        a.desc_key[di] = ((u64)b << 48) | base;
+                        a.desc_start[di] = rbase;
+                        a.desc_len[di] = run | ((u32)(sh + 1) << 24) | (1u << 31);  // sorted
+                    }
+                }
+            }
+            __syncthreads();
+            SR_MARK(7);
+            const u64 rbase = *(const u64*)(misc + 20);
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                if (!head[i]) continue;
+                const u32 p = (u32)tid + (u32)i * kSrBlock;
+                u32 q = p + 1;
+                while (q < len) {
+                    bool eq = true;
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) eq = eq && skey[(size_t)jj * SP + q] == skey[(size_t)jj * SP + p];
+                    if (!eq) break;
+                    q++;
+                }
+                const u64 r = rbase + bins[i * kSrWaves + wave] + hb[i];
+                if (r < a.rec_cap) {
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) a.rec_keys[(u64)jj * a.rec_cap + r] = skey[(size_t)jj * SP + p];
+                    a.rec_cnts[r] = q - p;
+                }
+            }
+            __syncthreads();
+            SR_MARK(8);
+        }
+    }
+#ifdef KC_EXPERIMENTS
+    if (blockIdx.x == 0 && tid == 0)
+        printf("kc: sort_runs block 0 ticks (100 MHz): scan %llu load %llu hist %llu binscan %llu scatter %llu "
+               "isort %llu heads %llu tid0 %llu write %llu\n",
+               (unsigned long long)ph[0], (unsigned long long)ph[1], (unsigned long long)ph[2],
+               (unsigned long long)ph[3], (unsigned long long)ph[4], (unsigned long long)ph[5],
+               (unsigned long long)ph[6], (unsigned long long)ph[7], (unsigned long long)ph[8]);
+#endif
+#undef SR_MARK
+}
+
+hipError_t launch_sort_runs(int W, const uint64_t* keys, uint64_t stride, const uint64_t* sub_starts,
+                            uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
+                            uint64_t* rec_cursor, uint64_t* stats, uint64_t* desc_key, uint64_t* desc_start,
+                            uint32_t* desc_len, uint64_t desc_cap, uint8_t* run_flags, uint8_t* bucket_flags,
+                            uint32_t* nflag, int grid, hipStream_t s) {
+    SortRunArgs a;
+    a.keys = keys;
+    a.stride = stride;
+    a.sub_starts = sub_starts;
+    a.nbuckets = nbuckets;
+    a.rec_keys = rec_keys;
+    a.rec_cnts = rec_cnts;
+    a.rec_cap = rec_cap;
+    a.rec_cursor = rec_cursor;
+    a.stats = stats;
+    a.desc_key = desc_key;
+    a.desc_start = desc_start;
+    a.desc_len = desc_len;
+    a.desc_cap = desc_cap;
+    a.run_flags = run_flags;
+    a.bucket_flags = bucket_flags;
+    a.nflag = nflag;
+    const size_t lds = (sort_runs_lds(W) + 15) & ~(size_t)15;
+    switch (W) {
+    case 1: hipLaunchKernelGGL(sort_runs_k<1>, dim3(grid), dim3(kSrBlock), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(sort_runs_k<2>, dim3(grid), dim3(kSrBlock), lds, s, a); break;
+    case 3: hipLaunchKernelGGL(sort_runs_k<3>, dim3(grid), dim3(kSrBlock), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(sort_runs_k<4>, dim3(grid), dim3(kSrBlock), lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 size_t bucket_lds_bytes(int W) {
     size_t lcap = (size_t)bucket_lds_slots(W);
     return lcap * (8 * W + 4 + (W >= 2 ? 4 : 0)) + (48 + (size_t)kBucketWaves * kQueue) * 4 + 16;
@@ -2227,8 +2623,12 @@ hipError_t launch_count_buckets(int W, const uint64_t* keys, uint64_t stride, co
                                 uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill,
                                 uint64_t spill_cap, uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid,
                                 uint64_t* desc_key, uint64_t* desc_start, uint32_t* desc_len, uint64_t desc_cap,
-                                hipStream_t s, bool distinct, const uint64_t* sub_starts) {
+                                hipStream_t s, bool distinct, const uint64_t* sub_starts,
+                                const uint8_t* run_flags, const uint8_t* bucket_flags, uint32_t run_per) {
     BucketArgs a;
+    a.run_flags = run_flags;
+    a.bucket_flags = bucket_flags;
+    a.run_per = run_per;
     a.skip = experiment_knob("KC_P5_SKIP");
     a.distinct = distinct ? 1 : 0;
     a.sub_starts = sub_starts;
@@ -2452,13 +2852,15 @@ __global__ __launch_bounds__(kP3Block) void p3_scatter_k(const u64* __restrict__
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     u64 nk[KPT][W];
     auto load = [&](u64 t) {
+        if (t >= ntiles) return;
         u64 lo = 0, hi = 0;
-        if (t < ntiles) p3_tile_range(rstart, tpre, t, TILE, &lo, &hi);
+        p3_tile_range(rstart, tpre, t, TILE, &lo, &hi);
+        // unconditional loads, clamped into the (never empty) tile
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
-            const u64 q = lo + (u64)i * kP3Block + tid;
+            const u64 q = min(lo + (u64)i * kP3Block + tid, hi - 1);
 #pragma unroll
-            for (int j = 0; j < W; j++) nk[i][j] = q < hi ? __builtin_nontemporal_load(kin + (u64)j * stride + q) : 0ull;
+            for (int j = 0; j < W; j++) nk[i][j] = __builtin_nontemporal_load(kin + (u64)j * stride + q);
         }
     };
     load(blockIdx.x);
@@ -2709,13 +3111,13 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             l0 = dlen[od] & 0xffffffu;
             if (l0 > (u32)CAP) l0 = 0;
         }
+        // unconditional loads (clamped into the segment; none past it is used)
 #pragma unroll
         for (int i = 0; i < PI; i++) {
-            const u32 p = (u32)tid + (u32)i * kSegBlock;
-            const bool ok = p < l0;
+            const u32 p = l0 ? min((u32)tid + (u32)i * kSegBlock, l0 - 1) : 0u;
 #pragma unroll
-            for (int j = 0; j < W; j++) nk[i][j] = ok ? rkeys[(u64)j * rstride + s0 + p] : 0ull;
-            nc[i] = ok ? rcnts[s0 + p] : 0u;
+            for (int j = 0; j < W; j++) nk[i][j] = rkeys[(u64)j * rstride + s0 + p];
+            nc[i] = rcnts[s0 + p];
         }
     };
     load_seg(blockIdx.x);
@@ -2727,7 +3129,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         const u64 obase = out_off[di];
         // digit = ((word0 & M48) - base) >> sh: the segment's key range over
         // the 4096 bins (base: the sorted descriptor key's bits below 48)
-        const int sh = (int)(lw >> 24);
+        const int sh = (int)(lw >> 24) & 63;
         const u64 dbase = dkey ? (dkey[di] & kM48) : 0ull;
         u64 ck[PI][W];
         u32 cc[PI];
@@ -2738,6 +3140,21 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
             cc[i] = nc[i];
         }
         load_seg(di + gridDim.x);
+        if (lw >> 31) {
+            // already sorted (sort_runs_k): copied to its place
+#pragma unroll
+            for (int i = 0; i < PI; i++) {
+                const u32 p = (u32)tid + (u32)i * kSegBlock;
+                if (p < len && !(skip & 1)) seg_put<W>(okeys, ocnts, ostride, packed, obase + p, ck[i], cc[i]);
+            }
+            for (u32 p = tid + PI * kSegBlock; p < ((skip & 1) ? 0u : len); p += kSegBlock) {
+                u64 kk[W];
+#pragma unroll
+                for (int j = 0; j < W; j++) kk[j] = rkeys[(u64)j * rstride + st + p];
+                seg_put<W>(okeys, ocnts, ostride, packed, obase + p, kk, rcnts[st + p]);
+            }
+            continue;
+        }
         for (int i = tid; i < 4096; i += kSegBlock) bcnt[i] = 0;
         if (tid == 0) misc[0] = 0;
         __syncthreads();
@@ -2764,7 +3181,7 @@ __global__ __launch_bounds__(kSegBlock) void seg_sort_k(const u64* __restrict__ 
         if (lane == 63) misc[1 + wave] = inc;
         if (max(max(c0, c1), max(c2, c3)) > kMaxBin) atomicOr(&misc[0], 1u);
         __syncthreads();
-        if (misc[0]) {
+        if (uni32(misc[0])) {
             if (tid == 0) {
                 const u64 f = atomicAdd((unsigned long long*)fb_n, 1ull);
                 fb[f] = (u32)di;
@@ -3302,36 +3719,42 @@ __global__ __launch_bounds__(kBlock) void merge_tile_packed_k(const u32* __restr
     constexpr int RW = MergePkCfg<W>::RW;
     constexpr int ITEMS = MergePkCfg<W>::ITEMS;
     constexpr int TILE = MergePkCfg<W>::TILE;
-    __shared__ u32 sin[TILE * RW];   // A slice, then B slice
-    __shared__ u32 sout[TILE * RW];  // merged tile
+    constexpr int NPT = TILE * RW / kBlock;  // u32 of a tile per thread
+    static_assert(TILE * RW % kBlock == 0 && TILE * RW * 4 % 16 == 0, "tile layout");
+    __shared__ __attribute__((aligned(16))) u32 sin[TILE * RW];   // A slice, then B slice
+    __shared__ __attribute__((aligned(16))) u32 sout[TILE * RW];  // merged tile
     const int tid = threadIdx.x;
     bool seen_dup = false;
+    // the next tile's A and B slices are loaded into registers while the
+    // current tile merges (software pipeline over the block's tiles)
+    u32 v[NPT];
+    auto fetch = [&](u64 t) {
+        if (t >= ntiles) return;
+        const u64 d0 = t * (u64)TILE, d1 = min(d0 + TILE, na + nb);
+        const u64 i0 = split[t], i1 = split[t + 1];
+        const u32 ea = (u32)(i1 - i0) * RW, tot = (u32)(d1 - d0) * RW;
+        const u32* pa = A + i0 * RW;
+        const u32* pb = B + (d0 - i0) * RW;
+#pragma unroll
+        for (int u = 0; u < NPT; u++) {
+            const u32 x = (u32)u * kBlock + (u32)tid;
+            const u32 xc = min(x, tot - 1);  // unconditional loads (no per-element waits)
+            v[u] = __builtin_nontemporal_load(xc < ea ? pa + xc : pb + (xc - ea));
+        }
+    };
+    fetch(blockIdx.x);
     for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const u64 d0 = t * (u64)TILE, d1 = min(d0 + TILE, na + nb);
         const u64 i0 = split[t], i1 = split[t + 1];
         const u64 j0 = d0 - i0, j1 = d1 - i1;
         const u32 la = (u32)(i1 - i0), lb = (u32)(j1 - j0), n = la + lb;
-        {
-            // A slice then B slice, LB independent loads in flight per thread
-            constexpr int LB = 10;
-            const u32 ea = la * RW, tot = n * RW;
-            const u32* pa = A + i0 * RW;
-            const u32* pb = B + j0 * RW;
-            for (u32 x0 = 0; x0 < tot; x0 += kBlock * LB) {
-                u32 v[LB];
 #pragma unroll
-                for (int u = 0; u < LB; u++) {
-                    const u32 x = x0 + (u32)u * kBlock + (u32)tid;
-                    v[u] = x < tot ? __builtin_nontemporal_load(x < ea ? pa + x : pb + (x - ea)) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < LB; u++) {
-                    const u32 x = x0 + (u32)u * kBlock + (u32)tid;
-                    if (x < tot) sin[x] = v[u];
-                }
-            }
+        for (int u = 0; u < NPT; u++) {
+            const u32 x = (u32)u * kBlock + (u32)tid;
+            if (x < n * RW) sin[x] = v[u];
         }
         __syncthreads();
+        fetch(t + gridDim.x);
         const u32 dl = min((u32)tid * ITEMS, n);
         u32 lo = dl > lb ? dl - lb : 0, hi = dl < la ? dl : la;
         while (lo < hi) {
@@ -3374,7 +3797,15 @@ __global__ __launch_bounds__(kBlock) void merge_tile_packed_k(const u32* __restr
                 }
             }
         }
-        for (u32 x = tid; x < n * RW; x += kBlock) out[d0 * RW + x] = sout[x];
+        u32* o = out + d0 * RW;
+        const u32 tot = n * RW;
+        if (((uintptr_t)o & 15u) == 0) {  // 16-byte stores (tiles start 16-byte aligned in an aligned run)
+            const u32 nv = tot / 4;
+            for (u32 x = tid; x < nv; x += kBlock) ((uint4*)o)[x] = ((const uint4*)sout)[x];
+            for (u32 x = nv * 4 + tid; x < tot; x += kBlock) o[x] = sout[x];
+        } else {
+            for (u32 x = tid; x < tot; x += kBlock) o[x] = sout[x];
+        }
         __syncthreads();
     }
     if (__ballot(seen_dup) && lane_id() == 0) atomicOr(dup, 1u);
@@ -4016,44 +4447,48 @@ hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, 
 // ---------------------------------------------------------------------------
 
 __global__ __launch_bounds__(kBlock) void sketch_k(const u32* __restrict__ codes, const unsigned short* __restrict__ inval,
-                                                  u64 n_reads, int G, int k, u64* __restrict__ out, u64 cap,
-                                                  u64* __restrict__ counter) {
+                                                  u64 n_reads, int G, int k, int rate_bits, u64* __restrict__ out,
+                                                  u64 cap, u64* __restrict__ counter) {
     const int ng = (k + 15) >> 4;  // groups a k-mer spans from a group start
     const int per = G - ng + 1;    // aligned k-mers per read
-    const u64 total = per > 0 ? n_reads * (u64)per : 0;
-    for (u64 it = (u64)blockIdx.x * kBlock + threadIdx.x; it < total; it += (u64)gridDim.x * kBlock) {
-        const u64 r = it / (u64)per;
-        const int g = (int)(it - r * (u64)per);
-        const u64 base = r * (u64)G + (u64)g;
-        u64 h = 0x243f6a8885a308d3ull ^ (u64)k;
-        bool ok = true;
-        for (int j = 0; j < ng; j++) {
-            const int nb = min(16, k - 16 * j);  // bases of this group inside the k-mer
-            const u32 keep = nb == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb));
-            const unsigned short bad = (unsigned short)(inval[base + j] & (nb == 16 ? 0xffffu : ~(0xffffu >> nb)));
-            ok = ok && bad == 0;
-            h = mix64(h ^ (u64)(codes[base + j] & keep) ^ ((u64)j << 40));
-        }
-        const bool take = ok && (h & 255u) == 0;
-        const u64 m = __ballot(take);
-        if (!m) continue;
-        u64 at = 0;
-        const int lead = __ffsll((long long)m) - 1;
-        if (lane_id() == lead) at = atomicAdd((unsigned long long*)counter, (unsigned long long)__popcll(m));
-        at = __shfl(at, lead);
-        if (take) {
-            const u64 q = at + (u64)__popcll(m & lanemask_lt());
-            if (q < cap) out[q] = h >> 8;
+    const u64 rmask = (1ull << rate_bits) - 1;
+    // one read per thread (no division per item); a wave takes one counter
+    // add per aligned position that sampled anything
+    for (u64 r0 = (u64)blockIdx.x * kBlock; r0 < n_reads; r0 += (u64)gridDim.x * kBlock) {
+        const u64 r = r0 + threadIdx.x;
+        const bool live = r < n_reads;
+        for (int g = 0; g < per; g++) {
+            const u64 base = (live ? r : 0) * (u64)G + (u64)g;
+            u64 h = 0x243f6a8885a308d3ull ^ (u64)k;
+            bool ok = live;
+            for (int j = 0; j < ng; j++) {
+                const int nb = min(16, k - 16 * j);  // bases of this group inside the k-mer
+                const u32 keep = nb == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb));
+                const unsigned short bad = (unsigned short)(inval[base + j] & (nb == 16 ? 0xffffu : ~(0xffffu >> nb)));
+                ok = ok && bad == 0;
+                h = mix64(h ^ (u64)(codes[base + j] & keep) ^ ((u64)j << 40));
+            }
+            const bool take = ok && (h & rmask) == 0;
+            const u64 m = __ballot(take);
+            if (!m) continue;
+            u64 at = 0;
+            const int lead = __ffsll((long long)m) - 1;
+            if (lane_id() == lead) at = atomicAdd((unsigned long long*)counter, (unsigned long long)__popcll(m));
+            at = __shfl(at, lead);
+            if (take) {
+                const u64 q = at + (u64)__popcll(m & lanemask_lt());
+                if (q < cap) out[q] = h >> 8;
+            }
         }
     }
 }
 
-hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, uint64_t* out,
-                         uint64_t cap, uint64_t* counter, hipStream_t s) {
+hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, int rate_bits,
+                         uint64_t* out, uint64_t cap, uint64_t* counter, hipStream_t s) {
     const int G = groups_per_read(L);
-    const u64 total = n_reads * (u64)(G > 0 ? G : 1);
-    hipLaunchKernelGGL(sketch_k, dim3(grid_for(total)), dim3(kBlock), 0, s, codes, (const unsigned short*)inval,
-                       n_reads, G, k, out, cap, counter);
+    if (G <= 0 || n_reads == 0) return hipSuccess;
+    hipLaunchKernelGGL(sketch_k, dim3(grid_for(n_reads)), dim3(kBlock), 0, s, codes, (const unsigned short*)inval,
+                       n_reads, G, k, rate_bits, out, cap, counter);
     return hipGetLastError();
 }
 

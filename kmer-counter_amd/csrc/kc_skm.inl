@@ -1665,15 +1665,17 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
     const u64 t_first = xcd_map ? (u64)(blockIdx.x & 7u) * tx + (blockIdx.x >> 3) : (u64)blockIdx.x;
     const u64 t_end = xcd_map ? min(ntiles, (u64)((blockIdx.x & 7u) + 1) * tx) : ntiles;
     auto load = [&](u64 t) {
+        if (t >= t_end) return;
         u64 lo = 0, hi = 0;
-        if (t < t_end) rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+        // unconditional loads (clamped into the tile, which is never empty):
+        // a per-element select on a load makes hipcc wait for each one
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
-            const u64 q = lo + (u64)i * kP3Block + tid;
+            const u64 q = min(lo + (u64)i * kP3Block + tid, hi - 1);
 #pragma unroll
-            for (int j = 0; j < NW; j++)
-                nk[i][j] = q < hi ? __builtin_nontemporal_load(kin + (u64)j * istride + q) : 0ull;
-            if constexpr (PAY) np[i] = q < hi ? __builtin_nontemporal_load(pin + q) : 0u;
+            for (int j = 0; j < NW; j++) nk[i][j] = __builtin_nontemporal_load(kin + (u64)j * istride + q);
+            if constexpr (PAY) np[i] = __builtin_nontemporal_load(pin + q);
         }
     };
     load(t_first);

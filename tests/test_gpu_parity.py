@@ -477,12 +477,13 @@ def test_presplit_buckets_high_cardinality(kca, orc, monkeypatch, k):
     were mostly distinct, the next batches split every bucket once more by key
     bits 40..47 (P3b, an MSD regional radix pass) and P5 counts runs of
     consecutive sub-buckets in one pass each; the runs cut from the records
-    merge on the device. Same bytes as the oracle; the pass can be disabled
-    (KC_NO_P3B) with the same result."""
+    merge on the device. Runs of sub-buckets are sorted in LDS (P5s); the
+    LDS hash table for every run (KC_NO_SORT_RUNS) and no P3b pass
+    (KC_NO_P3B) give the same bytes as the oracle."""
     monkeypatch.setenv("KC_P3B_MIN", "1")
     fq = kca.synth_fastq(30000, 150, seed=k + 3, n_rate=0.0005)
     outs = []
-    for env in ((), ("KC_NO_P3B",)):
+    for env in ((), ("KC_NO_SORT_RUNS",), ("KC_NO_P3B",)):
         for v in env:
             monkeypatch.setenv(v, "1")
         with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=24 << 20, engine="partition") as ctx:
@@ -490,7 +491,46 @@ def test_presplit_buckets_high_cardinality(kca, orc, monkeypatch, k):
             outs.append(ctx.records())
             st = ctx.stats()
         assert st["batches"] >= 3
-    assert outs[0] == outs[1] == orc.count_fastq(fq, k)
+        for v in env:
+            monkeypatch.delenv(v)
+    assert outs[0] == outs[1] == outs[2] == orc.count_fastq(fq, k)
+
+
+def _fastq_from_codes(codes):
+    """FASTQ bytes of reads given as base codes 0..3 (ACGT), one row a read."""
+    import numpy as np
+    seq = np.frombuffer(b"ACGT", dtype=np.uint8)[codes]
+    L = codes.shape[1]
+    qual = b"I" * L
+    out = []
+    for i, row in enumerate(seq):
+        out.append(b"@r%d\n%s\n+\n%s\n" % (i, row.tobytes(), qual))
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_sorted_runs_hand_off_to_hash_path(kca, orc, monkeypatch, capfd, k):
+    """P5s hands the runs it cannot sort to the LDS hash table: a sub-bucket
+    of more keys than a sorted run holds (12k reads sharing their first 12
+    bases) and runs whose keys crowd one sort bin (3k reads sharing their first
+    24 bases), among iid reads. One batch of >= 2^24 keys: the coverage sketch
+    marks it high-cardinality, so P3b and P5s run on it. Same bytes as the
+    oracle; the hand-off is seen in the P5s debug line."""
+    import numpy as np
+    monkeypatch.setenv("KC_DEBUG", "1")
+    rng = np.random.default_rng(k)
+    L = 150
+    reads = rng.integers(0, 4, size=(180000, L), dtype=np.uint8)
+    reads[:12000, :12] = rng.integers(0, 4, size=12, dtype=np.uint8)
+    reads[12000:15000, :24] = rng.integers(0, 4, size=24, dtype=np.uint8)
+    fq = _fastq_from_codes(reads[rng.permutation(len(reads))])
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=2 << 30, engine="partition") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    err = capfd.readouterr().err
+    flagged = [int(x.split("flagged=")[1].split()[0]) for x in err.splitlines() if "kc: P5s" in x]
+    assert flagged and max(flagged) > 0, err[-2000:]
+    assert got == orc.count_fastq(fq, k)
 
 
 def _u64_sortable(lo32, hi32):
