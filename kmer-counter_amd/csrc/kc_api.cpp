@@ -152,6 +152,7 @@ struct kc_ctx {
 };
 
 static kc_status cut_run(kc_ctx* c);
+static kc_status keep_finished_run(kc_ctx* c, uint64_t n);
 static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
 static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
 static void release_dev_runs(kc_ctx* c, bool free_pool);
@@ -188,6 +189,25 @@ static kc_status ensure(kc_ctx* c, DevBuf& b, size_t bytes) {
     HIPCHK(c, hipMalloc(&b.p, want));
     b.bytes = want;
     return KC_OK;
+}
+
+// As ensure, but a pooled run buffer that is big enough (best fit) is swapped
+// in before anything is allocated: finished runs, merge outputs and fin_packed
+// trade the same few large buffers instead of reallocating tens of GB per pass.
+static kc_status ensure_pooled(kc_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.p && b.bytes >= bytes) return KC_OK;
+    int best = -1;
+    for (size_t i = 0; i < c->run_pool.size(); i++)
+        if (c->run_pool[i].bytes >= bytes && (best < 0 || c->run_pool[i].bytes < c->run_pool[(size_t)best].bytes))
+            best = (int)i;
+    if (best >= 0) {
+        DevBuf t = c->run_pool[(size_t)best];
+        c->run_pool.erase(c->run_pool.begin() + best);
+        if (b.p) c->run_pool.push_back(b);
+        b = t;
+        return KC_OK;
+    }
+    return ensure(c, b, bytes);
 }
 
 static void release(DevBuf& b) {
@@ -447,6 +467,83 @@ static const uint32_t kSkmSample = 256;
 static const uint64_t kSkmSampleMinKeys = 1ull << 24;
 static const double kSkmDistinctMax = 0.35;
 
+// P5s direct (high cardinality, empty record state): sort_runs_k writes the
+// batch's records straight into fin_packed as a finished sorted run (record
+// 0: key 0 when present), each run of sub-buckets at its first key's position;
+// runs that held equal keys leave gaps that a segment copy closes. The run is
+// kept (keep_finished_run) and the record state stays empty. *done = false
+// when runs were handed to the hash path: nothing was kept and the caller
+// counts the batch into records as usual.
+static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub_starts, uint32_t nb, uint64_t n,
+                            uint8_t* rf, size_t fl, bool* done, uint64_t* records, float* ms) {
+    kc_status s;
+    *done = false;
+    const int W = c->W;
+    const size_t rs = (size_t)c->rs;
+    uint8_t* bf = rf + ((size_t)nb << 8);
+    uint32_t* nflag = (uint32_t*)(bf + nb);
+    if ((s = sync_stats(c))) return s;
+    const bool key0 = c->stats_h[ST_KEY0_PRESENT] != 0;
+    const uint64_t off0 = key0 ? 1 : 0;
+    if ((s = ensure_pooled(c, c->fin_packed, (off0 + n) * rs + 16))) return s;
+    HIPCHK(c, hipMemsetAsync(rf, 0, fl, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_sort_runs(W, keys, c->key_cap, sub_starts, nb, c->rec_keys, c->rec_cnts, c->rec_cap,
+                               c->rec_cursor, c->stats, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,
+                               (uint32_t*)c->desc_len.p, kDescCap, rf, bf, nflag, 2 * c->n_cu, c->stream,
+                               c->fin_packed.p, off0));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    uint32_t nf = 0;
+    uint64_t R = 0;
+    HIPCHK(c, hipMemcpyAsync(&nf, nflag, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&R, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
+    if ((s = sync_stats(c))) return s;
+    HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+    *records = R;
+    const uint64_t ndesc = c->stats_h[ST_DESC_FILL];
+    if (nf || (R < n && ndesc > kDescCap)) {
+        // undo (record cursor, descriptors): the caller counts into records
+        HIPCHK(c, hipMemsetAsync(c->rec_cursor, 0, 8, c->stream));
+        c->stats_h[ST_DESC_FILL] = 0;
+        HIPCHK(c, hipMemcpyAsync(c->stats + ST_DESC_FILL, &c->stats_h[ST_DESC_FILL], 8, hipMemcpyHostToDevice,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return KC_OK;
+    }
+    if (R < n) {
+        // equal keys in some runs: close the gaps (segments in key order)
+        if ((s = ensure(c, c->desc_k2, ndesc * 8)) || (s = ensure(c, c->desc_v, ndesc * 4)) ||
+            (s = ensure(c, c->desc_v2, ndesc * 4)) || (s = ensure(c, c->desc_lens, ndesc * 8)) ||
+            (s = ensure(c, c->desc_offs, ndesc * 8)) || (s = ensure(c, c->rle_tmp, scan_tmp_elems(ndesc) * 8)) ||
+            (s = ensure_pooled(c, c->merge_tmp, (off0 + R) * rs + 16)))
+            return s;
+        HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, ndesc, c->stream));
+        int which = 0;
+        if ((s = sort_records(c, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_k2.p, (uint32_t*)c->desc_v.p,
+                              (uint32_t*)c->desc_v2.p, ndesc, ndesc, &which, 1)))
+            return s;
+        const uint32_t* order = (const uint32_t*)(which ? c->desc_v2.p : c->desc_v.p);
+        HIPCHK(c, launch_desc_prep(order, (const uint32_t*)c->desc_len.p, ndesc, (uint64_t*)c->desc_lens.p,
+                                   c->stream));
+        HIPCHK(c, launch_scan_u64((const uint64_t*)c->desc_lens.p, (uint64_t*)c->desc_offs.p, ndesc,
+                                  (uint64_t*)c->rle_tmp.p, c->stream));
+        HIPCHK(c, launch_packed_seg_copy(W, c->fin_packed.p, c->merge_tmp.p, order, (const uint64_t*)c->desc_start.p,
+                                         (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, off0,
+                                         4 * c->n_cu, c->stream));
+        std::swap(c->fin_packed, c->merge_tmp);
+    }
+    std::vector<uint32_t> r0((size_t)c->rs / 4, 0u);
+    if (key0) {
+        r0.back() = (uint32_t)c->stats_h[ST_KEY0];
+        HIPCHK(c, hipMemcpyAsync(c->fin_packed.p, r0.data(), c->rs, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->batches = 1;  // this batch: moved to batches_cut with the run
+    if ((s = keep_finished_run(c, off0 + R))) return s;
+    *done = true;
+    return KC_OK;
+}
+
 // Engine "partition": per batch of reads
 //   P1 hist   : digit (word0 >> 48) & 255 per segment of reads
 //   P2 scatter: keys to their digit's region (LDS counting sort per tile)
@@ -629,6 +726,29 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             // the runs it flags (a sub-bucket too big, clustered keys) take
             // the LDS hash table (KC_NO_SORT_RUNS: hash table for all runs)
             const bool sort_runs = sub_starts && !getenv("KC_NO_SORT_RUNS");
+            uint64_t direct_min = 1ull << 22;  // (KC_P5S_DIRECT_MIN: path selector for tests)
+            if (const char* e = getenv("KC_P5S_DIRECT_MIN")) direct_min = strtoull(e, nullptr, 10);
+            if (sort_runs && c->rec_n == 0 && c->batches == 0 && c->stats_h[ST_CLAIMED] == 0 && !c->skm_used &&
+                c->runs.empty() && n >= direct_min && !getenv("KC_NO_P5S_DIRECT")) {
+                const size_t fl = ((size_t)nb << 8) + nb + 16;
+                if ((s = ensure(c, c->run_flags, fl))) return s;
+                bool dd = false;
+                uint64_t R = 0;
+                float t5 = 0.f;
+                if ((s = p5s_direct(c, p5_keys, sub_starts, nb, n, (uint8_t*)c->run_flags.p, fl, &dd, &R, &t5)))
+                    return s;
+                c->part_ms[4] += t5;
+                c->p5_launches++;
+                if (getenv("KC_DEBUG"))
+                    fprintf(stderr, "kc: P5s direct n=%llu records=%llu kept=%d %.3f ms\n", (unsigned long long)n,
+                            (unsigned long long)R, dd ? 1 : 0, t5);
+                if (dd) {
+                    c->hc_hint = R * 2 > n;
+                    c->engines_used |= 2u;
+                    done += nr;
+                    continue;
+                }
+            }
             if (sort_runs) {
                 if ((s = grow_records(c, rec0 + n))) return s;
                 const size_t fl = ((size_t)nb << 8) + nb + 16;
@@ -1979,7 +2099,7 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
         if ((s = ensure(c, c->desc_fb, ndesc * 4 + 16))) return s;
         fb = (uint32_t*)c->desc_fb.p;
         // sorted straight into the packed output, after the key-0 record
-        if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
+        if ((s = ensure_pooled(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
         phase("descriptor scan");
         HIPCHK(c, launch_seg_sort(W, c->rec_keys, c->rec_cnts, c->rec_cap, order, (const uint64_t*)c->desc_start.p,
                                   (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, k0 + off0,
@@ -1988,7 +2108,7 @@ static kc_status finish_part_sorted(kc_ctx* c, uint64_t ndesc, uint64_t* n_out) 
                                   (const uint64_t*)(which ? c->desc_k2.p : c->desc_key.p)));
         phase("segment sort");
     }
-    if ((s = ensure(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
+    if ((s = ensure_pooled(c, c->fin_packed, (size_t)n * c->rs + 16))) return s;
     // record 0: key 0^W (all-zero words) and its count (kept alive until the
     // stream is synchronised below)
     std::vector<uint32_t> r0((size_t)c->rs / 4, 0u);
@@ -2637,7 +2757,7 @@ static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const 
     uint64_t* split = (uint64_t*)c->fin_misc.p;
     HIPCHK(c, hipMemsetAsync(dup, 0, 4, c->stream));
     if (runs.size() <= 1) {
-        if ((s = ensure(c, c->fin_packed, n * rs + 16))) return s;
+        if ((s = ensure_pooled(c, c->fin_packed, n * rs + 16))) return s;
         if (n && runs[0].first != c->fin_packed.p)
             HIPCHK(c, hipMemcpyAsync(c->fin_packed.p, runs[0].first, n * rs, hipMemcpyDeviceToDevice, c->stream));
     } else {
@@ -2645,7 +2765,7 @@ static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const 
         int lvl = 0;
         while (runs.size() > 1) {
             DevBuf* o = out[lvl & 1];
-            if ((s = ensure(c, *o, n * rs + 16))) return s;
+            if ((s = ensure_pooled(c, *o, n * rs + 16))) return s;
             std::vector<std::pair<const void*, uint64_t>> next;
             uint64_t off = 0;
             for (size_t r = 0; r < runs.size(); r += 2) {
@@ -2707,6 +2827,12 @@ static kc_status cut_run(kc_ctx* c) {
     if ((s = finish_part(c, &n))) return s;  // fin_packed
     HIPCHK(c, hipStreamSynchronize(c->stream));
     kc::trace("cut_run: %llu records finished in %.3f ms", (unsigned long long)n, (kc::now_s() - t0) * 1e3);
+    return keep_finished_run(c, n);
+}
+
+// fin_packed (n finished records) becomes a sorted run and the record state
+// starts empty
+static kc_status keep_finished_run(kc_ctx* c, uint64_t n) {
     const size_t bytes = (size_t)n * c->rs;
     if (n) {
         // the run takes over fin_packed's buffer (no copy); fin_packed gets a

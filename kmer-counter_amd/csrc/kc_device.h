@@ -155,7 +155,14 @@ hipError_t launch_sort_runs(int W, const uint64_t* keys, uint64_t stride, const 
                             uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* stats, uint64_t* desc_key, uint64_t* desc_start,
                             uint32_t* desc_len, uint64_t desc_cap, uint8_t* run_flags, uint8_t* bucket_flags,
-                            uint32_t* nflag, int grid, hipStream_t s);
+                            uint32_t* nflag, int grid, hipStream_t s, void* packed = nullptr,
+                            uint64_t pk_base = 0);
+// Direct mode (packed != nullptr): records go to packed + (pk_base + run's first
+// key + rank) records of 2W+1 u32; *rec_cursor counts them (fewer than the keys
+// when runs held equal keys: then launch_packed_seg_copy closes the gaps).
+hipError_t launch_packed_seg_copy(int W, const void* src, void* dst, const uint32_t* order, const uint64_t* dstart,
+                                  const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc, uint64_t base,
+                                  int grid, hipStream_t s);
 // Starts of the 256 sub-buckets per region after a regional radix pass by key
 // bits 40..47 (rp_hist/rp_scatter over nreg regions): nreg * 256 + 1 entries
 hipError_t launch_sub_starts(const uint64_t* rstart, const uint64_t* tpre, const uint64_t* pos, uint32_t nreg,

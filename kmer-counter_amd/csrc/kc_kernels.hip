@@ -2279,7 +2279,21 @@ struct SortRunArgs {
     unsigned char* run_flags;     // nbuckets * 256
     unsigned char* bucket_flags;  // nbuckets
     u32* nflag;                   // runs flagged
+    u32* packed;                  // direct mode: SortedKMerFile records at pk_base + (run's first key) + rank
+    u64 pk_base;
 };
+
+// one SortedKMerFile record (W LE u64 words + LE u32 count) at index pos
+template <int W>
+__device__ __forceinline__ void put_packed(u32* __restrict__ packed, u64 pos, const u64 (&k)[W], u32 cnt) {
+    u32* o = packed + pos * (2 * W + 1);
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        o[2 * j] = (u32)k[j];
+        o[2 * j + 1] = (u32)(k[j] >> 32);
+    }
+    o[2 * W] = cnt;
+}
 
 template <int W>
 __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
@@ -2451,6 +2465,27 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
             if (dup) misc[23] = 1u;
             __syncthreads();
             SR_MARK(5);
+            if (!uni32(misc[23]) && a.packed) {
+                // direct mode, distinct keys: the run's records are its keys,
+                // each written to its place in the finished packed run (the
+                // run starts at its first key's position: no reservation)
+                const u64 rbase = a.pk_base + lo;
+                if (tid == 0) {
+                    atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)len);
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                    const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
+                    if (di < a.desc_cap) {
+                        a.desc_key[di] = ((u64)b << 48) | base;
+                        a.desc_start[di] = rbase;
+                        a.desc_len[di] = len | ((u32)(sh + 1) << 24) | (1u << 31);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < R; i++)
+                    if ((u32)tid + (u32)i * kSrBlock < len) put_packed<W>(a.packed, rbase + pos[i], k[i], 1u);
+                SR_MARK(8);
+                continue;
+            }
             if (!uni32(misc[23])) {
                 // distinct keys (the high-cardinality case): records are the
                 // keys, each written straight to its sorted place, count 1
@@ -2530,10 +2565,16 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
                 if (x1 < NV) bins[x1] = ex + v0;
                 const u32 run = __shfl(inc, 63);
                 if (lane == 0) {
-                    const u64 rbase = atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)run);
+                    u64 rbase;
+                    if (a.packed) {  // direct mode: the run's place; gaps are compacted later
+                        rbase = a.pk_base + lo;
+                        atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)run);
+                    } else {
+                        rbase = atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)run);
+                        if (rbase + run > a.rec_cap)
+                            atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                    }
                     *(u64*)(misc + 20) = rbase;
-                    if (rbase + run > a.rec_cap)
-                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
                     atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
                     const u64 di = atomicAdd((unsigned long long*)&a.stats[ST_DESC_FILL], 1ull);
                     if (di < a.desc_cap) {
@@ -2559,7 +2600,12 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
                     q++;
                 }
                 const u64 r = rbase + bins[i * kSrWaves + wave] + hb[i];
-                if (r < a.rec_cap) {
+                if (a.packed) {
+                    u64 kk[W];
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) kk[jj] = skey[(size_t)jj * SP + p];
+                    put_packed<W>(a.packed, r, kk, q - p);
+                } else if (r < a.rec_cap) {
 #pragma unroll
                     for (int jj = 0; jj < W; jj++) a.rec_keys[(u64)jj * a.rec_cap + r] = skey[(size_t)jj * SP + p];
                     a.rec_cnts[r] = q - p;
@@ -2584,8 +2630,10 @@ hipError_t launch_sort_runs(int W, const uint64_t* keys, uint64_t stride, const 
                             uint32_t nbuckets, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* stats, uint64_t* desc_key, uint64_t* desc_start,
                             uint32_t* desc_len, uint64_t desc_cap, uint8_t* run_flags, uint8_t* bucket_flags,
-                            uint32_t* nflag, int grid, hipStream_t s) {
+                            uint32_t* nflag, int grid, hipStream_t s, void* packed, uint64_t pk_base) {
     SortRunArgs a;
+    a.packed = (u32*)packed;
+    a.pk_base = pk_base;
     a.keys = keys;
     a.stride = stride;
     a.sub_starts = sub_starts;
@@ -2610,6 +2658,33 @@ hipError_t launch_sort_runs(int W, const uint64_t* keys, uint64_t stride, const 
     case 4: hipLaunchKernelGGL(sort_runs_k<4>, dim3(grid), dim3(kSrBlock), lds, s, a); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// Compaction of a packed run written in place by sort_runs_k (direct mode)
+// whose runs held equal keys: segment order[d] (start dstart, records
+// dlen & 0xffffff) moves to out_off[d] (u32 copies, one block per segment).
+__global__ __launch_bounds__(kBlock) void packed_seg_copy_k(const u32* __restrict__ src, u32* __restrict__ dst, int rw,
+                                                            const u32* __restrict__ order,
+                                                            const u64* __restrict__ dstart,
+                                                            const u32* __restrict__ dlen,
+                                                            const u64* __restrict__ out_off, u64 ndesc, u64 base) {
+    for (u64 d = blockIdx.x; d < ndesc; d += gridDim.x) {
+        const u32 o = order[d];
+        const u64 st = dstart[o];
+        const u32 len = dlen[o] & 0xffffffu;
+        const u64 ob = base + out_off[d];
+        const u32 nw = len * (u32)rw;
+        for (u32 x = threadIdx.x; x < nw; x += kBlock) dst[ob * (u64)rw + x] = src[st * (u64)rw + x];
+    }
+}
+
+hipError_t launch_packed_seg_copy(int W, const void* src, void* dst, const uint32_t* order, const uint64_t* dstart,
+                                  const uint32_t* dlen, const uint64_t* out_off, uint64_t ndesc, uint64_t base,
+                                  int grid, hipStream_t s) {
+    if (ndesc == 0) return hipSuccess;
+    hipLaunchKernelGGL(packed_seg_copy_k, dim3(grid), dim3(kBlock), 0, s, (const u32*)src, (u32*)dst, 2 * W + 1,
+                       order, dstart, dlen, out_off, ndesc, base);
     return hipGetLastError();
 }
 

@@ -477,13 +477,14 @@ def test_presplit_buckets_high_cardinality(kca, orc, monkeypatch, k):
     were mostly distinct, the next batches split every bucket once more by key
     bits 40..47 (P3b, an MSD regional radix pass) and P5 counts runs of
     consecutive sub-buckets in one pass each; the runs cut from the records
-    merge on the device. Runs of sub-buckets are sorted in LDS (P5s); the
-    LDS hash table for every run (KC_NO_SORT_RUNS) and no P3b pass
-    (KC_NO_P3B) give the same bytes as the oracle."""
+    merge on the device. Runs of sub-buckets are sorted in LDS (P5s), into
+    records or (KC_P5S_DIRECT_MIN=1) straight into each batch's finished
+    packed run; the LDS hash table for every run (KC_NO_SORT_RUNS) and no P3b
+    pass (KC_NO_P3B) give the same bytes as the oracle."""
     monkeypatch.setenv("KC_P3B_MIN", "1")
     fq = kca.synth_fastq(30000, 150, seed=k + 3, n_rate=0.0005)
     outs = []
-    for env in ((), ("KC_NO_SORT_RUNS",), ("KC_NO_P3B",)):
+    for env in ((), ("KC_P5S_DIRECT_MIN",), ("KC_NO_SORT_RUNS",), ("KC_NO_P3B",)):
         for v in env:
             monkeypatch.setenv(v, "1")
         with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=24 << 20, engine="partition") as ctx:
@@ -493,7 +494,35 @@ def test_presplit_buckets_high_cardinality(kca, orc, monkeypatch, k):
         assert st["batches"] >= 3
         for v in env:
             monkeypatch.delenv(v)
-    assert outs[0] == outs[1] == outs[2] == orc.count_fastq(fq, k)
+    assert outs[0] == outs[1] == outs[2] == outs[3] == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_direct_runs_with_equal_keys(kca, orc, monkeypatch, capfd, k):
+    """P5s direct mode on batches whose runs hold equal keys (a fifth of the
+    reads repeat earlier reads, so k-mers occur several times while most are
+    distinct): the runs leave gaps in the packed run, which a segment copy
+    closes. Key 0 (an all-A read) takes record 0. Same bytes as the oracle;
+    the direct path is seen in the debug line."""
+    import numpy as np
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    monkeypatch.setenv("KC_P5S_DIRECT_MIN", "1")
+    monkeypatch.setenv("KC_DEBUG", "1")
+    rng = np.random.default_rng(k + 11)
+    L = 150
+    reads = rng.integers(0, 4, size=(40000, L), dtype=np.uint8)
+    rep = rng.integers(0, 40000, size=8000)
+    reads[32000:] = reads[rep]
+    reads[5] = 0
+    fq = _fastq_from_codes(reads[rng.permutation(len(reads))])
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=24 << 20, engine="partition") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+    err = capfd.readouterr().err
+    kept = [x for x in err.splitlines() if "kc: P5s direct" in x and "kept=1" in x]
+    gaps = [x for x in kept if int(x.split("records=")[1].split()[0]) < int(x.split(" n=")[1].split()[0])]
+    assert kept and gaps, err[-2000:]
+    assert got == orc.count_fastq(fq, k)
 
 
 def _fastq_from_codes(codes):
@@ -528,7 +557,7 @@ def test_sorted_runs_hand_off_to_hash_path(kca, orc, monkeypatch, capfd, k):
         ctx.count_fastq(fq)
         got = ctx.records()
     err = capfd.readouterr().err
-    flagged = [int(x.split("flagged=")[1].split()[0]) for x in err.splitlines() if "kc: P5s" in x]
+    flagged = [int(x.split("flagged=")[1].split()[0]) for x in err.splitlines() if "kc: P5s" in x and "flagged=" in x]
     assert flagged and max(flagged) > 0, err[-2000:]
     assert got == orc.count_fastq(fq, k)
 
