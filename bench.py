@@ -614,8 +614,10 @@ def host_variants(kca, ctx, args, host, nbytes, out_path, k, L):
         ctx.count_chunk_host(base, sbytes, L)
         ctx.finish()
 
-    tc = one(chunks_step)
-    tb = one(block_step)
+    # best of 3 after a warm run, both ways alike (a single host-side rep
+    # varies by tens of ms from run to run on the shared host)
+    tc = one(chunks_step, reps=3)
+    tb = one(block_step, reps=3)
     res["reference_chunks"] = {"chunk_bytes": cs, "chunks": (sbytes + cs - 1) // cs,
                                "value_chunks": win / tc, "ms_chunks": tc * 1e3,
                                "value_one_block": win / tb, "ms_one_block": tb * 1e3,

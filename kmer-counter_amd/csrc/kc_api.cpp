@@ -9,6 +9,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -116,6 +117,16 @@ struct kc_ctx {
     hipEvent_t stage_free[2] = {nullptr, nullptr};  // kc_count_chunk: the encode of the staged chunk is done
     DevBuf file_stage[2];
     int chunk_slot = 0;
+    // kc_count_chunk accumulation: whole reads of consecutive chunks copied
+    // into one of two pinned buffers, uploaded and encoded when it fills (or
+    // before anything else counts, finishes or checkpoints)
+    char* acc_buf[2] = {nullptr, nullptr};
+    hipEvent_t acc_ev[2] = {nullptr, nullptr};
+    bool acc_busy[2] = {false, false};
+    size_t acc_n = 0;
+    int acc_i = 0;
+    int64_t acc_L = 0;
+    double acc_t[4] = {0, 0, 0, 0};  // KC_TRACE: host copy, buffer wait, flush, calls (s)
 
     // Pending batch: reads already indexed and 2-bit encoded into part_codes /
     // part_inval (/ part_rlen) by kc_count_* calls, counted together at the
@@ -1252,7 +1263,15 @@ static kc_status grow_keep(kc_ctx* c, DevBuf& b, size_t bytes, size_t keep) {
 static kc_status cut_run_if_full(kc_ctx* c);
 
 // Counts the pending batch (the engines: count_reads with pre-encoded reads).
+extern "C" {
+static kc_status chunk_acc_flush(kc_ctx* c);  // defined with the chunk entry points (C linkage block)
+}
+
 static kc_status pend_flush(kc_ctx* c) {
+    if (c->acc_n) {
+        kc_status s0 = chunk_acc_flush(c);
+        if (s0) return s0;
+    }
     if (c->pend_reads == 0) return KC_OK;
     kc::trace("flush %llu reads of length %lld", (unsigned long long)c->pend_reads, (long long)c->pend_L);
     const uint64_t n = c->pend_reads;
@@ -1585,6 +1604,10 @@ void kc_destroy(kc_ctx* c) {
     delete c->pool;
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (char* b : c->file_bufs) (void)hipHostFree(b);
+    for (int i = 0; i < 2; i++) {
+        if (c->acc_buf[i]) (void)hipHostFree(c->acc_buf[i]);
+        if (c->acc_ev[i]) (void)hipEventDestroy(c->acc_ev[i]);
+    }
     for (auto& b : c->file_stage) release(b);
     for (auto& e : c->file_ev)
         if (e) (void)hipEventDestroy(e);
@@ -1668,6 +1691,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->pend_reads = 0;
     c->pend_L = 0;
     c->pend_var = false;
+    c->acc_n = 0;  // (a DMA still reading a buffer is waited for before it is refilled)
     c->ckpt = false;
     c->finished = false;
     c->n_records = 0;
@@ -1678,7 +1702,14 @@ kc_status kc_reset(kc_ctx* c) {
 
 // Host staging (pinned ring + copy pool), created on first use.
 static kc_status stage_init(kc_ctx* c) {
-    if (!c->pool) c->pool = new kc::Pool(8);
+    if (!c->pool) {
+        // host copy threads: the CPUs this process may run on, at most 16 (the
+        // GPU box's cgroup quota; its affinity mask shows every core)
+        cpu_set_t cs;
+        int n = 8;
+        if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+        c->pool = new kc::Pool(std::max(2, std::min(16, n)));
+    }
     if (!c->ring) {
         c->ring = new kc::PinnedRing();
         HIPCHK(c, c->ring->init((size_t)64 << 20, 4));
@@ -1689,7 +1720,7 @@ static kc_status stage_init(kc_ctx* c) {
 // Reference-exact chunk in device memory: floor(size / L) reads at stride L
 // (GPUHandler.cu:13-15), encoded into the pending batch (codes engines) or
 // counted from the text (table engine).
-static kc_status chunk_device(kc_ctx* c, const uint8_t* d, int64_t size, int64_t L) {
+static kc_status chunk_device(kc_ctx* c, const uint8_t* d, int64_t size, int64_t L, bool add_stats = true) {
     if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     const uint64_t n = (uint64_t)(size / L);
     if (n == 0) return KC_OK;
@@ -1700,8 +1731,10 @@ static kc_status chunk_device(kc_ctx* c, const uint8_t* d, int64_t size, int64_t
         if ((s = pend_flush(c))) return s;
         if ((s = count_reads(c, d, nullptr, n, L))) return s;
     }
-    c->st.reads += n;
-    c->st.windows += n * (uint64_t)(L - c->k + 1);
+    if (add_stats) {
+        c->st.reads += n;
+        c->st.windows += n * (uint64_t)(L - c->k + 1);
+    }
     return KC_OK;
 }
 
@@ -1710,6 +1743,7 @@ kc_status kc_count_chunk_device(kc_ctx* c, const void* d_chunk, int64_t size, in
     kc_status s = check_line(c, L);
     if (s) return s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if ((s = chunk_acc_flush(c))) return s;
     if ((s = chunk_device(c, (const uint8_t*)d_chunk, size, L))) return s;
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's buffer was read by the encoder
     return KC_OK;
@@ -1723,12 +1757,54 @@ static kc_status copy_stream_init(kc_ctx* c) {
     return KC_OK;
 }
 
-// Host chunk: its whole reads go through the pinned ring into one of two
-// staging buffers on the copy stream, the encode waits for that upload on
-// the ctx stream; the call returns as soon as the caller's bytes are in
-// pinned memory. Chunk i + 1 therefore uploads while chunk i is encoded, and
-// consecutive chunks (the reference's ~7.8 MB at gpuMemoryLimit=1e8,
-// KMerCounter.cpp:193-212) stream at the PCIe rate.
+// One staged upload + encode of host bytes (whole reads of length L): through
+// the pinned ring (pageable source) or straight from a pinned buffer, into one
+// of two staging buffers on the copy stream; the encode waits for that upload
+// on the ctx stream, so the next upload overlaps this encode.
+static kc_status chunk_upload_count(kc_ctx* c, const char* src, size_t bytes, int64_t L, bool pinned_src,
+                                    hipEvent_t src_done, bool add_stats) {
+    kc_status s;
+    const int slot = c->chunk_slot;
+    c->chunk_slot ^= 1;
+    DevBuf& st = c->file_stage[slot];
+    if (st.bytes < bytes + 64) {
+        // growing: nothing may still read or write the old buffer
+        HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+        if ((s = ensure(c, st, bytes + 64))) return s;
+    }
+    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->stage_free[slot], 0));
+    if (pinned_src) {
+        HIPCHK(c, hipMemcpyAsync(st.p, src, bytes, hipMemcpyHostToDevice, c->copy_stream));
+        if (src_done) HIPCHK(c, hipEventRecord(src_done, c->copy_stream));
+    } else {
+        HIPCHK(c, c->ring->upload(st.p, src, bytes, c->copy_stream, c->pool));
+    }
+    HIPCHK(c, hipEventRecord(c->file_ev[slot], c->copy_stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->file_ev[slot], 0));
+    if ((s = chunk_device(c, (const uint8_t*)st.p, (int64_t)bytes, L, add_stats))) return s;
+    HIPCHK(c, hipEventRecord(c->stage_free[slot], c->stream));
+    return KC_OK;
+}
+
+static const size_t kAccBytes = (size_t)64 << 20;
+
+// Uploads and counts the accumulated chunk reads (kc_count_chunk), if any.
+static kc_status chunk_acc_flush(kc_ctx* c) {
+    if (!c->acc_n) return KC_OK;
+    const size_t bytes = c->acc_n;
+    const int i = c->acc_i;
+    c->acc_n = 0;  // first: counting may flush the pending batch, which comes back here
+    c->acc_i ^= 1;
+    c->acc_busy[i] = true;
+    return chunk_upload_count(c, c->acc_buf[i], bytes, c->acc_L, true, c->acc_ev[i], false);
+}
+
+// Host chunk (the reference's readData output, KMerCounter.cpp:193-212: ~7.8
+// MB at gpuMemoryLimit=1e8): its whole reads are copied into the pinned
+// accumulation buffer (the call returns once the caller's bytes are copied);
+// a full buffer (64 MB, about 8 such chunks) is uploaded and encoded while the
+// next one fills, so per chunk the cost is the host copy and no device call.
+// A chunk larger than half the buffer goes through the pinned ring directly.
 kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) {
     if (!c || (!chunk && size > 0) || size < 0) return KC_ERR_ARG;
     kc_status s = check_line(c, L);
@@ -1739,20 +1815,39 @@ kc_status kc_count_chunk(kc_ctx* c, const char* chunk, int64_t size, int64_t L) 
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if ((s = stage_init(c)) || (s = copy_stream_init(c))) return s;
     const size_t bytes = (size_t)(n * (uint64_t)L);
-    const int slot = c->chunk_slot;
-    c->chunk_slot ^= 1;
-    DevBuf& st = c->file_stage[slot];
-    if (st.bytes < bytes + 64) {
-        // growing: nothing may still read or write the old buffer
-        HIPCHK(c, hipStreamSynchronize(c->copy_stream));
-        if ((s = ensure(c, st, bytes + 64))) return s;
+    const bool tr = kc::trace_on();
+    double t0 = tr ? kc::now_s() : 0;
+    if (tr) c->acc_t[3] += 1;
+    if (c->acc_n && (c->acc_L != L || c->acc_n + bytes > kAccBytes))
+        if ((s = chunk_acc_flush(c))) return s;
+    if (tr) {
+        const double t = kc::now_s();
+        c->acc_t[2] += t - t0;
+        t0 = t;
     }
-    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->stage_free[slot], 0));
-    HIPCHK(c, c->ring->upload(st.p, chunk, bytes, c->copy_stream, c->pool));
-    HIPCHK(c, hipEventRecord(c->file_ev[slot], c->copy_stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->file_ev[slot], 0));
-    if ((s = chunk_device(c, (const uint8_t*)st.p, (int64_t)bytes, L))) return s;
-    HIPCHK(c, hipEventRecord(c->stage_free[slot], c->stream));
+    if (bytes > kAccBytes / 2) return chunk_upload_count(c, chunk, bytes, L, false, nullptr, true);
+    const int i = c->acc_i;
+    if (!c->acc_buf[i]) {
+        HIPCHK(c, hipHostMalloc((void**)&c->acc_buf[i], kAccBytes, hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->acc_ev[i], hipEventDisableTiming));
+    }
+    if (c->acc_n == 0) {
+        if (c->acc_busy[i]) {  // its previous upload must be done before it is refilled
+            HIPCHK(c, hipEventSynchronize(c->acc_ev[i]));
+            c->acc_busy[i] = false;
+        }
+        c->acc_L = L;
+    }
+    if (tr) {
+        const double t = kc::now_s();
+        c->acc_t[1] += t - t0;
+        t0 = t;
+    }
+    kc::par_memcpy(c->pool, c->acc_buf[i] + c->acc_n, chunk, bytes);
+    if (tr) c->acc_t[0] += kc::now_s() - t0;
+    c->acc_n += bytes;
+    c->st.reads += n;
+    c->st.windows += n * (uint64_t)(L - c->k + 1);
     return KC_OK;
 }
 
@@ -1766,6 +1861,7 @@ static kc_status fastq_device(kc_ctx* c, const void* d_fastq, uint64_t n, int64_
     kc_status s = check_line(c, L);
     if (s) return s;
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (count && (s = chunk_acc_flush(c))) return s;
     return ingest_fastq(c, (const uint8_t*)d_fastq, n, L, (c->cfg.flags & KC_FLAG_VARLEN) != 0, count, n_reads);
 }
 
@@ -1952,6 +2048,10 @@ extern "C" kc_status kc_count_file(kc_ctx* const* ctxs, uint32_t n_ctx, const ch
     if (L < c0->k) return KC_OK;
     kc_status s = check_line(c0, L);
     if (s) return s;
+    for (uint32_t g = 0; g < n_ctx; g++) {  // chunks accumulated by kc_count_chunk are counted first
+        HIPCHK(ctxs[g], hipSetDevice(ctxs[g]->cfg.device));
+        if ((s = chunk_acc_flush(ctxs[g]))) return s;
+    }
     uint64_t reads = 0;
     kc_ctx* failed = nullptr;
     if (mode == KC_INPUT_EXACT) {
@@ -2014,7 +2114,9 @@ kc_status kc_checkpoint(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
     if (c->finished) return fail(c, KC_ERR_STATE, "kc_finish was called; kc_reset first");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    kc_status s = sync_stats(c);
+    kc_status s = chunk_acc_flush(c);  // accumulated chunks are counted before the checkpoint
+    if (s) return s;
+    s = sync_stats(c);
     if (s) return s;
     c->ckpt = true;
     c->ckpt_reads = c->pend_reads;
@@ -2343,6 +2445,11 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     HIPCHK(c, hipSetDevice(c->cfg.device));
     kc_status s;
     c->ckpt = false;
+    if (c->acc_t[3] > 0) {
+        kc::trace("chunk calls %.0f: host copy %.3f ms, buffer waits %.3f ms, flushes %.3f ms", c->acc_t[3],
+                  c->acc_t[0] * 1e3, c->acc_t[1] * 1e3, c->acc_t[2] * 1e3);
+        for (double& x : c->acc_t) x = 0;
+    }
     if ((s = pend_flush(c))) return s;
     if ((s = sync_stats(c))) return s;
     if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;

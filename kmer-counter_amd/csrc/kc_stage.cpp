@@ -54,19 +54,28 @@ void Pool::loop() {
     uint64_t seen = 0;
     for (;;) {
         const std::function<void(int)>* fn;
+        // back-to-back jobs (a caller's consecutive chunk copies) find the
+        // worker spinning for ~100 us before it sleeps on the condition
+        for (int spin = 0; spin < 20000 && gen_.load(std::memory_order_acquire) == seen &&
+                           !stop_.load(std::memory_order_relaxed);
+             spin++)
+            __builtin_ia32_pause();
         {
             std::unique_lock<std::mutex> g(m_);
-            cv_.wait(g, [&]() { return stop_ || gen_ != seen; });
+            cv_.wait(g, [&]() { return stop_.load() || gen_.load() != seen; });
             if (stop_) return;
-            seen = gen_;
+            seen = gen_.load();
             fn = fn_;
             busy_++;
         }
         for (;;) {
             int i;
             {
+                // only pieces of the job this worker joined: a worker that
+                // joined after its job ended (fn null) must not take pieces of
+                // the next one, whose counters the caller has reset
                 std::lock_guard<std::mutex> g(m_);
-                if (next_ >= n_) break;
+                if (!fn || gen_.load() != seen || next_ >= n_) break;
                 i = next_++;
             }
             (*fn)(i);
@@ -108,8 +117,10 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
 }
 
 void par_memcpy(Pool* pool, void* dst, const void* src, size_t n) {
-    const size_t kPiece = (size_t)1 << 20;
-    int parts = pool ? (int)std::min<size_t>((size_t)pool->size(), (n + kPiece - 1) / kPiece) : 1;
+    const size_t kPiece = (size_t)1 << 18;
+    int parts = 1;
+    if (pool && n > kPiece)
+        parts = n <= ((size_t)64 << 20) ? (int)((n + kPiece - 1) / kPiece) : pool->size();
     if (parts <= 1) {
         memcpy(dst, src, n);
         return;

@@ -23,6 +23,7 @@
 
 #include <condition_variable>
 #include <functional>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -51,11 +52,12 @@ class Pool {
     std::condition_variable cv_, done_cv_;
     const std::function<void(int)>* fn_ = nullptr;
     int n_ = 0, next_ = 0, busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::atomic<uint64_t> gen_{0};  // job generation (written under m_, spun on without it)
+    std::atomic<bool> stop_{false};
 };
 
-// memcpy of n bytes split over the pool (pieces of >= 4 MiB)
+// memcpy of n bytes split over the pool: 256 KiB pieces up to 64 MiB (late
+// workers take fewer pieces), else one equal part per thread
 void par_memcpy(Pool* pool, void* dst, const void* src, size_t n);
 
 // true when p is pinned (hipHostMalloc'ed or registered) host memory

@@ -228,3 +228,22 @@ def test_python_options_mirror_reference_defaults(kca, orc):
         assert int(d["kmerLength"]) == o.GetKmerLength()
         assert int(d["noOfMergersAtOnce"]) == o.getNoOfMergersAtOnce()
         assert int(d["noOfMergeThreads"]) == o.getNoOfMergeThreads()
+
+
+def test_pool_par_memcpy_stress(tmp_path):
+    """kc_stage's copy pool: par_memcpy of mixed sizes (100 B .. 64 MiB + odd
+    tails) back to back through a 16-thread Pool, byte-exact (a worker that
+    joined a finished job must not take pieces of the next one)."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++") or not os.path.exists("/opt/rocm/lib/libamdhip64.so"):
+        pytest.skip("g++ or the HIP runtime library missing")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "pool_stress")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "kmer-counter_amd", "csrc"),
+                    "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-pthread",
+                    os.path.join(root, "tools", "pool_stress.cpp"),
+                    os.path.join(root, "kmer-counter_amd", "csrc", "kc_stage.cpp"), "-L/opt/rocm/lib",
+                    "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stdout + out.stderr

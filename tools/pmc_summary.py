@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Summarise the PMC passes of tools/gpu_pmc.sh per kernel (per launch) and
-write profiles/pmc_count_kmers.json for bench.py's roofline.traffic.
+write profiles/<name> (default pmc_count_kmers.json, which bench.py's
+roofline.traffic reads) — args: out_dir reads k [name].
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (FETCH_SIZE is in KiB and
 reports half the bytes of wide streaming reads on gfx950, MI355X_MICROARCH.md
@@ -43,6 +44,7 @@ for name, n, per in rows:
                                   "SQ_INSTS_VMEM_WR", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
                                   "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE")))
 k = int(sys.argv[3]) if len(sys.argv) > 3 else 31
+name_out = sys.argv[4] if len(sys.argv) > 4 else "pmc_count_kmers.json"
 W = (k + 31) // 32
 rec = {"reads_per_gpu": reads, "k": k, "kernels": {},
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, --kernel-trace only "
@@ -65,7 +67,7 @@ for name, n, per in rows:
     rec["kernels"][short(name)] = {"kernel": name, "bytes_per_launch": rd + wr, "read_bytes": rd,
                                    "write_bytes": wr, "launches": n}
 os.makedirs("profiles", exist_ok=True)
-json.dump(rec, open("profiles/pmc_count_kmers.json", "w"), indent=1)
-json.dump(rec, open(os.path.join(out, "pmc_count_kmers.json"), "w"), indent=1)  # travels back from the box
-print("wrote profiles/pmc_count_kmers.json", {t: round(v["bytes_per_launch"] / 1e9, 2) for t, v in rec["kernels"].items()
+json.dump(rec, open(os.path.join("profiles", name_out), "w"), indent=1)
+json.dump(rec, open(os.path.join(out, name_out), "w"), indent=1)  # travels back from the box
+print("wrote profiles/" + name_out, {t: round(v["bytes_per_launch"] / 1e9, 2) for t, v in rec["kernels"].items()
                                              if v["bytes_per_launch"] > 1e8})
