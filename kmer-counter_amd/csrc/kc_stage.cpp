@@ -55,7 +55,7 @@ void Pool::loop() {
     for (;;) {
         const std::function<void(int)>* fn;
         // back-to-back jobs (a caller's consecutive chunk copies) find the
-        // worker spinning for ~100 us before it sleeps on the condition
+        // worker spinning (up to ~0.5 ms) before it sleeps on the condition
         for (int spin = 0; spin < 20000 && gen_.load(std::memory_order_acquire) == seen &&
                            !stop_.load(std::memory_order_relaxed);
              spin++)
@@ -120,7 +120,7 @@ void par_memcpy(Pool* pool, void* dst, const void* src, size_t n) {
     const size_t kPiece = (size_t)1 << 18;
     int parts = 1;
     if (pool && n > kPiece)
-        parts = n <= ((size_t)64 << 20) ? (int)((n + kPiece - 1) / kPiece) : pool->size();
+        parts = n <= ((size_t)8 << 20) ? (int)((n + kPiece - 1) / kPiece) : pool->size();
     if (parts <= 1) {
         memcpy(dst, src, n);
         return;

@@ -56,7 +56,7 @@ class Pool {
     std::atomic<bool> stop_{false};
 };
 
-// memcpy of n bytes split over the pool: 256 KiB pieces up to 64 MiB (late
+// memcpy of n bytes split over the pool: 256 KiB pieces up to 8 MiB (late
 // workers take fewer pieces), else one equal part per thread
 void par_memcpy(Pool* pool, void* dst, const void* src, size_t n);
 
