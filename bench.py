@@ -372,7 +372,7 @@ def main():
         dev_step()
     D.barrier_sync()
     xch_ms[0] = 0.0
-    acc = {"insert_ms": 0.0, "finish_ms": 0.0, "decode_ms": 0.0, "dedup_ms": 0.0, "launches": 0,
+    acc = {"insert_ms": 0.0, "finish_ms": 0.0, "decode_ms": 0.0, "dedup_ms": 0.0, "presplit_ms": 0.0, "launches": 0,
            "part_ms": [0.0] * 5}
     t0 = time.perf_counter()
     n_rec = 0
@@ -384,6 +384,7 @@ def main():
         acc["finish_ms"] += st["finish_ms"]
         acc["decode_ms"] += st["decode_ms"]
         acc["dedup_ms"] += st.get("dedup_ms", 0.0)
+        acc["presplit_ms"] += st.get("presplit_ms", 0.0)
         acc["part_ms"] = [a + b for a, b in zip(acc["part_ms"], st["part_ms"])]
     D.barrier_sync()
     dev_el = D.max(time.perf_counter() - t0)
@@ -435,7 +436,8 @@ def main():
                                   "finish": acc["finish_ms"] / args.steps,
                                   "exchange_rank0": xch_ms[0] / args.steps,
                                   "partition_passes": [round(x / args.steps, 3) for x in acc["part_ms"]],
-                                  "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3)},
+                                  "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3),
+                                  "p3b_presplit (in partition_passes[2])": round(acc["presplit_ms"] / args.steps, 3)},
     }
     if args.mode == "e2e":
         value, ms = e2e["value"], e2e["ms_per_step"]
@@ -515,13 +517,25 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
     elif used & 2:
         keys_step = st["keys"] or windows_step
         p5_per_step = max(1, st["p5_launches"])
+        nb = max(1, st["batches"])
+        pre_b = st.get("presplit_batches", 0)
+        pre_ms = acc["presplit_ms"]
         specs = [
             ("P2", f"count_front<{W},2,true,1024>", part_ms[1], acc["launches"], windows_step,
              "k-mers", (G * 6) / max(1, L - k + 1) + 8 * W),
-            ("P3", f"p3_scatter_k<{W}>", part_ms[2], steps * st["batches"], keys_step, "keys", 16 * W),
-            ("P5", f"count_buckets<{W}>", part_ms[4], steps * p5_per_step, keys_step, "keys",
-             8 * W + (8 * W + 4) * recs_step / max(1, keys_step)),
+            ("P3", f"p3_scatter_k<{W}>", part_ms[2] - pre_ms, steps * st["batches"], keys_step, "keys", 16 * W),
         ]
+        if pre_b:
+            # P3b: word 0 read for the regional histogram + one scatter pass
+            specs.append(("P3b", f"rp_upsweep_k + rp_scatter_k<{W},false>", pre_ms, steps * pre_b,
+                          keys_step * pre_b / nb, "keys", 8 + 16 * W))
+        if st.get("sorted_run_batches", 0):
+            # P5s: keys read once, records written (packed, or SoA + segment copy)
+            specs.append(("P5", f"sort_runs_k<{W}>", part_ms[4], steps * p5_per_step, keys_step, "keys",
+                          8 * W + (8 * W + 4) * recs_step / max(1, keys_step)))
+        else:
+            specs.append(("P5", f"count_buckets<{W}>", part_ms[4], steps * p5_per_step, keys_step, "keys",
+                          8 * W + (8 * W + 4) * recs_step / max(1, keys_step)))
     else:
         specs = [("insert", f"count_front<{W},0,false,256>", acc["insert_ms"], acc["launches"], windows_step,
                   "k-mers", nbytes / windows_step + 8 * W + 8)]
@@ -537,14 +551,16 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
     dom = max(kernels, key=lambda t: kernels[t]["ms_per_step"])
     d = kernels[dom]
     t_bytes = None
-    p = os.path.join(ROOT, "profiles", "pmc_count_kmers.json")
-    try:
-        traffic = json.load(open(p))
-    except (OSError, ValueError):
-        traffic = None
-    # (the committed PMC summary is of the fixed-length cfg2 run)
-    if traffic and not varlen and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
-        t_bytes = traffic.get("kernels", {}).get(d["kernel"].replace(" ", ""), {}).get("bytes_per_launch")
+    # the committed PMC summaries (cfg2: pmc_count_kmers.json, cfg5:
+    # pmc_cfg5.json), used when they are of this workload (reads, k)
+    for fname in ("pmc_count_kmers.json", "pmc_cfg5.json"):
+        try:
+            traffic = json.load(open(os.path.join(ROOT, "profiles", fname)))
+        except (OSError, ValueError):
+            continue
+        if not varlen and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
+            t_bytes = traffic.get("kernels", {}).get(d["kernel"].replace(" ", ""), {}).get("bytes_per_launch")
+            break
     b_path = nbytes / windows_step + 8 * W + 8
     path_achieved = b_path * windows_step / (dev_el / steps) / 1e9
     return {"bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -56,8 +56,9 @@
 extern "C" {
 #endif
 
-#define KC_ABI_VERSION 4 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
-                            4: kc_count_file, kc_checkpoint / kc_rollback / kc_commit */
+#define KC_ABI_VERSION 5 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
+                            4: kc_count_file, kc_checkpoint / kc_rollback / kc_commit;
+                            5: kc_stats.presplit_ms / presplit_batches / sorted_run_batches */
 #define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
 
 typedef enum kc_status {
@@ -157,6 +158,13 @@ typedef struct kc_stats {
                                   P5a (identical records of a bucket counted once);
                                   part_ms[4] is then the weighted P5 walk alone */
     uint64_t dedup_records;    /* distinct records P5a listed since the last reset */
+    double presplit_ms;        /* key-prefix engine, high cardinality: summed device
+                                  time of P3b (every bucket split by key bits 40..47:
+                                  histogram, scatter, sub-bucket starts); included in
+                                  part_ms[2] */
+    uint64_t presplit_batches; /* batches that took P3b */
+    uint64_t sorted_run_batches; /* batches counted by P5s (runs of sub-buckets sorted
+                                    in LDS; part_ms[4] holds their time) */
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". (ABI 4: layout) */

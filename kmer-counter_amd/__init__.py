@@ -84,6 +84,9 @@ class Stats(ctypes.Structure):
         ("reserved1", ctypes.c_uint32),
         ("dedup_ms", ctypes.c_double),
         ("dedup_records", ctypes.c_uint64),
+        ("presplit_ms", ctypes.c_double),
+        ("presplit_batches", ctypes.c_uint64),
+        ("sorted_run_batches", ctypes.c_uint64),
     ]
 
     def as_dict(self):

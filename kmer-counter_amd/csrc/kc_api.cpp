@@ -95,6 +95,8 @@ struct kc_ctx {
     uint64_t batches = 0;
     int n_cu = 256;
     double part_ms[5] = {0, 0, 0, 0, 0};  // E+P1, P2, P3 scatter, P3 hist + P4, P5
+    double presplit_ms = 0;                 // P3b (also in part_ms[2])
+    uint64_t presplit_batches = 0, sorted_run_batches = 0;
     double dedup_ms = 0;                  // skm P5a
     uint64_t dedup_records = 0;
     uint64_t part_keys = 0;               // keys partitioned since the last reset
@@ -715,6 +717,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, hipEventSynchronize(c->ev1));
                 HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
                 c->part_ms[2] += t;
+                c->presplit_ms += t;
+                c->presplit_batches++;
                 p5_keys = c->keys_a;
                 p5_spill = c->keys_b;
                 sub_starts = (const uint64_t*)c->sub_starts.p;
@@ -754,6 +758,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                     fprintf(stderr, "kc: P5s direct n=%llu records=%llu kept=%d %.3f ms\n", (unsigned long long)n,
                             (unsigned long long)R, dd ? 1 : 0, t5);
                 if (dd) {
+                    c->sorted_run_batches++;
                     c->hc_hint = R * 2 > n;
                     c->engines_used |= 2u;
                     done += nr;
@@ -790,6 +795,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
                 c->part_ms[4] += t;
                 c->p5_launches++;
+                c->sorted_run_batches++;
                 if (getenv("KC_DEBUG"))
                     fprintf(stderr, "kc: P5s n=%llu runs=%llu flagged=%u records=%llu %.3f ms\n",
                             (unsigned long long)n, (unsigned long long)c->stats_h[ST_P5_PASSES], nf,
@@ -1672,6 +1678,9 @@ kc_status kc_reset(kc_ctx* c) {
     c->rec_n = 0;
     c->batches = 0;
     for (double& x : c->part_ms) x = 0;
+    c->presplit_ms = 0;
+    c->presplit_batches = 0;
+    c->sorted_run_batches = 0;
     c->dedup_ms = 0;
     c->dedup_records = 0;
     c->part_keys = 0;
@@ -2654,6 +2663,9 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     if (!c || !out) return KC_ERR_ARG;
     *out = c->st;
     for (int i = 0; i < 5; i++) out->part_ms[i] = c->part_ms[i];
+    out->presplit_ms = c->presplit_ms;
+    out->presplit_batches = c->presplit_batches;
+    out->sorted_run_batches = c->sorted_run_batches;
     out->batches = c->batches_cut + c->batches;
     out->keys = c->part_keys;
     out->p5_launches = c->p5_launches;
