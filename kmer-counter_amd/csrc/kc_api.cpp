@@ -658,8 +658,15 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
             c->part_ms[3] += t;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_p3_scatter(W, c->keys_a, c->keys_b, c->key_cap, p3t, p3t + 257, ntiles, p3h, 2 * c->n_cu,
-                                        c->stream));
+            // P3's scatter is the regional radix scatter (digit word0 >> 56 over
+            // the 256 P2 regions, same tiles; next tile's run starts prefetched,
+            // XCD-aware tile walk); KC_P3_SCATTER: the older p3_scatter_k
+            if (getenv("KC_P3_SCATTER") || p3_tile(W) != rp_tile(W, false))
+                HIPCHK(c, launch_p3_scatter(W, c->keys_a, c->keys_b, c->key_cap, p3t, p3t + 257, ntiles, p3h,
+                                            2 * c->n_cu, c->stream));
+            else
+                HIPCHK(c, launch_rp_scatter(W, false, c->keys_a, c->key_cap, c->keys_b, c->key_cap, nullptr, nullptr, p3t,
+                                            p3t + 257, 256, ntiles, p3h, 56, nullptr, 0, 2 * c->n_cu, c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));

@@ -2787,11 +2787,13 @@ constexpr int kP3Block = 1024;
 
 template <int W>
 struct P3Cfg {
-    static constexpr int KPT = (W == 1) ? 16 : (W == 2 ? 8 : 4);  // keys per thread
+    // keys per thread: the same tiles as rp_scatter_k<W,false> (rp_tile), which
+    // scatters P3 with these tiles' histograms
+    static constexpr int KPT = (W == 1) ? 16 : (W == 2 ? 8 : (W == 3 ? 5 : 4));
     static constexpr int TILE = kP3Block * KPT;
 };
 
-int p3_tile(int W) { return kP3Block * ((W == 1) ? 16 : (W == 2 ? 8 : 4)); }
+int p3_tile(int W) { return kP3Block * ((W == 1) ? 16 : (W == 2 ? 8 : (W == 3 ? 5 : 4))); }
 
 __device__ __forceinline__ void p3_tile_range(const u64* __restrict__ rstart, const u64* __restrict__ tpre, u64 t,
                                               int TILE, u64* lo, u64* hi) {
