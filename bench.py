@@ -460,6 +460,7 @@ def main():
             "engines_used": {1: "skm", 2: "key-prefix partition", 3: "skm + key-prefix",
                              4: "table"}.get(st.get("engines_used", 0), str(st.get("engines_used"))),
             "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"], "spill_runs": st["spill_runs"],
+            "key_passes": st.get("key_passes", 0),
         }
         print(json.dumps(line), flush=True)
     for p in (in_path, out_path, f"{out_path}.part{D.rank}"):
@@ -517,13 +518,17 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
     elif used & 2:
         keys_step = st["keys"] or windows_step
         p5_per_step = max(1, st["p5_launches"])
-        nb = max(1, st["batches"])
+        # P3 runs once per read batch, or once per key-range pass (a batch
+        # counted by key ranges: each pass partitions only its own keys, while
+        # P2 walks every window of the batch per pass)
+        nb = max(1, st.get("key_passes", 0) or st["batches"])
         pre_b = st.get("presplit_batches", 0)
         pre_ms = acc["presplit_ms"]
         specs = [
             ("P2", f"count_front<{W},2,true,1024>", part_ms[1], acc["launches"], windows_step,
-             "k-mers", (G * 6) / max(1, L - k + 1) + 8 * W),
-            ("P3", f"p3_scatter_k<{W}>", part_ms[2] - pre_ms, steps * st["batches"], keys_step, "keys", 16 * W),
+             "k-mers", (G * 6) / max(1, L - k + 1) + 8 * W * keys_step / max(1, windows_step)),
+            ("P3", f"rp_scatter_k<{W},false>", part_ms[2] - pre_ms, steps * nb, keys_step, "keys",
+             16 * W),
         ]
         if pre_b:
             # P3b: word 0 read for the regional histogram + one scatter pass

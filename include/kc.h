@@ -56,9 +56,10 @@
 extern "C" {
 #endif
 
-#define KC_ABI_VERSION 5 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
+#define KC_ABI_VERSION 6 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
                             4: kc_count_file, kc_checkpoint / kc_rollback / kc_commit;
-                            5: kc_stats.presplit_ms / presplit_batches / sorted_run_batches */
+                            5: kc_stats.presplit_ms / presplit_batches / sorted_run_batches;
+                            6: kc_stats.key_passes */
 #define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
 
 typedef enum kc_status {
@@ -165,6 +166,9 @@ typedef struct kc_stats {
     uint64_t presplit_batches; /* batches that took P3b */
     uint64_t sorted_run_batches; /* batches counted by P5s (runs of sub-buckets sorted
                                     in LDS; part_ms[4] holds their time) */
+    uint64_t key_passes;       /* key-prefix engine, high cardinality: key-range passes
+                                  (a batch too big for the working set counted by
+                                  disjoint key ranges whose runs concatenate) */
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". (ABI 4: layout) */

@@ -87,6 +87,7 @@ class Stats(ctypes.Structure):
         ("presplit_ms", ctypes.c_double),
         ("presplit_batches", ctypes.c_uint64),
         ("sorted_run_batches", ctypes.c_uint64),
+        ("key_passes", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -96,7 +96,7 @@ struct kc_ctx {
     int n_cu = 256;
     double part_ms[5] = {0, 0, 0, 0, 0};  // E+P1, P2, P3 scatter, P3 hist + P4, P5
     double presplit_ms = 0;                 // P3b (also in part_ms[2])
-    uint64_t presplit_batches = 0, sorted_run_batches = 0;
+    uint64_t presplit_batches = 0, sorted_run_batches = 0, key_passes = 0;
     double dedup_ms = 0;                  // skm P5a
     uint64_t dedup_records = 0;
     uint64_t part_keys = 0;               // keys partitioned since the last reset
@@ -483,12 +483,17 @@ static const double kSkmDistinctMax = 0.35;
 // P5s direct (high cardinality, empty record state): sort_runs_k writes the
 // batch's records straight into fin_packed as a finished sorted run (record
 // 0: key 0 when present), each run of sub-buckets at its first key's position;
-// runs that held equal keys leave gaps that a segment copy closes. The run is
-// kept (keep_finished_run) and the record state stays empty. *done = false
-// when runs were handed to the hash path: nothing was kept and the caller
-// counts the batch into records as usual.
+// runs that held equal keys leave gaps that a segment copy closes. With
+// key-range passes (count_reads_part) every pass appends its key range at
+// record pk_at (the records of the earlier passes); `last` keeps fin_packed as
+// the finished run (direct_keep) and the record state stays empty. *done =
+// false when runs were handed to the hash path: nothing of this batch was
+// kept and the caller counts it into records as usual. `total` sizes
+// fin_packed on the first pass (keys of all passes).
+static kc_status direct_keep(kc_ctx* c, uint64_t nrec);
 static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub_starts, uint32_t nb, uint64_t n,
-                            uint8_t* rf, size_t fl, bool* done, uint64_t* records, float* ms) {
+                            uint8_t* rf, size_t fl, bool* done, uint64_t* records, float* ms, uint64_t pk_at = 0,
+                            uint64_t total = 0, bool last = true) {
     kc_status s;
     *done = false;
     const int W = c->W;
@@ -498,13 +503,14 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub
     if ((s = sync_stats(c))) return s;
     const bool key0 = c->stats_h[ST_KEY0_PRESENT] != 0;
     const uint64_t off0 = key0 ? 1 : 0;
-    if ((s = ensure_pooled(c, c->fin_packed, (off0 + n) * rs + 16))) return s;
+    if (pk_at == 0 && (s = ensure_pooled(c, c->fin_packed, (off0 + (total > n ? total : n)) * rs + 16))) return s;
+    if (c->fin_packed.bytes < (off0 + pk_at + n) * rs) return fail(c, KC_ERR_INTERNAL, "key-range pass overflows its run");
     HIPCHK(c, hipMemsetAsync(rf, 0, fl, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_sort_runs(W, keys, c->key_cap, sub_starts, nb, c->rec_keys, c->rec_cnts, c->rec_cap,
                                c->rec_cursor, c->stats, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,
                                (uint32_t*)c->desc_len.p, kDescCap, rf, bf, nflag, 2 * c->n_cu, c->stream,
-                               c->fin_packed.p, off0));
+                               c->fin_packed.p, off0 + pk_at));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     uint32_t nf = 0;
     uint64_t R = 0;
@@ -514,21 +520,23 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub
     HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
     *records = R;
     const uint64_t ndesc = c->stats_h[ST_DESC_FILL];
-    if (nf || (R < n && ndesc > kDescCap)) {
-        // undo (record cursor, descriptors): the caller counts into records
+    auto clear_cursor = [&]() -> kc_status {
+        // record cursor and descriptors start empty again
         HIPCHK(c, hipMemsetAsync(c->rec_cursor, 0, 8, c->stream));
         c->stats_h[ST_DESC_FILL] = 0;
         HIPCHK(c, hipMemcpyAsync(c->stats + ST_DESC_FILL, &c->stats_h[ST_DESC_FILL], 8, hipMemcpyHostToDevice,
                                  c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         return KC_OK;
-    }
+    };
+    if (nf || (R < n && ndesc > kDescCap)) return clear_cursor();  // undo: the caller counts into records
     if (R < n) {
-        // equal keys in some runs: close the gaps (segments in key order)
+        // equal keys in some runs: close the gaps (segments in key order) into
+        // merge_tmp, then back to the pass's place
         if ((s = ensure(c, c->desc_k2, ndesc * 8)) || (s = ensure(c, c->desc_v, ndesc * 4)) ||
             (s = ensure(c, c->desc_v2, ndesc * 4)) || (s = ensure(c, c->desc_lens, ndesc * 8)) ||
             (s = ensure(c, c->desc_offs, ndesc * 8)) || (s = ensure(c, c->rle_tmp, scan_tmp_elems(ndesc) * 8)) ||
-            (s = ensure_pooled(c, c->merge_tmp, (off0 + R) * rs + 16)))
+            (s = ensure_pooled(c, c->merge_tmp, R * rs + 16)))
             return s;
         HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, ndesc, c->stream));
         int which = 0;
@@ -541,10 +549,22 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub
         HIPCHK(c, launch_scan_u64((const uint64_t*)c->desc_lens.p, (uint64_t*)c->desc_offs.p, ndesc,
                                   (uint64_t*)c->rle_tmp.p, c->stream));
         HIPCHK(c, launch_packed_seg_copy(W, c->fin_packed.p, c->merge_tmp.p, order, (const uint64_t*)c->desc_start.p,
-                                         (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, off0,
+                                         (const uint32_t*)c->desc_len.p, (const uint64_t*)c->desc_offs.p, ndesc, 0,
                                          4 * c->n_cu, c->stream));
-        std::swap(c->fin_packed, c->merge_tmp);
+        HIPCHK(c, hipMemcpyAsync((uint8_t*)c->fin_packed.p + (off0 + pk_at) * rs, c->merge_tmp.p, R * rs,
+                                 hipMemcpyDeviceToDevice, c->stream));
     }
+    if ((s = clear_cursor())) return s;
+    *done = true;
+    return last ? direct_keep(c, pk_at + R) : KC_OK;
+}
+
+// fin_packed, written by direct passes (nrec records after the key-0 slot),
+// becomes a finished sorted run
+static kc_status direct_keep(kc_ctx* c, uint64_t nrec) {
+    kc_status s;
+    if ((s = sync_stats(c))) return s;
+    const bool key0 = c->stats_h[ST_KEY0_PRESENT] != 0;
     std::vector<uint32_t> r0((size_t)c->rs / 4, 0u);
     if (key0) {
         r0.back() = (uint32_t)c->stats_h[ST_KEY0];
@@ -552,8 +572,65 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->batches = 1;  // this batch: moved to batches_cut with the run
-    if ((s = keep_finished_run(c, off0 + R))) return s;
-    *done = true;
+    return keep_finished_run(c, (key0 ? 1 : 0) + nrec);
+}
+
+// Key-range passes (high cardinality): when one batch cannot hold the keys of
+// all reads, the reads are not cut into batches whose sorted runs must then be
+// merged; the key space is cut instead. A P1 pass over all reads counts the
+// live keys by their top byte (word0 >> 56); consecutive top bytes are
+// grouped into passes of at most key_cap keys, balanced; each pass re-walks all
+// reads and keeps only its key range (P1/P2 filter), and P5s direct writes it
+// after the previous passes' records: the runs are disjoint key ranges in key
+// order, so the finished run is their concatenation (no merge). Returns the
+// pass bounds (empty: not applicable, count by read batches).
+static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vector<uint32_t>* kp, uint64_t* keys) {
+    kp->clear();
+    kc_status s;
+    PartGeom pg = part_geometry((int)L, (int)c->k, l.n_reads);
+    const uint64_t hn = 256 * pg.nseg;
+    if ((s = ensure(c, c->part_hist, hn * 8)) || (s = ensure(c, c->part_base, hn * 8)) ||
+        (s = ensure(c, c->part_tmp, scan_tmp_elems(hn) * 8)))
+        return s;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 56, c->stream));
+    HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn, (uint64_t*)c->part_tmp.p,
+                              c->stream));
+    std::vector<uint64_t> b(257);
+    HIPCHK(c, hipMemcpy2DAsync(b.data(), 8, c->part_base.p, pg.nseg * 8, 8, 256, hipMemcpyDeviceToHost, c->stream));
+    uint64_t tail[2];
+    HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->part_base.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->part_hist.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    c->part_ms[0] += t;
+    b[256] = tail[0] + tail[1];
+    const uint64_t total = b[256];
+    *keys = total;
+    if (total <= c->key_cap) return KC_OK;
+    uint64_t np = (total + c->key_cap - 1) / c->key_cap;
+    // (KC_KEY_PASSES_MIN: path selector for tests and measurements, same counts)
+    if (const char* e = getenv("KC_KEY_PASSES_MIN")) np = std::max<uint64_t>(np, strtoull(e, nullptr, 10));
+    const uint64_t cap = std::min<uint64_t>(c->key_cap, (total + np - 1) / np * 5 / 4);
+    const uint64_t target = (total + np - 1) / np;
+    std::vector<uint32_t> bounds{0};
+    uint64_t acc = 0;
+    for (uint32_t d = 0; d < 256; d++) {
+        const uint64_t x = b[d + 1] - b[d];
+        if (x > cap) return KC_OK;  // one top byte holds more than a batch: read batches
+        // close the pass before d when d would overflow it, or when stopping
+        // here is closer to the balanced target than taking d
+        if (acc > 0 && (acc + x > cap || (acc + x > target && acc + x - target > target - acc))) {
+            bounds.push_back(d);
+            acc = 0;
+        }
+        acc += x;
+    }
+    bounds.push_back(256);
+    if (bounds.size() - 1 > 16) return KC_OK;
+    *kp = bounds;
     return KC_OK;
 }
 
@@ -576,13 +653,12 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
     kc_status s;
     uint64_t done = 0;
     float t = 0.f;
-    while (done < n_reads) {
-        uint64_t nr = n_reads - done;
-        if (nr > max_reads) nr = max_reads;
+    const uint64_t G = (uint64_t)groups_per_read((int)L);
+    auto launch_args = [&](uint64_t read0, uint64_t nr) {
         CountLaunch l;
         l.base = base;
         l.seq_off = seq_off;
-        l.read0 = done;
+        l.read0 = read0;
         l.n_reads = nr;
         l.L = (int)L;
         l.k = (int)c->k;
@@ -592,18 +668,49 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         l.spill_cap = c->spill_cap;
         l.stats = c->stats;
         l.probe_limit = probe_limit(c);
+        const uint64_t g0 = pre0 < 0 ? 0 : ((uint64_t)pre0 + read0) * G;
+        l.codes = (const uint32_t*)c->part_codes.p + g0;
+        l.inval = (const uint16_t*)c->part_inval.p + g0;
+        return l;
+    };
+    // Key-range passes (plan_key_passes): high cardinality, all reads encoded,
+    // more keys than one batch holds, and an empty record state (P5s direct)
+    std::vector<uint32_t> kp;  // pass bounds on word0 >> 56
+    size_t kpi = 0;            // current pass
+    uint64_t kp_keys = 0;      // live keys of all passes
+    uint64_t kp_out = 0;       // records the direct passes wrote so far
+    bool kp_direct = false;    // every pass so far went direct
+    if (pre0 >= 0 && c->hc_hint && nw * n_reads > c->key_cap && c->rec_n == 0 && c->batches == 0 &&
+        c->stats_h[ST_CLAIMED] == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES") &&
+        !getenv("KC_NO_P3B") && !getenv("KC_NO_SORT_RUNS") && !getenv("KC_NO_P5S_DIRECT")) {
+        if ((s = plan_key_passes(c, launch_args(0, n_reads), L, &kp, &kp_keys))) return s;
+        kp_direct = !kp.empty();
+        if (!kp.empty()) c->key_passes += kp.size() - 1;
+        if (getenv("KC_DEBUG") && !kp.empty())
+            fprintf(stderr, "kc: %zu key-range passes over %llu keys\n", kp.size() - 1, (unsigned long long)kp_keys);
+    }
+    while (done < n_reads) {
+        const bool kpass = !kp.empty();
+        uint64_t nr = n_reads - done;
+        if (nr > max_reads && !kpass) nr = max_reads;
+        CountLaunch l = launch_args(done, nr);
+        if (kpass) {
+            l.flo = kp[kpi];
+            l.fhi = kp[kpi + 1];
+            l.no_stats = kpi > 0;
+        }
         PartGeom pg = part_geometry((int)L, (int)c->k, nr);
         uint64_t hn = 256 * pg.nseg;
         if ((s = ensure(c, c->part_hist, hn * 8)) || (s = ensure(c, c->part_base, hn * 8)) ||
             (s = ensure(c, c->part_tmp, scan_tmp_elems(hn) * 8)))
             return s;
-        const uint64_t G = (uint64_t)groups_per_read((int)L);
         const uint64_t ng = nr * G;
         if (pre0 < 0 && ((s = ensure(c, c->part_codes, ng * 4 + 16)) || (s = ensure(c, c->part_inval, ng * 2 + 16))))
             return s;
-        const uint64_t g0 = pre0 < 0 ? 0 : ((uint64_t)pre0 + done) * G;
-        l.codes = (const uint32_t*)c->part_codes.p + g0;
-        l.inval = (const uint16_t*)c->part_inval.p + g0;
+        if (pre0 < 0) {  // (buffers may have moved)
+            l.codes = (const uint32_t*)c->part_codes.p;
+            l.inval = (const uint16_t*)c->part_inval.p;
+        }
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
         if (pre0 < 0)
             HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
@@ -750,7 +857,41 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             const bool sort_runs = sub_starts && !getenv("KC_NO_SORT_RUNS");
             uint64_t direct_min = 1ull << 22;  // (KC_P5S_DIRECT_MIN: path selector for tests)
             if (const char* e = getenv("KC_P5S_DIRECT_MIN")) direct_min = strtoull(e, nullptr, 10);
-            if (sort_runs && c->rec_n == 0 && c->batches == 0 && c->stats_h[ST_CLAIMED] == 0 && !c->skm_used &&
+            if (kpass && kp_direct) {
+                // key-range pass: appended to the direct run of the earlier passes
+                bool dd = false;
+                uint64_t R = 0;
+                float t5 = 0.f;
+                const bool last = kpi + 2 == kp.size();
+                if (sort_runs) {
+                    const size_t fl = ((size_t)nb << 8) + nb + 16;
+                    if ((s = ensure(c, c->run_flags, fl))) return s;
+                    if ((s = p5s_direct(c, p5_keys, sub_starts, nb, n, (uint8_t*)c->run_flags.p, fl, &dd, &R, &t5,
+                                        kp_out, kp_keys, last)))
+                        return s;
+                    c->part_ms[4] += t5;
+                    c->p5_launches++;
+                    if (getenv("KC_DEBUG"))
+                        fprintf(stderr, "kc: P5s direct pass %zu [%u, %u) n=%llu records=%llu kept=%d %.3f ms\n", kpi,
+                                kp[kpi], kp[kpi + 1], (unsigned long long)n, (unsigned long long)R, dd ? 1 : 0, t5);
+                }
+                if (dd) {
+                    kp_out += R;
+                    c->engines_used |= 2u;
+                    if (!last) {
+                        kpi++;
+                        continue;
+                    }
+                    c->sorted_run_batches++;
+                    done += nr;
+                    continue;
+                }
+                // this pass cannot go direct: the earlier passes become a
+                // finished run, this pass and the later ones count into records
+                kp_direct = false;
+                if (kp_out > 0 && (s = direct_keep(c, kp_out))) return s;
+            }
+            if (!kpass && sort_runs && c->rec_n == 0 && c->batches == 0 && c->stats_h[ST_CLAIMED] == 0 && !c->skm_used &&
                 c->runs.empty() && n >= direct_min && !getenv("KC_NO_P5S_DIRECT")) {
                 const size_t fl = ((size_t)nb << 8) + nb + 16;
                 if ((s = ensure(c, c->run_flags, fl))) return s;
@@ -857,6 +998,10 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         }
         c->batches++;
         c->engines_used |= 2u;
+        if (kpass && kpi + 2 < kp.size()) {
+            kpi++;
+            continue;
+        }
         done += nr;
     }
     c->st.valid_kmers = c->stats_h[ST_VALID];
@@ -1167,6 +1312,12 @@ static const double kSketchDistinctMax = 0.7;
 static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre0) {
     kc_status s;
     const uint64_t G = (uint64_t)groups_per_read((int)L);
+    // the first reads holding 2^26 group-aligned k-mers: the engine choice
+    // changes speed only, never counts, and a batch's first ~6M reads tell
+    // high from low coverage (cfg2 at 30x reads as 3.8x there, 27% distinct)
+    // at an eighth of the cost of walking all of them
+    const uint64_t sketch_reads = ((1ull << 26) + G - 1) / G;
+    if (n_reads > sketch_reads) n_reads = sketch_reads;
     // sample rate 2^-rb by k-mer hash: about 2^18 samples (at least 1/256)
     const uint64_t aligned = n_reads * G;
     int rb = 8;
@@ -1211,19 +1362,27 @@ static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t p
     return KC_OK;
 }
 
-// pre0 >= 0: the reads are pre-encoded in part_codes / part_inval from read pre0
-static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L,
-                             int64_t pre0 = -1) {
-    // the coverage sketch picks the engine (auto) or, for the partition engine,
-    // sets the high-cardinality hint before its first batch
-    const bool sketch_skm = c->skm && !c->skm_hc && !c->skm_force && skm_geometry((int)L, (int)c->k).ok;
-    const bool sketch_part = !c->skm && c->part && !c->hc_hint;
+// The coverage sketch picks the engine (auto) or, for the partition engine,
+// sets the high-cardinality hint before its first batch
+static kc_status sketch_gate(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre0) {
+    const bool skm_ok = skm_geometry((int)L, (int)c->k).ok;
+    const bool sketch_skm = c->skm && !c->skm_hc && !c->skm_force && skm_ok;
+    // (the key-prefix engine: chosen, or the default engine's only one for this (L, k))
+    const bool sketch_part = c->part && !c->hc_hint && !(c->skm && !c->skm_hc && skm_ok);
     if ((sketch_skm || sketch_part) && !c->skm_checked && pre0 >= 0 && !getenv("KC_NO_SKETCH") &&
         n_reads * (uint64_t)(L - c->k + 1) >= kSkmSampleMinKeys) {
         kc_status s = sketch_engine(c, n_reads, L, pre0);
         if (s) return s;
         if (sketch_part) c->skm_checked = true;  // once per reset
     }
+    return KC_OK;
+}
+
+// pre0 >= 0: the reads are pre-encoded in part_codes / part_inval from read pre0
+static kc_status count_reads(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads, int64_t L,
+                             int64_t pre0 = -1) {
+    kc_status s0 = sketch_gate(c, n_reads, L, pre0);
+    if (s0) return s0;
     // very long reads (one read's windows do not fit a P2 workgroup's LDS)
     // take the table engine; both feed the same finish
     if (c->skm && !c->skm_hc) {
@@ -1250,11 +1409,16 @@ static uint64_t batch_reads(const kc_ctx* c, int64_t L) {
 // the batch may grow past one engine batch (count_reads splits it) up to
 // 1/8 of the device's memory in codes (6 B per 16 bases), so a malformed block
 // later in the same file can still be rolled back.
-static uint64_t pend_room(const kc_ctx* c, int64_t L) {
+// Without a checkpoint the codes engines still pend up to 16 engine batches
+// (within the same budget): a high-cardinality batch is then counted in
+// key-range passes over all its reads instead of read batches whose runs must
+// be merged (count_reads_part).
+static uint64_t pend_room(const kc_ctx* c, int64_t L, bool var = false) {
     const uint64_t b = batch_reads(c, L);
-    if (!c->ckpt) return b;
+    if (!c->ckpt && (!c->part || var)) return b;
     const uint64_t per_read = 6 * (uint64_t)groups_per_read((int)L) + 2;
-    const uint64_t budget = c->dev_total / 8 / per_read;
+    uint64_t budget = c->dev_total / 8 / per_read;
+    if (!c->ckpt && budget / 16 > b) budget = 16 * b;
     return budget > b ? budget : b;
 }
 
@@ -1292,7 +1456,25 @@ static kc_status pend_flush(kc_ctx* c) {
     c->flushes++;
     kc_status s;
     if (!c->pend_var) {
-        if ((s = count_reads(c, nullptr, nullptr, n, c->pend_L, 0))) return s;
+        const int64_t L = c->pend_L;
+        const uint64_t b = batch_reads(c, L);
+        if (n > b) {
+            // more than one engine batch: a high-cardinality batch on an empty
+            // record state is counted whole (key-range passes, count_reads_part),
+            // anything else batch by batch with a run cut between batches when
+            // the records outgrow half the working set
+            if ((s = sketch_gate(c, n, L, 0))) return s;
+            const bool passes = c->hc_hint && c->part && (!c->skm || c->skm_hc) && c->rec_n == 0 &&
+                                c->batches == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES");
+            if (!passes) {
+                for (uint64_t r0 = 0; r0 < n; r0 += b) {
+                    if ((s = count_reads(c, nullptr, nullptr, n - r0 < b ? n - r0 : b, L, (int64_t)r0))) return s;
+                    if ((s = cut_run_if_full(c))) return s;
+                }
+                return KC_OK;
+            }
+        }
+        if ((s = count_reads(c, nullptr, nullptr, n, L, 0))) return s;
         return cut_run_if_full(c);
     }
     // variable-length reads: the slot padding's invalid windows are no holes;
@@ -1319,7 +1501,7 @@ static kc_status pend_flush(kc_ctx* c) {
 // read index where the new reads go.
 static kc_status pend_reserve(kc_ctx* c, int64_t L, bool var, uint64_t n_new, uint64_t* off) {
     kc_status s;
-    if (c->pend_reads && (c->pend_L != L || c->pend_var != var || c->pend_reads + n_new > pend_room(c, L)))
+    if (c->pend_reads && (c->pend_L != L || c->pend_var != var || c->pend_reads + n_new > pend_room(c, L, var)))
         if ((s = pend_flush(c))) return s;
     const uint64_t G = (uint64_t)groups_per_read((int)L);
     const uint64_t keep = c->pend_reads * G, need = (c->pend_reads + n_new) * G;
@@ -1343,9 +1525,9 @@ static kc_status pend_add_reads(kc_ctx* c, const uint8_t* base, const uint64_t* 
     uint64_t done = 0;
     while (done < n_reads) {
         uint64_t free = 0;
-        if (c->pend_L == L && c->pend_var == var && c->pend_reads < pend_room(c, L))
-            free = pend_room(c, L) - c->pend_reads;
-        if (free == 0 || c->pend_reads == 0) free = pend_room(c, L);
+        if (c->pend_L == L && c->pend_var == var && c->pend_reads < pend_room(c, L, var))
+            free = pend_room(c, L, var) - c->pend_reads;
+        if (free == 0 || c->pend_reads == 0) free = pend_room(c, L, var);
         const uint64_t m = n_reads - done < free ? n_reads - done : free;
         uint64_t off = 0;
         if ((s = pend_reserve(c, L, var, m, &off))) return s;
@@ -1420,7 +1602,7 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     // where the block's reads go: the pending batch when they fit it (after
     // counting a pending batch of another kind or too full to take them)
     uint64_t off = 0;
-    const bool into_pend = codes && n_rec > 0 && n_rec <= pend_room(c, L);
+    const bool into_pend = codes && n_rec > 0 && n_rec <= pend_room(c, L, var);
     if (into_pend && (s = pend_reserve(c, L, var, n_rec, &off))) return s;
     const bool no_fuse = getenv("KC_NO_FQ_ENCODE") != nullptr;  // path selector (tests): same bytes either way
     const bool fused = into_pend && !var && !no_fuse;                               // fq_encode_k
@@ -1688,6 +1870,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->presplit_ms = 0;
     c->presplit_batches = 0;
     c->sorted_run_batches = 0;
+    c->key_passes = 0;
     c->dedup_ms = 0;
     c->dedup_records = 0;
     c->part_keys = 0;
@@ -2479,6 +2662,15 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     HIPCHK(c, hipEventElapsedTime(&tf, c->ev0, c->ev1));
     c->st.finish_ms += tf;
     c->st.table_used = c->stats_h[ST_CLAIMED];
+    if (c->dev_runs.size() == 1 && n == 0) {
+        // one sorted run and no table run (key-range passes, one direct
+        // batch): the run is the output, its buffer becomes fin_packed
+        if (c->fin_packed.p) c->run_pool.push_back(c->fin_packed);
+        c->fin_packed = c->dev_runs[0];
+        n = c->dev_run_n[0];
+        c->dev_runs.clear();
+        c->dev_run_n.clear();
+    }
     if (!c->dev_runs.empty()) {
         // sorted runs in HBM (cut runs, spill runs): the table run joins them
         // (taking over fin_packed's buffer), one merge of all
@@ -2673,6 +2865,7 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     out->presplit_ms = c->presplit_ms;
     out->presplit_batches = c->presplit_batches;
     out->sorted_run_batches = c->sorted_run_batches;
+    out->key_passes = c->key_passes;
     out->batches = c->batches_cut + c->batches;
     out->keys = c->part_keys;
     out->p5_launches = c->p5_launches;

@@ -74,6 +74,8 @@ struct CountLaunch {
     const uint32_t* codes = nullptr;   // partition engine: reads encoded by kernel E
     const uint16_t* inval = nullptr;   //   (groups_per_read(L) words per read)
     const uint16_t* rlen = nullptr;    // KC_FLAG_VARLEN: each read's own length (<= L), read r at rlen[r]
+    uint32_t flo = 0, fhi = 256;       // partition P1/P2: keys with word0 >> 56 in [flo, fhi) only
+    bool no_stats = false;             //   (key-range passes after the first: statistics counted once)
 };
 
 // E: encode the launch's reads once into 2-bit codes (u32 per 16 bases, first

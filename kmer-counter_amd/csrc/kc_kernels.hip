@@ -306,6 +306,8 @@ struct PartArgs {
     const u32* codes; // CODES front end: encoded reads (kernel E), G u32 per read
     const unsigned short* inval;  //      not-ACGT masks, G u16 per read
     int G;            //                  16-base groups per read
+    u32 flo, fhi;     // key-range pass: only keys with word0 >> 56 in [flo, fhi) (P1 and P2)
+    int no_stats;     // key-range pass after the first: valid / key-0 statistics not counted again
 };
 
 static size_t sink_lds_host(int W, int sink, int scap) {
@@ -512,6 +514,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             const int nchr = (nw + kRoll - 1) / kRoll;
             const int total = nr * nchr;
             if constexpr (SINK == SINK_SCATTER) {
+                const bool filt = pa.fhi - pa.flo < 256u;
                 // Two phases per run of kRoll windows. A: roll the windows once
                 // to get the lane's live mask (valid, non-zero keys). One LDS
                 // reservation per wave covers all kRoll steps: step s of the
@@ -562,7 +565,9 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                             my_hole |= active && !valid;
                             valids += valid ? 1u : 0u;
                             zeros += (valid && is_zero) ? 1u : 0u;
-                            livem |= (valid && !is_zero ? 1u : 0u) << sstep;
+                            const u64 w0 = W == 1 ? (kr[0] & last_mask) : kr[0];
+                            const bool in = (u32)(w0 >> 56) - pa.flo < pa.fhi - pa.flo;
+                            livem |= (valid && !is_zero && in ? 1u : 0u) << sstep;
 #pragma unroll
                             for (int j = 0; j < W - 1; j++) kr[j] = (kr[j] << 2) | (kr[j + 1] >> 62);
                             kr[W - 1] = (kr[W - 1] << 2) | (tl >> 62);
@@ -570,7 +575,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                         }
                     }
                     my_valid += valids;
-                    if (__ballot(zeros != 0u)) {
+                    if (!pa.no_stats && __ballot(zeros != 0u)) {
                         wave_add(&a.stats[ST_KEY0], zeros);
                         if (lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
                     }
@@ -589,6 +594,28 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                     if (lane_id() == 0) wbase = atomicAdd(&s_misc[0], wtot);
                     wbase = __builtin_amdgcn_readfirstlane(wbase);
                     const u64 lt = lanemask_lt();
+                    if (filt) {
+                        // key-range pass: about half the lanes hold no key of
+                        // the range; only live lanes stage (no trash traffic)
+#pragma unroll
+                        for (int sstep = 0; sstep < kRoll; sstep++) {
+                            if ((livem >> sstep) & 1u) {
+                                u64 key[W];
+#pragma unroll
+                                for (int j = 0; j < W; j++) key[j] = raw[j];
+                                key[W - 1] &= last_mask;
+                                const u32 idx = wbase + soff[sstep] + (u32)__popcll(bal[sstep] & lt);
+#pragma unroll
+                                for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
+                                atomicAdd(&s_cnt[(u32)(key[0] >> pa.shift) & 255u], 1u);
+                            }
+#pragma unroll
+                            for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
+                            raw[W - 1] = (raw[W - 1] << 2) | (tail >> 62);
+                            tail <<= 2;
+                        }
+                        continue;
+                    }
 #pragma unroll
                     for (int sstep = 0; sstep < kRoll; sstep++) {
                         // branch-free: a lane without a live key writes the trash
@@ -654,7 +681,8 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                         const bool live = valid && !is_zero;
 
                         if constexpr (SINK == SINK_HIST) {
-                            if (live) atomicAdd(&s_hist[(u32)(key[0] >> pa.shift) & 255u], 1u);
+                            if (live && (u32)(key[0] >> 56) - pa.flo < pa.fhi - pa.flo)
+                                atomicAdd(&s_hist[(u32)(key[0] >> pa.shift) & 255u], 1u);
                         } else {
                             // key 0^W: one atomic per wave
                             u64 zmask = __ballot(valid && is_zero);
@@ -745,7 +773,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             __syncthreads();
         }
     }
-    if constexpr (SINK != SINK_HIST) {
+    if (SINK != SINK_HIST && !pa.no_stats) {
         wave_add(&a.stats[ST_VALID], my_valid);
         if (__ballot(my_hole) && lane_id() == 0) atomicOr((unsigned long long*)&a.stats[ST_KEY0_PRESENT], 1ull);
     }
@@ -989,6 +1017,9 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
     if (!l.codes || !l.inval) return hipErrorInvalidValue;
     pa.nseg = pg.nseg;
     pa.seg_tiles = pg.seg_tiles;
+    pa.flo = l.flo;
+    pa.fhi = l.fhi;
+    pa.no_stats = l.no_stats ? 1 : 0;
     pa.shift = shift;
     pa.max_win = pg.max_win;
     pa.scap = pg.scap;
@@ -1017,6 +1048,9 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     if (!l.codes || !l.inval) return hipErrorInvalidValue;
     pa.nseg = pg.nseg;
     pa.seg_tiles = pg.seg_tiles;
+    pa.flo = l.flo;
+    pa.fhi = l.fhi;
+    pa.no_stats = l.no_stats ? 1 : 0;
     pa.shift = shift;
     pa.max_win = pg.max_win;
     pa.scap = pg.scap;
@@ -2366,8 +2400,15 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
             }
             u32 l2 = 0;
             while ((1u << l2) < e - s0) l2++;
-            const int sh = 29 + (int)l2;  // (e - s0) << 40 over 2^11 bins
+            const int sh = 29 + (int)l2;  // (the descriptor's digit span: (e - s0) << 40 rounded up to 2^l2)
             const u64 base = (u64)s0 << 40;
+            // bins over the run's exact span of e - s0 sub-buckets: digit =
+            // floor(off / 2^29 * ceil(2^32 / span) / 2^32), monotone in the key
+            // and < 2^11 (clamped); a span rounded up to a power of two would
+            // leave up to half the bins empty and put twice the keys in the
+            // others (bins over 8 keys take the slow position loop)
+            const u32 span = e - s0;
+            const u32 smul = (u32)((0x100000000ull + span - 1) / span);
             for (u32 i = tid; i < kSrBins; i += kSrBlock) bins[i] = 0;
             if (tid == 0) {
                 misc[0] = 0;
@@ -2378,7 +2419,7 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
             u32 dg[R];
 #pragma unroll
             for (int i = 0; i < R; i++) {
-                dg[i] = (u32)(((k[i][0] & M48) - base) >> sh) & (kSrBins - 1);
+                dg[i] = min((u32)(((u64)(u32)(((k[i][0] & M48) - base) >> 29) * smul) >> 32), kSrBins - 1);
                 if ((u32)tid + (u32)i * kSrBlock < len) atomicAdd(&bins[dg[i]], 1u);
             }
             __syncthreads();
@@ -2480,9 +2521,29 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
                         a.desc_len[di] = len | ((u32)(sh + 1) << 24) | (1u << 31);
                     }
                 }
+                // the keys into sorted order in LDS (every thread is past its
+                // reads of skey: the barrier above), then the run's records
+                // written as consecutive dwords: one wave store covers 256
+                // contiguous bytes instead of 64 scattered records
 #pragma unroll
-                for (int i = 0; i < R; i++)
-                    if ((u32)tid + (u32)i * kSrBlock < len) put_packed<W>(a.packed, rbase + pos[i], k[i], 1u);
+                for (int i = 0; i < R; i++) {
+                    if ((u32)tid + (u32)i * kSrBlock >= len) continue;
+#pragma unroll
+                    for (int jj = 0; jj < W; jj++) skey[(size_t)jj * SP + pos[i]] = k[i][jj];
+                }
+                __syncthreads();
+                constexpr u32 RW = 2 * W + 1;  // dwords per SortedKMerFile record
+                u32* __restrict__ out = a.packed + rbase * RW;
+                const u32 nd = len * RW;
+                for (u32 u = (u32)tid; u < nd; u += kSrBlock) {
+                    const u32 r = u / RW, w = u - r * RW;
+                    u32 v = 1u;
+                    if (w < 2 * W) {
+                        const u64 x = skey[(size_t)(w >> 1) * SP + r];
+                        v = (w & 1u) ? (u32)(x >> 32) : (u32)x;
+                    }
+                    out[u] = v;
+                }
                 SR_MARK(8);
                 continue;
             }

@@ -562,6 +562,79 @@ def test_sorted_runs_hand_off_to_hash_path(kca, orc, monkeypatch, capfd, k):
     assert got == orc.count_fastq(fq, k)
 
 
+def _hc_reads(rng, n, L, dup=0, clusters=()):
+    """n iid reads of L bases (codes 0..3); the last `dup` reads repeat earlier
+    ones (equal keys), read 5 is all A (key 0); clusters = ((reads, bases), ...)
+    give groups of reads sharing their first `bases` bases."""
+    import numpy as np
+    reads = rng.integers(0, 4, size=(n, L), dtype=np.uint8)
+    if dup:
+        reads[n - dup:] = reads[rng.integers(0, n - dup, size=dup)]
+    r0 = 10
+    for cnt, nb in clusters:
+        reads[r0:r0 + cnt, :nb] = rng.integers(0, 4, size=nb, dtype=np.uint8)
+        r0 += cnt
+    reads[5] = 0
+    return reads[rng.permutation(n)]
+
+
+@pytest.mark.parametrize("k", [31, 55, 100])
+def test_key_range_passes(kca, orc, monkeypatch, capfd, k):
+    """High cardinality with more keys than one batch holds (SURVEY cfg5's
+    shape, scaled down to a 128 MB working set): the default engine counts
+    all reads in key-range passes (each pass re-walks the reads and keeps one
+    range of word0 >> 56; P5s direct appends it to one run, so the run is the
+    concatenation of the passes and kc_finish merges nothing). Repeated reads
+    put equal keys into runs (per-pass gap compaction), an all-A read gives
+    key 0. Same bytes as the oracle and as read batches + run merge
+    (KC_NO_KEY_PASSES)."""
+    import numpy as np
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L = 150
+    n = max(180000, (1 << 24) // (L - k + 1) + 2000)  # the coverage sketch needs 2^24 keys
+    fq = _fastq_from_codes(_hc_reads(np.random.default_rng(k + 101), n, L, dup=n // 20))
+    outs, sts = [], []
+    for env in ((), ("KC_NO_KEY_PASSES",)):
+        for v in env:
+            monkeypatch.setenv(v, "1")
+        with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=128 << 20) as ctx:
+            ctx.count_fastq(fq)
+            outs.append(ctx.records())
+            sts.append(ctx.stats())
+        for v in env:
+            monkeypatch.delenv(v)
+    err = capfd.readouterr().err
+    assert sts[0]["key_passes"] >= 2 and sts[1]["key_passes"] == 0, err[-3000:]
+    direct = [x for x in err.splitlines() if "kc: P5s direct pass" in x]
+    assert len(direct) == sts[0]["key_passes"] and all("kept=1" in x for x in direct), err[-3000:]
+    assert sts[1]["spill_runs"] >= 2
+    assert outs[0] == outs[1] == orc.count_fastq(fq, k)
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_key_range_pass_hands_off(kca, orc, monkeypatch, capfd, k):
+    """A key-range pass that P5s cannot take direct (a sub-bucket of 12k keys:
+    reads sharing their first 12 bases, among iid reads): the passes before it
+    become a finished run, that pass and the later ones count into records
+    (the LDS hash table for the flagged runs), kc_finish merges the two. Same
+    bytes as the oracle."""
+    import numpy as np
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L = 150
+    n = 190000
+    fq = _fastq_from_codes(_hc_reads(np.random.default_rng(k + 7), n, L, clusters=((12000, 12),)))
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=128 << 20) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    err = capfd.readouterr().err
+    direct = [x for x in err.splitlines() if "kc: P5s direct pass" in x]
+    assert st["key_passes"] >= 2 and any("kept=0" in x for x in direct), err[-3000:]
+    assert got == orc.count_fastq(fq, k)
+
+
 def _u64_sortable(lo32, hi32):
     """(hi << 32 | lo) as int64 whose signed order is the unsigned order."""
     import torch
@@ -570,15 +643,20 @@ def _u64_sortable(lo32, hi32):
 
 
 @pytest.mark.slow
-def test_config5_full_size_properties(kca):
+@pytest.mark.parametrize("batches", [False, True], ids=["key_passes", "read_batches"])
+def test_config5_full_size_properties(kca, monkeypatch, batches):
     """BASELINE config 5 (k=55 two-word keys, 20M x 150 bp iid reads, ~1.92e9
     distinct) on the default engine with a working set below the distinct
     count: the records outgrow it, are cut into sorted runs (the reference's
     spill -> sort path) and kc_finish merges the runs on the device. Checked
     on the device: keys strictly ascending (two-word order), counts sum to the
     valid windows, and every k-mer of sampled reads is present with a count
-    no lower than its multiplicity in the sample."""
+    no lower than its multiplicity in the sample. Default: key-range passes
+    (one run, concatenated); read_batches (KC_NO_KEY_PASSES): one sorted run
+    per read batch, merged on the device."""
     import torch
+    if batches:
+        monkeypatch.setenv("KC_NO_KEY_PASSES", "1")
 
     n, L, k = 20_000_000, 150, 55
     dev = torch.device("cuda", 0)
@@ -588,7 +666,11 @@ def test_config5_full_size_properties(kca):
         ctx.free_device(ptr)
         nrec = ctx.finish()
         st = ctx.stats()
-        assert st["spill_runs"] >= 2 and st["valid_kmers"] == n * (L - k + 1)
+        assert st["valid_kmers"] == n * (L - k + 1)
+        if batches:
+            assert st["spill_runs"] >= 2 and st["key_passes"] == 0
+        else:
+            assert st["key_passes"] >= 2 and st["spill_runs"] == 1
         rec = torch.empty(nrec * 20, dtype=torch.uint8, device=dev)
         ctx.export_records(rec)
     words = rec.view(torch.int32).view(nrec, 5)
