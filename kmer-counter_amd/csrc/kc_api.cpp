@@ -79,6 +79,8 @@ struct kc_ctx {
     uint64_t digs_bytes = 0;
     uint64_t* keys_b = nullptr;
     DevBuf part_hist, part_base, part_tmp, part_starts, part_sort_hist;
+    DevBuf part_ghist;  // key-range passes: P1 histogram by 16 key groups (+ the group totals)
+    DevBuf part_base2;  // key-range passes: the second pass of a walk's run starts
     DevBuf part_dedup;  // skm P5a: per-bucket list starts (u64) and lengths (u32), list cursor
     DevBuf p3b_buf, sub_starts;  // key-prefix engine, high cardinality: P3b tile positions, sub-bucket starts
     DevBuf run_flags;            //   P5s: runs left to the LDS hash path
@@ -589,25 +591,21 @@ static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vecto
     kc_status s;
     PartGeom pg = part_geometry((int)L, (int)c->k, l.n_reads);
     const uint64_t hn = 256 * pg.nseg;
-    if ((s = ensure(c, c->part_hist, hn * 8)) || (s = ensure(c, c->part_base, hn * 8)) ||
-        (s = ensure(c, c->part_tmp, scan_tmp_elems(hn) * 8)))
-        return s;
+    constexpr uint32_t NG = 16;  // key groups: word0 >> 60
+    if ((s = ensure(c, c->part_ghist, (NG * hn + NG) * 8))) return s;
+    uint64_t* gh = (uint64_t*)c->part_ghist.p;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 56, c->stream));
-    HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn, (uint64_t*)c->part_tmp.p,
-                              c->stream));
-    std::vector<uint64_t> b(257);
-    HIPCHK(c, hipMemcpy2DAsync(b.data(), 8, c->part_base.p, pg.nseg * 8, 8, 256, hipMemcpyDeviceToHost, c->stream));
-    uint64_t tail[2];
-    HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->part_base.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->part_hist.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, launch_part_hist(l, pg, gh, 48, c->stream, 4));
+    HIPCHK(c, launch_hist_group_totals(gh, pg.nseg, NG, gh + NG * hn, c->stream));
+    std::vector<uint64_t> gt(NG);
+    HIPCHK(c, hipMemcpyAsync(gt.data(), gh + NG * hn, NG * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float t = 0.f;
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
     c->part_ms[0] += t;
-    b[256] = tail[0] + tail[1];
-    const uint64_t total = b[256];
+    uint64_t total = 0;
+    for (uint64_t x : gt) total += x;
     *keys = total;
     if (total <= c->key_cap) return KC_OK;
     uint64_t np = (total + c->key_cap - 1) / c->key_cap;
@@ -617,13 +615,13 @@ static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vecto
     const uint64_t target = (total + np - 1) / np;
     std::vector<uint32_t> bounds{0};
     uint64_t acc = 0;
-    for (uint32_t d = 0; d < 256; d++) {
-        const uint64_t x = b[d + 1] - b[d];
-        if (x > cap) return KC_OK;  // one top byte holds more than a batch: read batches
-        // close the pass before d when d would overflow it, or when stopping
-        // here is closer to the balanced target than taking d
+    for (uint32_t g = 0; g < NG; g++) {
+        const uint64_t x = gt[g];
+        if (x > cap) return KC_OK;  // one group holds more than a batch: read batches
+        // close the pass before g when g would overflow it, or when stopping
+        // here is closer to the balanced target than taking g
         if (acc > 0 && (acc + x > cap || (acc + x > target && acc + x - target > target - acc))) {
-            bounds.push_back(d);
+            bounds.push_back(g * (256 / NG));
             acc = 0;
         }
         acc += x;
@@ -680,12 +678,21 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
     uint64_t kp_keys = 0;      // live keys of all passes
     uint64_t kp_out = 0;       // records the direct passes wrote so far
     bool kp_direct = false;    // every pass so far went direct
+    // two passes per walk: P2 writes the second pass's keys (SoA, stride = its
+    // key count, then its digit bytes) into fin_packed past the records the
+    // first pass will write; that pass's P3 reads them from there
+    size_t kp_u_pass = ~(size_t)0;  // the pass whose P2 output is at kp_u_keys
+    uint64_t* kp_u_keys = nullptr;
+    uint64_t kp_u_n = 0;
     if (pre0 >= 0 && c->hc_hint && nw * n_reads > c->key_cap && c->rec_n == 0 && c->batches == 0 &&
         c->stats_h[ST_CLAIMED] == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES") &&
         !getenv("KC_NO_P3B") && !getenv("KC_NO_SORT_RUNS") && !getenv("KC_NO_P5S_DIRECT")) {
         if ((s = plan_key_passes(c, launch_args(0, n_reads), L, &kp, &kp_keys))) return s;
         kp_direct = !kp.empty();
         if (!kp.empty()) c->key_passes += kp.size() - 1;
+        // the finished run's buffer (key 0 slot + every key), before the first
+        // walk: it holds the second pass's P2 output until that pass's P3
+        if (!kp.empty() && (s = ensure_pooled(c, c->fin_packed, (1 + kp_keys) * (size_t)c->rs + 16))) return s;
         if (getenv("KC_DEBUG") && !kp.empty())
             fprintf(stderr, "kc: %zu key-range passes over %llu keys\n", kp.size() - 1, (unsigned long long)kp_keys);
     }
@@ -711,31 +718,77 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             l.codes = (const uint32_t*)c->part_codes.p;
             l.inval = (const uint16_t*)c->part_inval.p;
         }
-        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        if (pre0 < 0)
-            HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
-        HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 48, c->stream));
-        HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn, (uint64_t*)c->part_tmp.p,
-                                  c->stream));
-        uint64_t tail[2];
-        HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->part_base.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->part_hist.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-        c->part_ms[0] += t;
-        const uint64_t n = tail[0] + tail[1];
-        if (n > c->key_cap) return fail(c, KC_ERR_INTERNAL, "batch keys %llu exceed capacity", (unsigned long long)n);
-
-        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48, c->digs,
-                                      c->stream));
-        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-        HIPCHK(c, hipEventSynchronize(c->ev1));
-        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-        c->part_ms[1] += t;
-        c->st.insert_launches++;
-        c->st.insert_ms += t;
+        // this pass's P2 output: keys_a (+ digs), or fin_packed when the
+        // previous pass's walk wrote it (two passes per walk)
+        const bool from_u = kpass && kp_u_pass == kpi;
+        uint64_t* p2_keys = from_u ? kp_u_keys : c->keys_a;
+        const uint64_t p2_stride = from_u ? kp_u_n : c->key_cap;
+        const uint8_t* p2_digs = from_u ? (const uint8_t*)(kp_u_keys + (size_t)W * kp_u_n) : c->digs;
+        const uint64_t* p2_base = (const uint64_t*)(from_u ? c->part_base2.p : c->part_base.p);
+        uint64_t n = from_u ? kp_u_n : 0;
+        if (!from_u) {
+            const bool dual = kpass && kp_direct && kpi + 2 < kp.size() && !getenv("KC_NO_DUAL_PASS") &&
+                              !getenv("KC_P3_SCATTER");
+            if (dual && (s = ensure(c, c->part_base2, hn * 8))) return s;
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            if (pre0 < 0)
+                HIPCHK(c, launch_encode_reads(l, (uint32_t*)c->part_codes.p, (uint16_t*)c->part_inval.p, c->stream));
+            if (kpass)  // the pass's histogram from the planner's grouped one (no walk)
+                HIPCHK(c, launch_hist_group_sum((const uint64_t*)c->part_ghist.p, pg.nseg, l.flo / 16, l.fhi / 16,
+                                                (uint64_t*)c->part_hist.p, c->stream));
+            else
+                HIPCHK(c, launch_part_hist(l, pg, (uint64_t*)c->part_hist.p, 48, c->stream));
+            HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base.p, hn,
+                                      (uint64_t*)c->part_tmp.p, c->stream));
+            uint64_t tail[4] = {0, 0, 0, 0};
+            HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->part_base.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->part_hist.p + hn - 1, 8, hipMemcpyDeviceToHost, c->stream));
+            if (dual) {
+                HIPCHK(c, launch_hist_group_sum((const uint64_t*)c->part_ghist.p, pg.nseg, kp[kpi + 1] / 16,
+                                                kp[kpi + 2] / 16, (uint64_t*)c->part_hist.p, c->stream));
+                HIPCHK(c, launch_scan_u64((uint64_t*)c->part_hist.p, (uint64_t*)c->part_base2.p, hn,
+                                          (uint64_t*)c->part_tmp.p, c->stream));
+                HIPCHK(c, hipMemcpyAsync(&tail[2], (uint64_t*)c->part_base2.p + hn - 1, 8, hipMemcpyDeviceToHost,
+                                         c->stream));
+                HIPCHK(c, hipMemcpyAsync(&tail[3], (uint64_t*)c->part_hist.p + hn - 1, 8, hipMemcpyDeviceToHost,
+                                         c->stream));
+            }
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[0] += t;
+            n = tail[0] + tail[1];
+            if (n > c->key_cap)
+                return fail(c, KC_ERR_INTERNAL, "batch keys %llu exceed capacity", (unsigned long long)n);
+            // the second pass's keys go past the records this pass will write
+            // (key 0 slot + the earlier passes' records + this pass's keys)
+            uint64_t* u = nullptr;
+            const uint64_t n2 = tail[2] + tail[3];
+            if (dual) {
+                const size_t at = ((1 + kp_out + n) * (size_t)c->rs + 15) & ~(size_t)15;
+                if (at + n2 * (8 * (size_t)W + 1) <= c->fin_packed.bytes && n2 > 0)
+                    u = (uint64_t*)((uint8_t*)c->fin_packed.p + at);
+            }
+            if (u) {
+                l.fhi = kp[kpi + 2];  // the walk keeps both passes' ranges
+            }
+            HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48, c->digs,
+                                          c->stream, u ? (const uint64_t*)c->part_base2.p : nullptr, u,
+                                          u ? n2 : 0, u ? (uint8_t*)(u + (size_t)W * n2) : nullptr,
+                                          u ? kp[kpi + 1] : 256u));
+            HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+            HIPCHK(c, hipEventSynchronize(c->ev1));
+            HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+            c->part_ms[1] += t;
+            c->st.insert_launches++;
+            c->st.insert_ms += t;
+            if (u) {
+                kp_u_pass = kpi + 1;
+                kp_u_keys = u;
+                kp_u_n = n2;
+            }
+        }
 
         if (experiment_knob("KC_P2_SKIP")) {  // keys are invalid, stop after P2
             c->batches++;
@@ -745,7 +798,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         if (n > 0) {
             // P3 tiles: regions (P2 digits) cut into tiles of their own
             std::vector<uint64_t> rt(2 * 257);
-            HIPCHK(c, hipMemcpy2DAsync(rt.data(), 8, c->part_base.p, pg.nseg * 8, 8, 256, hipMemcpyDeviceToHost,
+            HIPCHK(c, hipMemcpy2DAsync(rt.data(), 8, p2_base, pg.nseg * 8, 8, 256, hipMemcpyDeviceToHost,
                                        c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             rt[256] = n;
@@ -758,7 +811,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             uint64_t* p3t = p3h + 256 * ntiles + p3_tmp_elems(ntiles);
             HIPCHK(c, hipMemcpyAsync(p3t, rt.data(), 2 * 257 * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_p3_hist(W, c->digs, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
+            HIPCHK(c, launch_p3_hist(W, p2_digs, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
                                      c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
@@ -768,12 +821,14 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             // P3's scatter is the regional radix scatter (digit word0 >> 56 over
             // the 256 P2 regions, same tiles; next tile's run starts prefetched,
             // XCD-aware tile walk); KC_P3_SCATTER: the older p3_scatter_k
-            if (getenv("KC_P3_SCATTER") || p3_tile(W) != rp_tile(W, false))
+            if (getenv("KC_P3_SCATTER") || p3_tile(W) != rp_tile(W, false)) {
+                if (from_u) return fail(c, KC_ERR_INTERNAL, "p3_scatter_k reads keys_a only");
                 HIPCHK(c, launch_p3_scatter(W, c->keys_a, c->keys_b, c->key_cap, p3t, p3t + 257, ntiles, p3h,
                                             2 * c->n_cu, c->stream));
-            else
-                HIPCHK(c, launch_rp_scatter(W, false, c->keys_a, c->key_cap, c->keys_b, c->key_cap, nullptr, nullptr, p3t,
+            } else {
+                HIPCHK(c, launch_rp_scatter(W, false, p2_keys, p2_stride, c->keys_b, c->key_cap, nullptr, nullptr, p3t,
                                             p3t + 257, 256, ntiles, p3h, 56, nullptr, 0, 2 * c->n_cu, c->stream));
+            }
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -1827,6 +1882,8 @@ void kc_destroy(kc_ctx* c) {
     if (c->rec_cursor) (void)hipFree(c->rec_cursor);
     if (c->pool_cursor) (void)hipFree(c->pool_cursor);
     release(c->part_hist);
+    release(c->part_ghist);
+    release(c->part_base2);
     release(c->p3b_buf);
     release(c->run_flags);
     release(c->sub_starts);

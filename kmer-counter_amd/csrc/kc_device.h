@@ -117,11 +117,18 @@ struct PartGeom {
 };
 PartGeom part_geometry(int L, int k, uint64_t n_reads);
 // P1: hist[d * nseg + seg] = keys of segment seg with digit d = (hash >> shift) & 255
-hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* hist, int shift, hipStream_t s);
+hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* hist, int shift, hipStream_t s,
+                            int gbits = 0);
+// key-range passes: pass histogram = groups [g0, g1) of a gbits = 4 P1 histogram; group totals
+hipError_t launch_hist_group_sum(const uint64_t* h, uint64_t nseg, uint32_t g0, uint32_t g1, uint64_t* out,
+                                 hipStream_t s);
+hipError_t launch_hist_group_totals(const uint64_t* h, uint64_t nseg, uint32_t groups, uint64_t* tot, hipStream_t s);
 // P2: scatter keys to out (SoA, out_stride) at base = exclusive scan of hist;
 // also counts key 0 / holes / valid windows into l.stats
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
-                               uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s);
+                               uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s,
+                               const uint64_t* base2 = nullptr, uint64_t* out2 = nullptr,
+                               uint64_t out2_stride = 0, uint8_t* digs2 = nullptr, uint32_t fmid = 256);
 // P3 (regional scatter, see kc_kernels.hip): rstart[257] region bounds,
 // tpre[257] tile prefix per region (tiles of p3_tile(W) keys); hist holds
 // 256 * ntiles u64, tmp scan_tmp_elems(256 * ntiles) u64.

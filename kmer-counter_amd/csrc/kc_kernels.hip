@@ -307,13 +307,22 @@ struct PartArgs {
     const unsigned short* inval;  //      not-ACGT masks, G u16 per read
     int G;            //                  16-base groups per read
     u32 flo, fhi;     // key-range pass: only keys with word0 >> 56 in [flo, fhi) (P1 and P2)
+    int gbits;        // HIST: 2^gbits groups of word0 >> 56 (its top gbits bits), 256 digits each
+    // SCATTER, two key-range passes in one walk: keys with word0 >> 56 in
+    // [fmid, fhi) go to out2 (stride out2_stride, digit bytes digs2, run
+    // starts base2) as the second pass's P2 output
+    u64* out2;
+    u64 out2_stride;
+    const u64* base2;
+    unsigned char* digs2;
+    u32 fmid;
     int no_stats;     // key-range pass after the first: valid / key-0 statistics not counted again
 };
 
 static size_t sink_lds_host(int W, int sink, int scap) {
     if (sink == SINK_HIST) return 256 * 4;
     if (sink == SINK_SCATTER)
-        return 2 * 256 * 8 + 260 * 4 + 256 * 4 + 32 + (size_t)W * 8 * (scap + 1) + 2 * (size_t)scap + 16;
+        return 2 * 512 * 8 + 516 * 4 + 512 * 4 + 64 + (size_t)W * 8 * (scap + 1) + 2 * (size_t)scap + 16;
     return 0;
 }
 
@@ -327,13 +336,14 @@ __device__ __forceinline__ u64 code_word(const u32* cr, int b) {
     return o ? ((hi << (2 * o)) | (u64)(cr[g + 2] >> (32 - 2 * o))) : hi;
 }
 
-// Exclusive scan of 256 per-digit values held by threads 0..255 of a block of
-// any size (waves 0..3 scan, one barrier that every thread executes).
-// scratch: >= 4 u32. Threads >= 256 get 0.
+// Exclusive scan of NB per-digit values held by threads 0..NB-1 of a block of
+// any size (waves 0..NB/64-1 scan, one barrier that every thread executes).
+// scratch: >= NB/64 u32. Threads >= NB get 0.
+template <int NB = 256>
 __device__ __forceinline__ u32 digit_scan256(u32 v, u32* scratch, int tid) {
     const int lane = lane_id(), wave = tid >> 6;
     u32 inc = v;
-    if (tid < 256) {
+    if (tid < NB) {
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const u32 y = __shfl_up(inc, o);
@@ -343,9 +353,9 @@ __device__ __forceinline__ u32 digit_scan256(u32 v, u32* scratch, int tid) {
     }
     __syncthreads();
     u32 pre = 0;
-    if (tid < 256)
+    if (tid < NB)
         for (int w = 0; w < wave; w++) pre += scratch[w];
-    return tid < 256 ? pre + inc - v : 0u;
+    return tid < NB ? pre + inc - v : 0u;
 }
 
 constexpr int kPrefetch = 4;  // code words prefetched per thread (CODES front end)
@@ -367,12 +377,13 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                           ~(size_t)15;
     unsigned char* sk = smem + sk_off;
     u32* s_hist = (u32*)sk;                      // HIST
-    u64* s_cur = (u64*)sk;                       // SCATTER: global cursor of each digit's run
-    u64* s_gb = s_cur + 256;                     //          flush: s_cur[d] - start of d in flush order
-    u32* s_cnt = (u32*)(s_gb + 256);             //          staged keys per digit (+ trash counter 256)
-    u32* s_fill = s_cnt + 256 + 4;               //          rank cursor
-    u32* s_misc = s_fill + 256;                  //          [0] staged count, [4..7] scan scratch
-    u64* s_stage = (u64*)(s_misc + 8);           //          W x (scap + 1) staged keys (slot scap: trash);
+    // SCATTER slots: digit d of the (first) pass at d, of the second pass at 256 + d
+    u64* s_cur = (u64*)sk;                       // SCATTER: global cursor of each slot's run
+    u64* s_gb = s_cur + 512;                     //          flush: s_cur[d] - start of d in flush order
+    u32* s_cnt = (u32*)(s_gb + 512);             //          staged keys per slot (+ trash counter 512)
+    u32* s_fill = s_cnt + 512 + 4;               //          rank cursor
+    u32* s_misc = s_fill + 512;                  //          [0] staged count, [4..11] scan scratch
+    u64* s_stage = (u64*)(s_misc + 16);          //          W x (scap + 1) staged keys (slot scap: trash);
                                                  //          the digit is recomputed from word 0
     unsigned short* s_perm = (unsigned short*)(s_stage + (size_t)W * (pa.scap + 1));  // scap flush order
     u32* scan_tmp = s_misc + 4;
@@ -415,11 +426,12 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
 
     for (u64 unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
         if constexpr (SINK == SINK_HIST) {
-            if (tid < 256) s_hist[tid] = 0;
+            for (int i = tid; i < (256 << pa.gbits); i += NT) s_hist[i] = 0;
         } else if constexpr (SINK == SINK_SCATTER) {
-            if (tid < 256) {
+            if (tid < 512) {
                 s_cnt[tid] = 0;
-                s_cur[tid] = pa.base[(u64)tid * pa.nseg + unit];
+                s_cur[tid] = tid < 256 ? pa.base[(u64)tid * pa.nseg + unit]
+                                       : (pa.out2 ? pa.base2[(u64)(tid - 256) * pa.nseg + unit] : 0ull);
             }
             if (tid == 0) s_misc[0] = 0;
         }
@@ -514,7 +526,8 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             const int nchr = (nw + kRoll - 1) / kRoll;
             const int total = nr * nchr;
             if constexpr (SINK == SINK_SCATTER) {
-                const bool filt = pa.fhi - pa.flo < 256u;
+                const bool filt = pa.fhi - pa.flo < 256u || pa.out2 != nullptr;
+                const u32 fmid = pa.out2 ? pa.fmid : 256u;  // first slot of the second pass: word0 >> 56 >= fmid
                 // Two phases per run of kRoll windows. A: roll the windows once
                 // to get the lane's live mask (valid, non-zero keys). One LDS
                 // reservation per wave covers all kRoll steps: step s of the
@@ -607,7 +620,9 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                                 const u32 idx = wbase + soff[sstep] + (u32)__popcll(bal[sstep] & lt);
 #pragma unroll
                                 for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
-                                atomicAdd(&s_cnt[(u32)(key[0] >> pa.shift) & 255u], 1u);
+                                atomicAdd(&s_cnt[((u32)(key[0] >> 56) >= fmid ? 256u : 0u) |
+                                                 ((u32)(key[0] >> pa.shift) & 255u)],
+                                          1u);
                             }
 #pragma unroll
                             for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
@@ -630,7 +645,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                         const u32 d = (u32)(key[0] >> pa.shift) & 255u;
 #pragma unroll
                         for (int j = 0; j < W; j++) s_stage[(size_t)j * (pa.scap + 1) + idx] = key[j];
-                        atomicAdd(&s_cnt[lv ? d : 256u], 1u);
+                        atomicAdd(&s_cnt[lv ? d : 512u], 1u);
 #pragma unroll
                         for (int j = 0; j < W - 1; j++) raw[j] = (raw[j] << 2) | (raw[j + 1] >> 62);
                         raw[W - 1] = (raw[W - 1] << 2) | (tail >> 62);
@@ -681,8 +696,9 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                         const bool live = valid && !is_zero;
 
                         if constexpr (SINK == SINK_HIST) {
-                            if (live && (u32)(key[0] >> 56) - pa.flo < pa.fhi - pa.flo)
-                                atomicAdd(&s_hist[(u32)(key[0] >> pa.shift) & 255u], 1u);
+                            const u32 top = (u32)(key[0] >> 56);
+                            if (live && top - pa.flo < pa.fhi - pa.flo)
+                                atomicAdd(&s_hist[((top >> (8 - pa.gbits)) << 8) | ((u32)(key[0] >> pa.shift) & 255u)], 1u);
                         } else {
                             // key 0^W: one atomic per wave
                             u64 zmask = __ballot(valid && is_zero);
@@ -735,30 +751,36 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                 // each digit's run with consecutive lanes
                 const u32 n = s_misc[0];
                 if (tile + 1 == t_end || n + (u32)pa.max_win > (u32)pa.scap) {
-                    const u32 st = digit_scan256(tid < 256 ? s_cnt[tid] : 0u, scan_tmp, tid);
-                    if (tid < 256) {
+                    const u32 fmid = pa.out2 ? pa.fmid : 256u;
+                    auto slot = [&](u64 k0) {
+                        return ((u32)(k0 >> 56) >= fmid ? 256u : 0u) | ((u32)(k0 >> pa.shift) & 255u);
+                    };
+                    const u32 st = digit_scan256<512>(tid < 512 ? s_cnt[tid] : 0u, scan_tmp, tid);
+                    if (tid < 512) {
                         s_fill[tid] = st;
                         s_gb[tid] = s_cur[tid] - st;
                     }
                     __syncthreads();
                     for (u32 i = tid; i < n; i += NT) {
-                        u32 q = atomicAdd(&s_fill[(u32)(s_stage[i] >> pa.shift) & 255u], 1u);
+                        u32 q = atomicAdd(&s_fill[slot(s_stage[i])], 1u);
                         s_perm[q] = (unsigned short)i;
                     }
                     __syncthreads();
                     for (u32 q = tid; q < n; q += NT) {
                         const u32 i = s_perm[q];
                         const u64 k0 = s_stage[i];
-                        const u64 g = s_gb[(u32)(k0 >> pa.shift) & 255u] + q;
+                        const u32 sl = slot(k0);
+                        const u64 g = s_gb[sl] + q;
                         if (pa.skip & 1) continue;
-                        pa.out[g] = k0;
+                        u64* __restrict__ o = sl >= 256u ? pa.out2 : pa.out;
+                        const u64 ost = sl >= 256u ? pa.out2_stride : pa.out_stride;
+                        o[g] = k0;
 #pragma unroll
-                        for (int j = 1; j < W; j++)
-                            pa.out[(u64)j * pa.out_stride + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
-                        pa.digs[g] = (unsigned char)(k0 >> 56);
+                        for (int j = 1; j < W; j++) o[(u64)j * ost + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
+                        (sl >= 256u ? pa.digs2 : pa.digs)[g] = (unsigned char)(k0 >> 56);
                     }
                     __syncthreads();
-                    if (tid < 256) {
+                    if (tid < 512) {
                         s_cur[tid] += s_cnt[tid];
                         s_cnt[tid] = 0;
                     }
@@ -769,7 +791,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
         }
         if constexpr (SINK == SINK_HIST) {
             __syncthreads();
-            if (tid < 256) pa.hist[(u64)tid * pa.nseg + unit] = s_hist[tid];
+            for (int i = tid; i < (256 << pa.gbits); i += NT) pa.hist[(u64)i * pa.nseg + unit] = s_hist[i];
             __syncthreads();
         }
     }
@@ -1002,7 +1024,9 @@ PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     return p;
 }
 
-hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* hist, int shift, hipStream_t s) {
+hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* hist, int shift, hipStream_t s,
+                            int gbits) {
+    if (gbits < 0 || gbits > 4) return hipErrorInvalidValue;
     if (l.n_reads == 0) return hipSuccess;
     const CountGeom& g = pg.geom;
     CountArgs a = make_args(l, g);
@@ -1020,17 +1044,19 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
     pa.flo = l.flo;
     pa.fhi = l.fhi;
     pa.no_stats = l.no_stats ? 1 : 0;
+    pa.gbits = gbits;
     pa.shift = shift;
     pa.max_win = pg.max_win;
     pa.scap = pg.scap;
-    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_HIST, pg.scap);
+    size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + ((size_t)256 << gbits) * 4;
     int grid = (int)hmin(pg.nseg, 4096);
     KC_FRONT_SWITCH(SINK_HIST, true, kBlock, grid, lds, s, a, pa)
     return hipGetLastError();
 }
 
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
-                               uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s) {
+                               uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s, const uint64_t* base2,
+                               uint64_t* out2, uint64_t out2_stride, uint8_t* digs2, uint32_t fmid) {
     if (l.n_reads == 0) return hipSuccess;
     const CountGeom& g = pg.geom;
     CountArgs a = make_args(l, g);
@@ -1051,6 +1077,12 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa.flo = l.flo;
     pa.fhi = l.fhi;
     pa.no_stats = l.no_stats ? 1 : 0;
+    if (out2 && (!base2 || !digs2 || fmid <= l.flo || fmid >= l.fhi)) return hipErrorInvalidValue;
+    pa.out2 = out2;
+    pa.out2_stride = out2_stride;
+    pa.base2 = base2;
+    pa.digs2 = (unsigned char*)digs2;
+    pa.fmid = fmid;
     pa.shift = shift;
     pa.max_win = pg.max_win;
     pa.scap = pg.scap;
@@ -1058,6 +1090,50 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     size_t lds = ((g.lds + 15) & ~(size_t)15) + 16 + sink_lds_host(W, SINK_SCATTER, pg.scap);
     int grid = (int)hmin(pg.nseg, 4096);
     KC_FRONT_SWITCH(SINK_SCATTER, true, kP2Block, grid, lds, s, a, pa)
+    return hipGetLastError();
+}
+
+// Key-range passes: a P1 histogram of 16 groups (word0 >> 60) x 256 digits
+// per segment (launch_part_hist, gbits = 4) gives every pass its digit x
+// segment histogram without walking the reads again (groups [g0, g1)
+// summed), and the planner its group totals.
+__global__ __launch_bounds__(kBlock) void hist_group_sum_k(const u64* __restrict__ h, u64 nseg, u32 g0, u32 g1,
+                                                           u64* __restrict__ out) {
+    const u64 n = 256 * nseg;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+        u64 v = 0;
+        for (u32 g = g0; g < g1; g++) v += h[(u64)g * n + i];
+        out[i] = v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void hist_group_totals_k(const u64* __restrict__ h, u64 nseg,
+                                                              u64* __restrict__ tot) {
+    __shared__ u64 part[kBlock / 64];
+    const u64 n = 256 * nseg;
+    const u64* hg = h + (u64)blockIdx.x * n;
+    u64 v = 0;
+    for (u64 i = threadIdx.x; i < n; i += kBlock) v += hg[i];
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 t = 0;
+        for (int w = 0; w < kBlock / 64; w++) t += part[w];
+        tot[blockIdx.x] = t;
+    }
+}
+
+hipError_t launch_hist_group_sum(const uint64_t* h, uint64_t nseg, uint32_t g0, uint32_t g1, uint64_t* out,
+                                 hipStream_t s) {
+    const u64 n = 256 * nseg;
+    const int grid = (int)hmin((n + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(hist_group_sum_k, dim3(grid), dim3(kBlock), 0, s, (const u64*)h, (u64)nseg, g0, g1, (u64*)out);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_group_totals(const uint64_t* h, uint64_t nseg, uint32_t groups, uint64_t* tot, hipStream_t s) {
+    hipLaunchKernelGGL(hist_group_totals_k, dim3(groups), dim3(kBlock), 0, s, (const u64*)h, (u64)nseg, (u64*)tot);
     return hipGetLastError();
 }
 

@@ -2463,40 +2463,28 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                     ++sub;
                     continue;
                 }
-                u64 rbase = 0;
+                // one scan of the table: each wave's occupied slots of a
+                // 64-slot chunk take consecutive places from an LDS cursor
+                // (record order inside the bucket is free: the finish sorts)
                 const u32 nclaimed = *lfill;
-                if (tid == 0 && nclaimed)
-                    rbase = atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)nclaimed);
-                if (pf_next) prefetch_pass(b + gridDim.x);
-                u32 wc = 0;
-                for (u32 c0 = s0; c0 < s1; c0 += 64) {
-                    const u32 i = c0 + (u32)lane;
-                    const bool occ = i < s1 && ((W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u));
-                    wc += (u32)__popcll(__ballot(occ));
-                }
-                if (lane == 0) wtot_l[wave] = wc;
-                __syncthreads();
-                u32 total = 0, before = 0;
-                for (int w = 0; w < kBucketWaves; w++) {
-                    const u32 v = wtot_l[w];
-                    before += w < wave ? v : 0u;
-                    total += v;
-                }
                 if (tid == 0) {
-                    *(u64*)(misc + 16) = rbase;
-                    if (rbase + total > a.rec_cap || total != nclaimed)
-                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
-                    *lfill = 0;
-                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
+                    *(u64*)(misc + 16) =
+                        nclaimed ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)nclaimed) : 0ull;
+                    misc[24] = 0u;
                 }
+                if (pf_next) prefetch_pass(b + gridDim.x);
                 __syncthreads();
-                u64 pos = *(u64*)(misc + 16) + before;
+                const u64 rbase = *(const u64*)(misc + 16);
                 for (u32 c0 = s0; c0 < s1; c0 += 64) {
                     const u32 i = c0 + (u32)lane;
                     const bool occ = i < s1 && ((W == 1) ? (lkeys[i] != 0ull) : (lstate[i] == 2u));
                     const u64 bm = __ballot(occ);
+                    if (bm == 0ull) continue;
+                    u32 at = 0;
+                    if (lane == 0) at = atomicAdd(&misc[24], (u32)__popcll(bm));
+                    at = (u32)__builtin_amdgcn_readfirstlane((int)at);
                     if (occ) {
-                        const u64 qq = pos + (u64)__popcll(bm & lane_lt);
+                        const u64 qq = rbase + at + (u64)__popcll(bm & lane_lt);
                         if (qq < a.rec_cap) {
 #pragma unroll
                             for (int j = 0; j < W; j++)
@@ -2508,7 +2496,14 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                         lcnt[i] = 0;
                         if constexpr (W >= 2) lstate[i] = 0;
                     }
-                    pos += (u64)__popcll(bm);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    const u32 total = misc[24];
+                    if (rbase + total > a.rec_cap || total != nclaimed)
+                        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
+                    *lfill = 0;
+                    atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
                 }
             }
             __syncthreads();

@@ -595,7 +595,7 @@ def test_key_range_passes(kca, orc, monkeypatch, capfd, k):
     n = max(180000, (1 << 24) // (L - k + 1) + 2000)  # the coverage sketch needs 2^24 keys
     fq = _fastq_from_codes(_hc_reads(np.random.default_rng(k + 101), n, L, dup=n // 20))
     outs, sts = [], []
-    for env in ((), ("KC_NO_KEY_PASSES",)):
+    for env in ((), ("KC_NO_DUAL_PASS",), ("KC_NO_KEY_PASSES",)):
         for v in env:
             monkeypatch.setenv(v, "1")
         with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=128 << 20) as ctx:
@@ -605,11 +605,15 @@ def test_key_range_passes(kca, orc, monkeypatch, capfd, k):
         for v in env:
             monkeypatch.delenv(v)
     err = capfd.readouterr().err
-    assert sts[0]["key_passes"] >= 2 and sts[1]["key_passes"] == 0, err[-3000:]
+    assert sts[0]["key_passes"] >= 2 and sts[2]["key_passes"] == 0, err[-3000:]
+    # two passes per P2 walk by default, one per walk under KC_NO_DUAL_PASS
+    assert sts[0]["insert_launches"] == (sts[0]["key_passes"] + 1) // 2
+    assert sts[1]["insert_launches"] == sts[1]["key_passes"]
     direct = [x for x in err.splitlines() if "kc: P5s direct pass" in x]
-    assert len(direct) == sts[0]["key_passes"] and all("kept=1" in x for x in direct), err[-3000:]
-    assert sts[1]["spill_runs"] >= 2
-    assert outs[0] == outs[1] == orc.count_fastq(fq, k)
+    assert len(direct) == sts[0]["key_passes"] + sts[1]["key_passes"] and all("kept=1" in x for x in direct), \
+        err[-3000:]
+    assert sts[2]["spill_runs"] >= 2
+    assert outs[0] == outs[1] == outs[2] == orc.count_fastq(fq, k)
 
 
 @pytest.mark.parametrize("k", [31, 55])
