@@ -982,7 +982,7 @@ hipError_t launch_encode_reads_var(const uint8_t* base, const uint64_t* seq_off,
 
 // P2 workgroup: kP2Block threads, one per CU, most of the CU's LDS for staging
 constexpr int kP2Block = 1024;
-constexpr size_t kPartLds = 152 * 1024;  // + alignment and the sink's fixed arrays stays under 160 KiB
+constexpr size_t kPartLds = 160 * 1024 - 512;  // the P2 workgroup's LDS (front + sink, with alignment) stays under 160 KiB
 
 PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     PartGeom p;
@@ -1007,7 +1007,10 @@ PartGeom part_geometry(int L, int k, uint64_t n_reads) {
     const size_t per_key = (size_t)W * 8 + 2;  // staged key words + u16 permutation entry
     while (g.R > 1 && front(g.R) + sink_lds_host(W, SINK_SCATTER, 2 * g.R * nw) > kPartLds) g.R--;
     g.R = balance_reads(g.R, nw, kP2Block);
-    size_t room = kPartLds > front(g.R) + 4096 ? kPartLds - front(g.R) - 4096 : 0;
+    // staging room: what the front end and the sink's fixed arrays (slot
+    // cursors and counters, sink_lds_host at scap = 0) leave
+    const size_t fixed = sink_lds_host(W, SINK_SCATTER, 0) + 64;
+    size_t room = kPartLds > front(g.R) + fixed ? kPartLds - front(g.R) - fixed : 0;
     int scap = (int)(room / per_key);
     if (scap > 65535) scap = 65535;  // u16 permutation indices
     if (scap < g.R * nw) scap = g.R * nw;
