@@ -1367,12 +1367,6 @@ static const double kSketchDistinctMax = 0.7;
 static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre0) {
     kc_status s;
     const uint64_t G = (uint64_t)groups_per_read((int)L);
-    // the first reads holding 2^26 group-aligned k-mers: the engine choice
-    // changes speed only, never counts, and a batch's first ~6M reads tell
-    // high from low coverage (cfg2 at 30x reads as 3.8x there, 27% distinct)
-    // at an eighth of the cost of walking all of them
-    const uint64_t sketch_reads = ((1ull << 26) + G - 1) / G;
-    if (n_reads > sketch_reads) n_reads = sketch_reads;
     // sample rate 2^-rb by k-mer hash: about 2^18 samples (at least 1/256)
     const uint64_t aligned = n_reads * G;
     int rb = 8;
