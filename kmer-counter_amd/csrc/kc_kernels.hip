@@ -791,7 +791,14 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
         }
         if constexpr (SINK == SINK_HIST) {
             __syncthreads();
-            for (int i = tid; i < (256 << pa.gbits); i += NT) pa.hist[(u64)i * pa.nseg + unit] = s_hist[i];
+            if (pa.gbits == 0) {
+                for (int i = tid; i < 256; i += NT) pa.hist[(u64)i * pa.nseg + unit] = s_hist[i];
+            } else {
+                // grouped (key-range passes): the unit's bins contiguous, u32
+                // (hist_group_sum_k transposes a pass's groups to digit-major)
+                u32* h32 = (u32*)pa.hist + (u64)unit * (256u << pa.gbits);
+                for (int i = tid; i < (256 << pa.gbits); i += NT) h32[i] = s_hist[i];
+            }
             __syncthreads();
         }
     }
@@ -1100,43 +1107,72 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
 // per segment (launch_part_hist, gbits = 4) gives every pass its digit x
 // segment histogram without walking the reads again (groups [g0, g1)
 // summed), and the planner its group totals.
-__global__ __launch_bounds__(kBlock) void hist_group_sum_k(const u64* __restrict__ h, u64 nseg, u32 g0, u32 g1,
+__global__ __launch_bounds__(kBlock) void hist_group_sum_k(const u32* __restrict__ h, u64 nseg, u32 g0, u32 g1,
                                                            u64* __restrict__ out) {
-    const u64 n = 256 * nseg;
-    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
-        u64 v = 0;
-        for (u32 g = g0; g < g1; g++) v += h[(u64)g * n + i];
-        out[i] = v;
+    // h: per segment 4096 u32 bins (group g, digit d at g * 256 + d); out:
+    // the pass's digit-major histogram out[d * nseg + seg]. 32 segments per
+    // step through an LDS tile: loads contiguous per segment, stores 32
+    // consecutive segments of one digit
+    __shared__ u32 tile[256][33];
+    const int tid = threadIdx.x;
+    for (u64 s0 = (u64)blockIdx.x * 32; s0 < nseg; s0 += (u64)gridDim.x * 32) {
+        const u32 ns = (u32)min((u64)32, nseg - s0);
+        for (u32 j = 0; j < ns; j++) {
+            const u32* hs = h + (s0 + j) * 4096u;
+            u32 v = 0;
+            for (u32 g = g0; g < g1; g++) v += hs[g * 256u + (u32)tid];
+            tile[tid][j] = v;
+        }
+        __syncthreads();
+        for (u32 x = (u32)tid; x < 256u * 32u; x += kBlock) {
+            const u32 d = x >> 5, j = x & 31u;
+            if (j < ns) out[(u64)d * nseg + s0 + j] = tile[d][j];
+        }
+        __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(kBlock) void hist_group_totals_k(const u64* __restrict__ h, u64 nseg,
+// group totals (tot zeroed by the caller): thread t holds bin t of every
+// group for the block's segments, summed per group across the block
+__global__ __launch_bounds__(kBlock) void hist_group_totals_k(const u32* __restrict__ h, u64 nseg,
                                                               u64* __restrict__ tot) {
-    __shared__ u64 part[kBlock / 64];
-    const u64 n = 256 * nseg;
-    const u64* hg = h + (u64)blockIdx.x * n;
-    u64 v = 0;
-    for (u64 i = threadIdx.x; i < n; i += kBlock) v += hg[i];
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+    __shared__ u64 part[16][kBlock / 64];
+    u64 v[16];
+#pragma unroll
+    for (int g = 0; g < 16; g++) v[g] = 0;
+    for (u64 sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const u32* hs = h + sg * 4096u + threadIdx.x;
+#pragma unroll
+        for (int g = 0; g < 16; g++) v[g] += hs[g * 256];
+    }
+#pragma unroll
+    for (int g = 0; g < 16; g++) {
+        u64 x = v[g];
+        for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+        if (lane_id() == 0) part[g][threadIdx.x >> 6] = x;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 16) {
         u64 t = 0;
-        for (int w = 0; w < kBlock / 64; w++) t += part[w];
-        tot[blockIdx.x] = t;
+        for (int w = 0; w < kBlock / 64; w++) t += part[threadIdx.x][w];
+        if (t) atomicAdd((unsigned long long*)&tot[threadIdx.x], (unsigned long long)t);
     }
 }
 
 hipError_t launch_hist_group_sum(const uint64_t* h, uint64_t nseg, uint32_t g0, uint32_t g1, uint64_t* out,
                                  hipStream_t s) {
-    const u64 n = 256 * nseg;
-    const int grid = (int)hmin((n + kBlock - 1) / kBlock, 8192);
-    hipLaunchKernelGGL(hist_group_sum_k, dim3(grid), dim3(kBlock), 0, s, (const u64*)h, (u64)nseg, g0, g1, (u64*)out);
+    if (g1 > 16 || g0 >= g1) return hipErrorInvalidValue;
+    const int grid = (int)hmin((nseg + 31) / 32, 4096);
+    hipLaunchKernelGGL(hist_group_sum_k, dim3(grid), dim3(kBlock), 0, s, (const u32*)h, (u64)nseg, g0, g1, (u64*)out);
     return hipGetLastError();
 }
 
 hipError_t launch_hist_group_totals(const uint64_t* h, uint64_t nseg, uint32_t groups, uint64_t* tot, hipStream_t s) {
-    hipLaunchKernelGGL(hist_group_totals_k, dim3(groups), dim3(kBlock), 0, s, (const u64*)h, (u64)nseg, (u64*)tot);
+    if (groups != 16) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(tot, 0, 16 * 8, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(hist_group_totals_k, dim3((u32)hmin(nseg, 1024)), dim3(kBlock), 0, s, (const u32*)h, (u64)nseg,
+                       (u64*)tot);
     return hipGetLastError();
 }
 
