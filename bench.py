@@ -1,40 +1,51 @@
 #!/usr/bin/env python3
 """Benchmark of the k-mer count path (BASELINE.json metric).
 
-`value` is SURVEY §8d's end-to-end rate: k-mers / wall seconds from the first
-FASTQ byte in to the output file closed. Workload (BASELINE.json configs[1],
-cfg 2): k=31, 50M x 150 bp reads per GPU sampled from a 250 Mbp random genome
-(splitmix64 generator, seed 2), written untimed to a FASTQ file in the work
-directory (page cache: host memory). One step =
-  kc_reset; kc_count_file (pread into pinned blocks, PCIe upload, GPU FASTQ
-  decode, counting) ; kc_finish (sorted SortedKMerFile records in HBM);
-  kc_write_output (device -> pinned -> the output file, closed).
-The timed region is exactly K such steps, bracketed by barrier + device
-synchronize, max over ranks.
+Workload (BASELINE.json configs[1], cfg 2): k=31, 50M x 150 bp reads per GPU
+sampled from a 250 Mbp random genome (splitmix64 generator, seed 2),
+generated in HBM before timing.
+
+`value` (the task contract: inputs resident in HBM when the timed region
+starts) is the device-resident rate: one step = kc_reset; kc_count_fastq_device
+(GPU FASTQ decode + 2-bit encode + counting) ; kc_finish (the sorted
+SortedKMerFile records in HBM); at N > 1 also the exchange below. The timed
+region is exactly K such steps after W warmup steps, bracketed by barrier +
+device synchronize, max over ranks. `roofline` prices the step's dominant
+kernel and `path_frac` the whole step (SURVEY §8d bytes per k-mer).
 
 Sub-objects of the same line (same input, same context):
-  device_resident : the FASTQ already in HBM, records left in HBM (the
-                    kernel-only figure; roofline and per-kernel rates);
+  end_to_end      : SURVEY §8d's PCIe-inclusive rate, from the first FASTQ byte
+                    of a file (page cache) to the SortedKMerFile closed:
+                    kc_count_file (pread into pinned blocks, PCIe upload, GPU
+                    decode, count), kc_finish, kc_write_output. Each step writes
+                    a new output file, deleted right after the step (outside
+                    its interval); the input file is written untimed into the
+                    first of $TMPDIR, /tmp, /dev/shm, ... with room for it
+                    (statvfs). N = 1 by default (--e2e at N > 1);
   host_memory     : the FASTQ in (pageable) host memory, one kc_count_fastq
                     call, output file written;
   reference_chunks: the same reads as the reference's chunks (concatenated
                     sequences of 7.8 MB at gpuMemoryLimit=1e8,
                     KMerCounter.cpp:193-212) through ~960 kc_count_chunk calls
-                    vs one kc_count_chunk call of all of them, output in HBM.
+                    vs one kc_count_chunk call of all of them, output in HBM;
+  cpu_baseline    : the CPU port of the reference pipeline on a bounded sample
+                    (N = 1, rank 0).
 
 N GPUs (one process per GPU, torch.distributed; RCCL = backend nccl): rank r
-counts reads [r R, (r+1) R) from its own input file (weak scaling).
+counts reads [r R, (r+1) R) of the one read stream (weak scaling).
   --exchange alltoall (default at N > 1): the sorted runs are
     exchanged by key-space owner (RCCL all-to-all) and merged on the device;
-    every rank writes its owned key range as its own part file; the parts in
-    rank order are the node's SortedKMerFile (concatenation, no merge).
+    rank r owns the r-th key range (in the e2e leg it writes it as its own part
+    file); the parts in rank order are the node's SortedKMerFile.
   --exchange none (cfg3, read-shard): the runs are gathered to rank 0's GPU
     (RCCL) and merged there (device merge path), rank 0 writes the file.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5] [--reads R] [--exchange alltoall|none]
-                    [--mode e2e|device] [--no-cpu] [--no-variants] [--workdir DIR] [--min-read-length M]
+                    [--value device|e2e] [--e2e|--no-e2e] [--no-cpu] [--no-variants] [--workdir DIR]
+                    [--min-read-length M]
 
-Prints one JSON line on rank 0 (contract in the task statement).
+Prints one JSON line on rank 0 (contract in the task statement); a failure
+prints one line with an `error` field instead and exits 1.
 """
 import argparse
 import importlib.util
@@ -236,41 +247,37 @@ def write_node_output(kca, ctx, D, path, exchange):
     return n * ctx.rs
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
-                    help="SURVEY §8d preset: 2 = k=31, 50M x 150 bp from a 250 Mbp genome (the metric's "
-                         "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality) with a "
-                         "48 GiB working set: the records outgrow half of it and are cut into sorted runs (the "
-                         "spill -> sort -> merge path), merged on the device")
-    ap.add_argument("--mode", default="e2e", choices=["e2e", "device"],
-                    help="value = file-to-file rate (e2e) or the device-resident rate (device)")
-    ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
-    ap.add_argument("--k", type=int, default=None)
-    ap.add_argument("--L", type=int, default=150)
-    ap.add_argument("--genome", type=int, default=None, help="0 = iid uniform reads")
-    ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--mem", type=int, default=None, help="gpuMemoryLimit per GPU (bytes)")
-    ap.add_argument("--engine", default="auto", choices=["auto", "skm", "partition", "table"])
-    ap.add_argument("--cpu-reads", type=int, default=1_000_000)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-variants", action="store_true", help="skip the host_memory / reference_chunks lines")
-    ap.add_argument("--workdir", default=None, help="input/output files (default $TMPDIR or /tmp)")
-    ap.add_argument("--min-read-length", type=int, default=0,
-                    help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
-    ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
-                    help="N>1: key-space all-to-all (cfg4) or read-shard + merge on rank 0 (cfg3)")
-    args = ap.parse_args()
-    preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
-              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=48 << 30)}[args.config]
-    for key, v in preset.items():
-        if getattr(args, key) is None:
-            setattr(args, key, v)
+def pick_workdir(explicit, need_bytes):
+    """Directory for the e2e leg's input and output files: --workdir, else the
+    first of $TMPDIR, /tmp, /dev/shm, /var/tmp and the repository that has
+    `need_bytes` free (os.statvfs). Returns (dir, free bytes, tried)."""
+    cands = [explicit] if explicit else [os.environ.get("TMPDIR"), "/tmp", "/dev/shm", "/var/tmp", ROOT]
+    tried = {}
+    for d in cands:
+        if not d or d in tried or not os.path.isdir(d) or not os.access(d, os.W_OK):
+            continue
+        st = os.statvfs(d)
+        tried[d] = st.f_bavail * st.f_frsize
+        if tried[d] >= need_bytes:
+            return d, tried[d], tried
+    return None, 0, tried
 
-    D = Dist()
+
+def write_input_file(ctx, ptr, nbytes, path, piece=256 << 20):
+    """The device FASTQ to a file through one bounded host buffer (the host
+    never holds the whole input)."""
+    import numpy as np
+
+    buf = np.empty(min(piece, max(1, nbytes)), dtype=np.uint8)
+    with open(path, "wb") as f:
+        for off in range(0, nbytes, piece):
+            n = min(piece, nbytes - off)
+            ctx.copy_to_host_addr(buf.ctypes.data, ptr + off, n)
+            f.write(memoryview(buf)[:n])
+    del buf
+
+
+def main(args, D, state):
     import numpy as np
 
     kca = load_pkg()
@@ -279,79 +286,18 @@ def main():
     varlen = 0 < args.min_read_length < L
     ctx = kca.Context(kmer_length=k, line_length=L, device=D.device, gpu_memory_limit=args.mem,
                       engine=args.engine, variable_length=varlen)
+    state["ctx"] = ctx
     first = shard_first(D.rank, args.reads)
     lmin = args.min_read_length if varlen else 0
     ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first, lmin)
+    state["ptr"] = ptr
     exchange = args.exchange if D.world > 1 else "none"
-
-    # ---- input file (untimed): the same bytes, in the page cache ---------------
-    workdir = args.workdir or os.environ.get("TMPDIR") or "/tmp"
-    in_path = os.path.join(workdir, f"kc_bench_in.{os.getpid()}.fq")
-    out_path = os.path.join(workdir, f"kc_bench_out.{os.getpid() if D.world == 1 else 'node'}.bin")
-    host = np.empty(nbytes, dtype=np.uint8)
-    ctx.copy_to_host_addr(host.ctypes.data, ptr, nbytes)
-    host.tofile(in_path)
-    rs = ctx.rs
 
     def windows_of_step(st):
         return st["windows"] if varlen else args.reads * (L - k + 1)
 
-    # ---- end-to-end: file in -> output file closed -------------------------------
-    phase = {"count_file": 0.0, "finish": 0.0, "output": 0.0}
-    out_bytes = [0]
-    out_files = []
-
-    def e2e_step():
-        # every step writes a new output file (no page cache of an earlier
-        # output to overwrite); the files are removed after the timed region
-        path = f"{out_path}.{len(out_files)}"
-        out_files.append(path)
-        t0 = time.perf_counter()
-        ctx.reset()
-        ctx.count_file(in_path, L if varlen else 0)
-        t1 = time.perf_counter()
-        ctx.finish()
-        t2 = time.perf_counter()
-        out_bytes[0] = write_node_output(kca, ctx, D, path, exchange)
-        t3 = time.perf_counter()
-        phase["count_file"] += t1 - t0
-        phase["finish"] += t2 - t1
-        phase["output"] += t3 - t2
-
-    def timed(step, steps, warmup):
-        for _ in range(warmup):
-            step()
-        for key in phase:
-            phase[key] = 0.0
-        D.barrier_sync()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        D.barrier_sync()
-        return D.max(time.perf_counter() - t0)
-
-    e2e = None
-    if args.mode == "e2e":
-        el = timed(e2e_step, args.steps, args.warmup)
-        for p in out_files:
-            for q in (p, f"{p}.part{D.rank}"):
-                if os.path.exists(q) and (D.rank == 0 or q != p):
-                    os.unlink(q)
-        st = ctx.stats()
-        win = D.sum(windows_of_step(st))
-        in_b = D.sum(nbytes)
-        step_s = el / args.steps
-        ph = {key: v / args.steps * 1e3 for key, v in phase.items()}
-        e2e = {"value": win / step_s, "ms_per_step": step_s * 1e3,
-               "phases_ms_rank0": {key: round(v, 2) for key, v in ph.items()},
-               "input_bytes": int(in_b), "output_bytes": int(D.sum(out_bytes[0])),
-               # PCIe / file rates of rank 0's phases (count_file includes the GPU decode and counting of
-               # whatever fits no flush before it; the output phase is D2H + file write)
-               "input_GBps_rank0": round(nbytes / (ph["count_file"] / 1e3) / 1e9, 2),
-               "output_GBps_rank0": round(out_bytes[0] / (ph["output"] / 1e3) / 1e9, 2) if ph["output"] else None,
-               "workdir": workdir}
-
-    # ---- device-resident (kernel-only) figure ----------------------------------
+    # ---- device-resident step: the FASTQ in HBM -> sorted records in HBM -------
+    # (the contract's `value`: inputs resident in HBM when the timed region starts)
     xch_ms = [0.0]
 
     def dev_step():
@@ -368,7 +314,7 @@ def main():
             xch_ms[0] += (time.perf_counter() - t) * 1e3
         return n
 
-    for _ in range(args.warmup if args.mode == "device" else 0):
+    for _ in range(args.warmup):
         dev_step()
     D.barrier_sync()
     xch_ms[0] = 0.0
@@ -394,12 +340,38 @@ def main():
         windows_per_gpu = D.sum(windows_per_gpu) / D.world
     dev_value = windows_per_gpu * D.world * args.steps / dev_el
     roofline = device_roofline(args, st, acc, windows_per_gpu, nbytes, dev_el, varlen, k, L, W)
+    device_resident = {
+        "value": dev_value, "ms_per_step": dev_el / args.steps * 1e3,
+        "breakdown_ms_per_step": {"fastq_index": acc["decode_ms"] / args.steps,
+                                  "finish": acc["finish_ms"] / args.steps,
+                                  "exchange_rank0": xch_ms[0] / args.steps,
+                                  "partition_passes": [round(x / args.steps, 3) for x in acc["part_ms"]],
+                                  "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3),
+                                  "p3b_presplit (in partition_passes[2])": round(acc["presplit_ms"] / args.steps, 3)},
+    }
+    stats_dev = st
+
+    # ---- end-to-end: FASTQ file in -> SortedKMerFile closed (PCIe-inclusive) ----
+    e2e = None
+    run_e2e = args.e2e if args.e2e is not None else (D.world == 1)
+    if run_e2e:
+        try:
+            e2e = e2e_leg(kca, ctx, D, args, state, ptr, nbytes, exchange, windows_of_step)
+        except Exception as ex:  # reported in the line; the device figure stands
+            e2e = {"error": f"{type(ex).__name__}: {ex}"}
+    elif D.world > 1:
+        e2e = {"skipped": "N > 1: the file-to-file leg runs with --e2e (each rank writes its own 15.7 GB input file)"}
 
     # ---- host-memory input and the reference's chunks (N = 1) --------------------
     variants = {}
     if D.world == 1 and not args.no_variants and not varlen:
-        variants = host_variants(kca, ctx, args, host, nbytes, out_path, k, L)
-    del host
+        try:
+            variants = host_variants(kca, ctx, args, state, nbytes, k, L)
+        except Exception as ex:
+            variants = {"error": f"{type(ex).__name__}: {ex}"}
+    for p in list(state.get("files", [])):
+        _unlink(p)
+    state["files"] = []
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu:
@@ -413,33 +385,22 @@ def main():
     lens = f"{args.min_read_length}..{L} bp (variable-length, KC_FLAG_VARLEN)" if varlen else f"{L} bp"
     base = f"k={k}, {args.reads} x {lens} reads per GPU {src} (seed {args.seed})"
     cfg_tag = f"cfg{args.config}{'v' if varlen else ''}"
-    if args.mode == "e2e":
-        path_desc = ("FASTQ file (page cache) -> pinned blocks -> PCIe -> GPU decode + count -> sorted records -> "
-                     "PCIe -> SortedKMerFile closed")
-    else:
-        path_desc = "FASTQ in HBM -> sorted records in HBM (device-resident)"
+    path_desc = "FASTQ in HBM -> sorted SortedKMerFile records in HBM (device-resident)"
     if D.world == 1:
         workload, parallelism = f"{cfg_tag}: {base}; {path_desc}", "single GPU"
     elif exchange == "alltoall":
         workload = (f"cfg4 pattern at {D.world} GPUs: {base}; {path_desc}; key-space all-to-all of the sorted "
-                    f"(key, count) records + per-GPU merge, each rank writes its key range as a part file "
+                    f"(key, count) records (RCCL) + per-GPU merge: rank r owns the r-th key range "
                     f"(rank-order concatenation = the SortedKMerFile)")
         parallelism = f"read-shard count + key-space all-to-all x{D.world}"
     else:
         workload = (f"cfg3 pattern at {D.world} GPUs: {base}; {path_desc}; runs gathered to rank 0's GPU "
-                    f"(RCCL) and merged there by merge path, rank 0 writes the file")
+                    f"(RCCL) and merged there by merge path")
         parallelism = f"read-shard x{D.world} + device merge on rank 0"
 
-    device_resident = {
-        "value": dev_value, "ms_per_step": dev_el / args.steps * 1e3,
-        "breakdown_ms_per_step": {"fastq_index": acc["decode_ms"] / args.steps,
-                                  "finish": acc["finish_ms"] / args.steps,
-                                  "exchange_rank0": xch_ms[0] / args.steps,
-                                  "partition_passes": [round(x / args.steps, 3) for x in acc["part_ms"]],
-                                  "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3),
-                                  "p3b_presplit (in partition_passes[2])": round(acc["presplit_ms"] / args.steps, 3)},
-    }
-    if args.mode == "e2e":
+    if args.value == "e2e":
+        if not e2e or "value" not in e2e:
+            raise RuntimeError(f"--value e2e but the end-to-end leg did not run: {e2e}")
         value, ms = e2e["value"], e2e["ms_per_step"]
     else:
         value, ms = dev_value, dev_el / args.steps * 1e3
@@ -449,31 +410,192 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": workload, "k": k, "read_length": L, "reads_per_gpu": args.reads,
-                       "parallelism": parallelism, "gpu_memory_limit": args.mem, "mode": args.mode},
+                       "parallelism": parallelism, "gpu_memory_limit": args.mem, "value": args.value},
             "roofline": roofline,
             "path_frac": roofline["path_frac"],
             "cpu_baseline": cpu,
-            "end_to_end": e2e,
             "device_resident": device_resident,
+            "end_to_end": e2e,
             "host_variants": variants or None,
             "engine": args.engine,
             "engines_used": {1: "skm", 2: "key-prefix partition", 3: "skm + key-prefix",
-                             4: "table"}.get(st.get("engines_used", 0), str(st.get("engines_used"))),
-            "distinct_kmers_per_gpu": n_rec, "spilled_kmers": st["spilled_kmers"], "spill_runs": st["spill_runs"],
-            "key_passes": st.get("key_passes", 0),
+                             4: "table"}.get(stats_dev.get("engines_used", 0), str(stats_dev.get("engines_used"))),
+            "distinct_kmers_per_gpu": n_rec, "spilled_kmers": stats_dev["spilled_kmers"],
+            "spill_runs": stats_dev["spill_runs"], "key_passes": stats_dev.get("key_passes", 0),
         }
         print(json.dumps(line), flush=True)
-    for p in (in_path, out_path, f"{out_path}.part{D.rank}"):
-        try:
-            if D.rank == 0 or p != out_path:
-                os.unlink(p)
-        except OSError:
-            pass
     ctx.free_device(ptr)
+    state.pop("ptr", None)
     ctx.close()
     if D.dist is not None:
         D.dist.barrier()
         D.dist.destroy_process_group()
+
+
+def _unlink(p):
+    try:
+        os.unlink(p)
+    except OSError:
+        pass
+
+
+def e2e_leg(kca, ctx, D, args, state, ptr, nbytes, exchange, windows_of_step):
+    """The file-to-file step: kc_reset; kc_count_file (pinned read-ahead blocks,
+    PCIe upload, GPU decode + count); kc_finish; kc_write_output (device ->
+    pinned -> output file, closed). The input file is written untimed (page
+    cache). Every step writes a new output file, which is deleted right after
+    the step, outside the step's timed interval; the steps are timed one by one
+    (barrier + synchronize on both sides) and summed, so at most one output
+    file exists at a time whatever --steps is."""
+    out_est = int(nbytes * 0.3) + (64 << 20)  # records <= ~22% of the FASTQ bytes at cfg2/cfg5
+    need = nbytes + 2 * out_est + (1 << 30)
+    workdir, free, tried = pick_workdir(args.workdir, need)
+    if workdir is None:
+        return {"skipped": f"no directory with {need / 1e9:.1f} GB free for the input file and one output file",
+                "free_bytes": tried}
+    tag = os.getpid() if D.world == 1 else f"r{D.rank}"
+    in_path = os.path.join(workdir, f"kc_bench_in.{tag}.fq")
+    out_path = os.path.join(workdir, f"kc_bench_out.{os.getpid() if D.world == 1 else 'node'}.bin")
+    state.setdefault("files", []).append(in_path)
+    write_input_file(ctx, ptr, nbytes, in_path)
+    state["in_path"] = in_path
+    varlen = 0 < args.min_read_length < args.L
+    phase = {"count_file": 0.0, "finish": 0.0, "output": 0.0}
+    out_bytes = [0]
+
+    def step(path):
+        t0 = time.perf_counter()
+        ctx.reset()
+        ctx.count_file(in_path, args.L if varlen else 0)
+        t1 = time.perf_counter()
+        ctx.finish()
+        t2 = time.perf_counter()
+        out_bytes[0] = write_node_output(kca, ctx, D, path, exchange)
+        t3 = time.perf_counter()
+        return t1 - t0, t2 - t1, t3 - t2
+
+    def cleanup(path):
+        for q in (path, f"{path}.part{D.rank}"):
+            if D.rank == 0 or q != path:
+                _unlink(q)
+
+    total = 0.0
+    for i in range(args.warmup + args.steps):
+        path = f"{out_path}.{i}"
+        state["files"].extend([path, f"{path}.part{D.rank}"])
+        D.barrier_sync()
+        t0 = time.perf_counter()
+        ph = step(path)
+        D.barrier_sync()
+        dt = D.max(time.perf_counter() - t0)
+        cleanup(path)  # outside the step's interval
+        if i >= args.warmup:
+            total += dt
+            for key, v in zip(phase, ph):
+                phase[key] += v
+    st = ctx.stats()
+    win = D.sum(windows_of_step(st))
+    in_b = D.sum(nbytes)
+    step_s = total / args.steps
+    ph = {key: v / args.steps * 1e3 for key, v in phase.items()}
+    _unlink(in_path)
+    state["files"].remove(in_path)
+    state.pop("in_path", None)
+    return {"value": win / step_s, "ms_per_step": step_s * 1e3,
+            "path": ("FASTQ file (page cache) -> pinned blocks -> PCIe -> GPU decode + count -> sorted records -> "
+                     "PCIe -> SortedKMerFile closed"),
+            "phases_ms_rank0": {key: round(v, 2) for key, v in ph.items()},
+            "input_bytes": int(in_b), "output_bytes": int(D.sum(out_bytes[0])),
+            # PCIe / file rates of rank 0's phases (count_file includes the GPU decode and counting of
+            # whatever fits no flush before it; the output phase is D2H + file write)
+            "input_GBps_rank0": round(nbytes / (ph["count_file"] / 1e3) / 1e9, 2),
+            "output_GBps_rank0": round(out_bytes[0] / (ph["output"] / 1e3) / 1e9, 2) if ph["output"] else None,
+            "workdir": workdir, "workdir_free_GB": round(free / 1e9, 1),
+            "timing": "steps timed one by one (barrier + sync both sides, max over ranks) and summed; each step's "
+                      "output file deleted between steps"}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="SURVEY §8d preset: 2 = k=31, 50M x 150 bp from a 250 Mbp genome (the metric's "
+                         "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality) with a "
+                         "48 GiB working set: the keys outgrow one batch and are counted in key-range passes "
+                         "(the spill -> sort -> merge path)")
+    ap.add_argument("--value", default="device", choices=["device", "e2e"],
+                    help="value = the device-resident rate (the FASTQ resident in HBM when the timed region "
+                         "starts: the contract's definition, default) or the file-to-file rate (e2e)")
+    ap.add_argument("--mode", default=None, choices=["e2e", "device"], help="alias of --value (round-3 scripts)")
+    ap.add_argument("--e2e", dest="e2e", action="store_true", default=None,
+                    help="run the file-to-file leg (default: at N = 1 only)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false")
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU")
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--L", type=int, default=150)
+    ap.add_argument("--genome", type=int, default=None, help="0 = iid uniform reads")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--mem", type=int, default=None, help="gpuMemoryLimit per GPU (bytes)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "skm", "partition", "table"])
+    ap.add_argument("--cpu-reads", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the host_memory / reference_chunks lines")
+    ap.add_argument("--workdir", default=None, help="input/output files (default: $TMPDIR, /tmp, /dev/shm, ... "
+                                                    "whichever has the space)")
+    ap.add_argument("--min-read-length", type=int, default=0,
+                    help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
+    ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
+                    help="N>1: key-space all-to-all (cfg4) or read-shard + merge on rank 0 (cfg3)")
+    args = ap.parse_args(argv)
+    if args.mode:
+        args.value = args.mode
+        if args.mode == "e2e" and args.e2e is None:
+            args.e2e = True
+    preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
+              5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=48 << 30)}[args.config]
+    for key, v in preset.items():
+        if getattr(args, key) is None:
+            setattr(args, key, v)
+    return args
+
+
+def run():
+    """Entry point: any failure still prints one JSON line (rank 0) with an
+    `error` field, and removes the files the run wrote."""
+    import traceback
+
+    args = None
+    state = {"files": []}
+    D = None
+    try:
+        args = parse_args()
+        D = Dist()
+        main(args, D, state)
+        return 0
+    except BaseException as ex:  # noqa: B902 - report everything, then fail
+        tb = traceback.format_exc()
+        rank = int(os.environ.get("RANK", "0"))
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "k-mers/s",
+                              "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                              "steps": getattr(args, "steps", None), "warmup": getattr(args, "warmup", None),
+                              "error": f"{type(ex).__name__}: {ex}", "traceback_tail": tb[-2000:]}), flush=True)
+        try:
+            sys.stderr.write(tb)
+            sys.stderr.flush()
+        except OSError:
+            pass
+        return 1
+    finally:
+        for p in state.get("files", []):
+            _unlink(p)
+        try:
+            if state.get("ptr") and state.get("ctx"):
+                state["ctx"].free_device(state["ptr"])
+        except Exception:
+            pass
 
 
 def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W):
@@ -578,41 +700,49 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
                     "device-resident step"}
 
 
-def host_variants(kca, ctx, args, host, nbytes, out_path, k, L):
+def host_variants(kca, ctx, args, state, nbytes, k, L):
     """host_memory: the FASTQ from pageable host memory in one kc_count_fastq
-    call -> output file. reference_chunks: the same reads as the reference's
-    chunks (sequences only, 7.8 MB each at gpuMemoryLimit=1e8) through
-    kc_count_chunk, against one kc_count_chunk of all of them (records left
-    in HBM in both)."""
+    call -> output file (deleted right after). reference_chunks: the same
+    reads as the reference's chunks (sequences only, 7.8 MB each at
+    gpuMemoryLimit=1e8) through kc_count_chunk, against one kc_count_chunk of
+    all of them (records left in HBM in both). N = 1 only; the host copies are
+    freed before the next one is made."""
     import numpy as np
 
     res = {}
     win = args.reads * (L - k + 1)
 
-    def one(step, reps=1):
+    def one(step, reps=1, after=lambda: None):
         step()  # warm
+        after()
         best = None
         for _ in range(reps):
             t = time.perf_counter()
             step()
             dt = time.perf_counter() - t
+            after()  # outside the interval
             best = dt if best is None else min(best, dt)
         return best
 
-    outs = []
+    workdir, _, tried = pick_workdir(args.workdir, int(nbytes * 0.3) + (2 << 30))
+    if workdir is None:
+        res["host_memory"] = {"skipped": "no directory with room for one output file", "free_bytes": tried}
+    else:
+        host = np.empty(nbytes, dtype=np.uint8)
+        ctx.copy_to_host_addr(host.ctypes.data, state["ptr"], nbytes)
+        out = os.path.join(workdir, f"kc_bench_out.{os.getpid()}.host")
+        state.setdefault("files", []).append(out)
 
-    def host_step():
-        outs.append(f"{out_path}.h{len(outs)}")
-        ctx.reset()
-        ctx.count_fastq_host(host.ctypes.data, nbytes)
-        ctx.write_output(outs[-1])
+        def host_step():
+            ctx.reset()
+            ctx.count_fastq_host(host.ctypes.data, nbytes)
+            ctx.write_output(out)
 
-    dt = one(host_step)
-    for p in outs:
-        os.unlink(p)
-    res["host_memory"] = {"value": win / dt, "ms_per_step": dt * 1e3,
-                          "path": "FASTQ in pageable host memory -> pinned ring -> PCIe -> GPU decode + count -> "
-                                  "SortedKMerFile closed"}
+        dt = one(host_step, after=lambda: _unlink(out))
+        del host
+        res["host_memory"] = {"value": win / dt, "ms_per_step": dt * 1e3,
+                              "path": "FASTQ in pageable host memory -> pinned ring -> PCIe -> GPU decode + count -> "
+                                      "SortedKMerFile closed"}
     # the reference's chunk layout: concatenated sequences
     sptr, sbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, 0, 0, layout=1)
     seqs = np.empty(sbytes, dtype=np.uint8)
@@ -648,4 +778,4 @@ def host_variants(kca, ctx, args, host, nbytes, out_path, k, L):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(run())

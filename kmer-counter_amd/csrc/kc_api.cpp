@@ -4,6 +4,7 @@
 //
 // Replaces PrepareGPU / processKMers / FreeGPU (GPUHandler.cu:397-519) and the
 // host aggregation of KMerCounter (KMerCounter.cpp:51-106).
+#include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
@@ -168,6 +169,7 @@ struct kc_ctx {
 
 static kc_status cut_run(kc_ctx* c);
 static kc_status keep_finished_run(kc_ctx* c, uint64_t n);
+static kc_status cut_run_if_full(kc_ctx* c);
 static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
 static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
 static void release_dev_runs(kc_ctx* c, bool free_pool);
@@ -360,10 +362,13 @@ static kc_status flush_keys(kc_ctx* c, uint64_t* keys, uint64_t stride, uint64_t
         snprintf(name, sizeof(name), "/kc.%d.%llu.%zu", (int)getpid(), (unsigned long long)c->id, c->runs.size());
         run.path = c->temp_dir + name;
         FILE* f = fopen(run.path.c_str(), "wb");
-        if (!f) return fail(c, KC_ERR_IO, "cannot create spill run %s", run.path.c_str());
+        if (!f) return fail(c, KC_ERR_IO, "cannot create spill run %s: %s", run.path.c_str(), strerror(errno));
         size_t w = fwrite(run.mem.data(), 1, bytes, f);
-        fclose(f);
-        if (w != bytes) return fail(c, KC_ERR_IO, "short write to spill run %s", run.path.c_str());
+        const int we = errno;
+        const int ce = fclose(f) != 0 ? errno : 0;
+        if (w != bytes || ce)
+            return fail(c, KC_ERR_IO, "short write to spill run %s (%zu of %llu bytes): %s", run.path.c_str(), w,
+                        (unsigned long long)bytes, strerror(w != bytes ? we : ce));
         std::vector<uint8_t>().swap(run.mem);
     }
     c->runs.push_back(std::move(run));
@@ -617,7 +622,8 @@ static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vecto
     uint64_t acc = 0;
     for (uint32_t g = 0; g < NG; g++) {
         const uint64_t x = gt[g];
-        if (x > cap) return KC_OK;  // one group holds more than a batch: read batches
+        if (x > c->key_cap) return KC_OK;  // one group holds more than a batch: read batches
+        // (a group above the balanced cap but within a batch gets a pass of its own)
         // close the pass before g when g would overflow it, or when stopping
         // here is closer to the balanced target than taking g
         if (acc > 0 && (acc + x > cap || (acc + x > target && acc + x - target > target - acc))) {
@@ -1053,6 +1059,12 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         }
         c->batches++;
         c->engines_used |= 2u;
+        // records past half the working set become a sorted run between
+        // batches and between passes that did not go direct, as pend_flush
+        // does between its calls (a call of many batches or passes must not
+        // grow the records past the working set). Not while the next pass's
+        // keys wait in fin_packed (two passes per walk), which the cut writes.
+        if (!(kpass && kp_u_pass == kpi + 1) && (s = cut_run_if_full(c))) return s;
         if (kpass && kpi + 2 < kp.size()) {
             kpi++;
             continue;
@@ -1651,7 +1663,9 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     // where the block's reads go: the pending batch when they fit it (after
     // counting a pending batch of another kind or too full to take them)
     uint64_t off = 0;
-    const bool into_pend = codes && n_rec > 0 && n_rec <= pend_room(c, L, var);
+    // (count = false, kc_check_fastq: the two-pass index checks the block and
+    // nothing is reserved, encoded or flushed: a validation has no side effects)
+    const bool into_pend = count && codes && n_rec > 0 && n_rec <= pend_room(c, L, var);
     if (into_pend && (s = pend_reserve(c, L, var, n_rec, &off))) return s;
     const bool no_fuse = getenv("KC_NO_FQ_ENCODE") != nullptr;  // path selector (tests): same bytes either way
     const bool fused = into_pend && !var && !no_fuse;                               // fq_encode_k
@@ -2172,10 +2186,15 @@ static kc_status file_upload(kc_ctx* c, int slot, const char* p, size_t n) {
 }
 
 // The GPU decode of an uploaded block (waits for its checks, hence for the
-// upload: the reader may refill the block when this returns).
+// upload: the reader may refill the host block when this returns). Kernels
+// queued by the decode may still read the staging buffer (an encode of reads
+// appended to the pending batch is not waited for), so the next upload into
+// this slot waits for stage_free[slot], recorded after them.
 static kc_status file_decode(kc_ctx* c, int slot, size_t n, int64_t L, bool count, uint64_t* got) {
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->file_ev[slot], 0));
-    return fastq_device(c, c->file_stage[slot].p, n, L, got, count);
+    kc_status s = fastq_device(c, c->file_stage[slot].p, n, L, got, count);
+    HIPCHK(c, hipEventRecord(c->stage_free[slot], c->stream));
+    return s;
 }
 
 // Streams the file's blocks to the contexts (each block to whichever context
@@ -2315,7 +2334,7 @@ extern "C" kc_status kc_count_file(kc_ctx* const* ctxs, uint32_t n_ctx, const ch
         // context's checkpoint room (rolled back on a malformed block), else
         // it is validated first.
         struct stat sb;
-        if (stat(path, &sb) != 0) return fail(c0, KC_ERR_IO, "cannot stat %s", path);
+        if (stat(path, &sb) != 0) return fail(c0, KC_ERR_IO, "cannot stat %s: %s", path, strerror(errno));
         const uint64_t est = (uint64_t)sb.st_size / (uint64_t)(2 * L + 6) + 1;  // records are >= 2L + 6 bytes
         bool once = true;
         for (uint32_t g = 0; g < n_ctx; g++) {
@@ -2385,6 +2404,7 @@ kc_status kc_rollback(kc_ctx* c) {
         return fail(c, KC_ERR_STATE, "reads were counted since the checkpoint: it cannot be rolled back");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     c->pend_reads = c->ckpt_reads;
+    c->acc_n = 0;  // chunks accumulated since (kc_checkpoint flushed the accumulator) are forgotten too
     c->st.reads = c->ckpt_st_reads;
     c->st.windows = c->ckpt_st_windows;
     HIPCHK(c, hipMemcpyAsync(c->stats, c->ckpt_stats, sizeof(c->ckpt_stats), hipMemcpyHostToDevice, c->stream));
@@ -2804,8 +2824,15 @@ static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0,
     const uint64_t bytes = c->n_records * c->rs;
     const double t0 = kc::trace_on() ? kc::now_s() : 0;
     int fd = open(path, O_CREAT | O_WRONLY, 0644);
-    if (fd < 0) return fail(c, KC_ERR_IO, "cannot open output file %s", path);
-    if (bytes) (void)fallocate(fd, 0, (off_t)at, (off_t)bytes);  // a hint: filesystems without it just write
+    if (fd < 0) return fail(c, KC_ERR_IO, "cannot open output file %s: %s", path, strerror(errno));
+    // the range is reserved up front: a full filesystem fails here, by name,
+    // before any byte moves (filesystems without fallocate just write)
+    if (bytes && fallocate(fd, 0, (off_t)at, (off_t)bytes) != 0 && errno != EOPNOTSUPP && errno != ENOSYS) {
+        const int e = errno;
+        close(fd);
+        return fail(c, KC_ERR_IO, "cannot reserve %llu bytes at %llu in %s: %s", (unsigned long long)bytes,
+                    (unsigned long long)at, path, strerror(e));
+    }
     if (kc::trace_on()) kc::trace("output open + fallocate %.3f ms", (kc::now_s() - t0) * 1e3);
     kc_status s = KC_OK;
     if (bytes) {
@@ -2814,21 +2841,31 @@ static kc_status table_run_to_file(kc_ctx* c, const char* path, uint64_t at = 0,
             close(fd);
             return s;
         }
+        int werr = 0;
+        uint64_t wat = 0;
         hipError_t e = c->ring->download(c->fin_packed.p, bytes, c->stream, [&](const char* p, size_t n, size_t off) {
             size_t done = 0;
             while (done < n) {
                 const size_t piece = std::min((size_t)8 << 20, n - done);
                 ssize_t w = pwrite(fd, p + done, piece, (off_t)(at + off + done));
-                if (w <= 0) return false;
+                if (w < 0 && errno == EINTR) continue;
+                if (w <= 0) {
+                    werr = w < 0 ? errno : ENOSPC;  // a 0-byte write: no room
+                    wat = at + off + done;
+                    return false;
+                }
                 done += (size_t)w;
             }
             return true;
         });
-        if (e == hipErrorUnknown) s = fail(c, KC_ERR_IO, "short write to %s", path);
+        if (e == hipErrorUnknown)
+            s = fail(c, KC_ERR_IO, "write to %s failed at byte %llu of %llu: %s", path, (unsigned long long)wat,
+                     (unsigned long long)(at + bytes), strerror(werr));
         else if (e != hipSuccess) s = fail(c, KC_ERR_HIP, "output copy: %s", hipGetErrorString(e));
     }
-    if (!s && whole && ftruncate(fd, (off_t)(at + bytes)) != 0) s = fail(c, KC_ERR_IO, "cannot size %s", path);
-    if (close(fd) != 0 && !s) s = fail(c, KC_ERR_IO, "cannot close %s", path);
+    if (!s && whole && ftruncate(fd, (off_t)(at + bytes)) != 0)
+        s = fail(c, KC_ERR_IO, "cannot size %s: %s", path, strerror(errno));
+    if (close(fd) != 0 && !s) s = fail(c, KC_ERR_IO, "cannot close %s: %s", path, strerror(errno));
     if (kc::trace_on()) kc::trace("output %llu bytes in %.3f ms", (unsigned long long)bytes, (kc::now_s() - t0) * 1e3);
     return s;
 }
@@ -2885,7 +2922,7 @@ kc_status kc_write_runs(kc_ctx* c, const char* prefix, uint32_t* n_runs) {
             if (!in || !out) {
                 if (in) fclose(in);
                 if (out) fclose(out);
-                return fail(c, KC_ERR_IO, "cannot copy run %s", from.c_str());
+                return fail(c, KC_ERR_IO, "cannot copy run %s to %s: %s", from.c_str(), name.c_str(), strerror(errno));
             }
             std::vector<char> buf(1 << 20);
             size_t got;
@@ -2894,10 +2931,11 @@ kc_status kc_write_runs(kc_ctx* c, const char* prefix, uint32_t* n_runs) {
             fclose(out);
         } else {
             FILE* out = fopen(name.c_str(), "wb");
-            if (!out) return fail(c, KC_ERR_IO, "cannot write run %s", name.c_str());
+            if (!out) return fail(c, KC_ERR_IO, "cannot write run %s: %s", name.c_str(), strerror(errno));
             size_t w = bytes ? fwrite(p, 1, bytes, out) : 0;
-            fclose(out);
-            if (w != bytes) return fail(c, KC_ERR_IO, "short write %s", name.c_str());
+            const int we = errno;
+            const int ce = fclose(out) != 0 ? errno : 0;
+            if (w != bytes || ce) return fail(c, KC_ERR_IO, "short write %s: %s", name.c_str(), strerror(w != bytes ? we : ce));
         }
         count++;
         return KC_OK;

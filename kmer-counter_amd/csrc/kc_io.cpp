@@ -4,6 +4,7 @@
 // SortedKMerFile.cpp:18-124) with a heap merge over buffered streams.
 #include "kc_io.h"
 
+#include <errno.h>
 #include <stdio.h>
 #include <string.h>
 #include <unistd.h>
@@ -99,14 +100,20 @@ void RunReader::pop() {
 
 RunWriter::RunWriter(const std::string& path, int rs) : rs_(rs) {
     f_ = fopen(path.c_str(), "wb");
+    if (!f_) errno_ = errno;
     buf_.resize(kIoBuf - kIoBuf % rs);
+}
+
+void RunWriter::failed() {
+    if (!err_) errno_ = errno ? errno : EIO;
+    err_ = true;
 }
 
 RunWriter::~RunWriter() { close(); }
 
 void RunWriter::put(const uint8_t* rec) {
     if (len_ + rs_ > buf_.size()) {
-        if (f_ && fwrite(buf_.data(), 1, len_, f_) != len_) err_ = true;
+        if (f_ && fwrite(buf_.data(), 1, len_, f_) != len_) failed();
         len_ = 0;
     }
     memcpy(buf_.data() + len_, rec, rs_);
@@ -115,24 +122,30 @@ void RunWriter::put(const uint8_t* rec) {
 
 bool RunWriter::close() {
     if (!f_) return false;
-    if (len_ && fwrite(buf_.data(), 1, len_, f_) != len_) err_ = true;
+    if (len_ && fwrite(buf_.data(), 1, len_, f_) != len_) failed();
     len_ = 0;
-    if (fclose(f_) != 0) err_ = true;
+    if (fclose(f_) != 0) failed();
     f_ = nullptr;
     return !err_;
 }
 
-bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int W) {
+bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int W, int* err_no) {
     const int rs = 8 * W + 4;
     std::vector<RunReader*> rd;
     bool ok = true;
     for (const auto& r : runs) {
         RunReader* x = new RunReader(r, W);
-        if (!x->ok()) ok = false;
+        if (!x->ok()) {
+            if (ok && err_no) *err_no = errno ? errno : EIO;
+            ok = false;
+        }
         rd.push_back(x);
     }
     RunWriter w(out, rs);
-    if (!w.ok()) ok = false;
+    if (!w.ok()) {
+        if (ok && err_no) *err_no = w.error_number();
+        ok = false;
+    }
     if (ok) {
         auto greater = [&](int a, int b) {
             int c = key_compare(rd[a]->head(), rd[b]->head(), W);
@@ -163,6 +176,7 @@ bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int 
         }
         if (have) w.put(acc.data());
         ok = w.close();
+        if (!ok && err_no) *err_no = w.error_number();
     }
     for (auto* x : rd) delete x;
     return ok;
@@ -184,12 +198,17 @@ bool merge_tree(const std::vector<RunSource>& runs_in, const std::string& out, i
         std::vector<std::string> outs(groups);
         std::atomic<size_t> cursor(0);
         std::atomic<bool> good(true);
+        std::atomic<int> bad_errno(0);
         auto work = [&]() {
             for (;;) {
                 size_t g = cursor.fetch_add(1);
                 if (g >= groups) break;
                 std::vector<RunSource> grp(runs.begin() + g * fan_in, runs.begin() + (g + 1) * fan_in);
-                if (!merge_runs(grp, outs[g], W)) good = false;
+                int e = 0;
+                if (!merge_runs(grp, outs[g], W, &e)) {
+                    good = false;
+                    bad_errno = e;
+                }
             }
         };
         for (size_t g = 0; g < groups; g++) outs[g] = tmp_prefix + ".m" + std::to_string(round) + "_" + std::to_string(g);
@@ -198,7 +217,7 @@ bool merge_tree(const std::vector<RunSource>& runs_in, const std::string& out, i
         for (auto& t : pool) t.join();
         if (!good) {
             ok = false;
-            if (err) *err = "merge of sorted runs failed (I/O)";
+            if (err) *err = std::string("merge of sorted runs into ") + tmp_prefix + "* failed: " + strerror(bad_errno.load());
             break;
         }
         for (size_t g = 0; g < groups; g++) {
@@ -212,8 +231,9 @@ bool merge_tree(const std::vector<RunSource>& runs_in, const std::string& out, i
         round++;
     }
     if (ok) {
-        ok = merge_runs(runs, out, W);
-        if (!ok && err) *err = "cannot write output file " + out;
+        int e = 0;
+        ok = merge_runs(runs, out, W, &e);
+        if (!ok && err) *err = "cannot write output file " + out + ": " + strerror(e);
     }
     for (const auto& t : temps) unlink(t.c_str());
     return ok;

@@ -55,11 +55,14 @@ class RunWriter {
     bool ok() const { return f_ != nullptr && !err_; }
     void put(const uint8_t* rec);
     bool close();
+    int error_number() const { return errno_; }  // errno of the first failure (0: none)
 
   private:
+    void failed();
     FILE* f_ = nullptr;
     int rs_;
     bool err_ = false;
+    int errno_ = 0;
     std::vector<uint8_t> buf_;
     size_t len_ = 0;
 };
@@ -67,7 +70,8 @@ class RunWriter {
 // k-way merge of sorted runs into `out`; equal keys are summed as uint32
 // (KMerFileMerger::Merge, KMerFileMerger.cpp:49-96). Empty runs are skipped
 // (the reference dereferences NULL on them, KMerFileMerger.cpp:58).
-bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int W);
+// On failure *err_no (if given) holds the errno of the failing call.
+bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int W, int* err_no = nullptr);
 
 // Merge tree with the reference handler's knobs (KMerFileMergeHandler.cpp):
 // while more than fan_in runs remain, groups of fan_in runs are merged into

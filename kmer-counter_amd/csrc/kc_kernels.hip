@@ -4691,37 +4691,59 @@ hipError_t launch_fq_validate(const uint64_t* seq_off, const uint64_t* seq_end, 
 // ---------------------------------------------------------------------------
 // Coverage sketch (engine choice): one k-mer per read and 16-base group, the
 // one starting at the group (aligned to the read, not to the genome), kept
-// when its hash falls in 1/256 of the hash space; its 56-bit fingerprint is
-// appended to `out`. Reads from a genome at coverage c repeat such a k-mer in
-// ~c/16 reads (a read starting at the same position mod 16), so the share of
-// distinct fingerprints estimates the coverage: iid reads ~1, cfg2's 30x
-// ~0.45. The k-mer's bases are taken from the 2-bit codes (first base
+// when a hash of its first 16 bases (its first code word) falls in 2^-rb of
+// the hash space; its 56-bit fingerprint (a hash of the whole k-mer) is
+// appended to `out`. The sample is a function of the k-mer, so every copy of
+// a sampled k-mer is kept. Reads from a genome at coverage c repeat such a
+// k-mer in ~c/16 reads (a read starting at the same position mod 16), so the
+// share of distinct fingerprints estimates the coverage: iid reads ~1, cfg2's
+// 30x ~0.46. The k-mer's bases are taken from the 2-bit codes (first base
 // highest in each u32 of 16 bases); k-mers with a not-ACGT base are skipped.
+// Per aligned position a lane loads one code word and hashes it with two u32
+// multiplies; only the ~2^-rb sampled lanes load the rest of the k-mer and its
+// not-ACGT masks and compute the fingerprint (the earlier form hashed every
+// aligned k-mer whole with 64-bit mixes: 2.9 ms at cfg2).
 // ---------------------------------------------------------------------------
+
+__device__ __forceinline__ u32 sketch_mix32(u32 h) {  // murmur3 finaliser
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
 
 __global__ __launch_bounds__(kBlock) void sketch_k(const u32* __restrict__ codes, const unsigned short* __restrict__ inval,
                                                   u64 n_reads, int G, int k, int rate_bits, u64* __restrict__ out,
                                                   u64 cap, u64* __restrict__ counter) {
     const int ng = (k + 15) >> 4;  // groups a k-mer spans from a group start
     const int per = G - ng + 1;    // aligned k-mers per read
-    const u64 rmask = (1ull << rate_bits) - 1;
+    const u32 rmask = (1u << rate_bits) - 1;
+    const int nb0 = min(16, k);
+    const u32 keep0 = nb0 == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb0));
+    const u32 seed = 0x9e3779b9u ^ (u32)k;
     // one read per thread (no division per item); a wave takes one counter
     // add per aligned position that sampled anything
     for (u64 r0 = (u64)blockIdx.x * kBlock; r0 < n_reads; r0 += (u64)gridDim.x * kBlock) {
         const u64 r = r0 + threadIdx.x;
         const bool live = r < n_reads;
+        const u64 row = (live ? r : 0) * (u64)G;
         for (int g = 0; g < per; g++) {
-            const u64 base = (live ? r : 0) * (u64)G + (u64)g;
-            u64 h = 0x243f6a8885a308d3ull ^ (u64)k;
-            bool ok = live;
-            for (int j = 0; j < ng; j++) {
-                const int nb = min(16, k - 16 * j);  // bases of this group inside the k-mer
-                const u32 keep = nb == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb));
-                const unsigned short bad = (unsigned short)(inval[base + j] & (nb == 16 ? 0xffffu : ~(0xffffu >> nb)));
-                ok = ok && bad == 0;
-                h = mix64(h ^ (u64)(codes[base + j] & keep) ^ ((u64)j << 40));
+            const u64 base = row + (u64)g;
+            bool take = live && (sketch_mix32((codes[base] & keep0) ^ seed) & rmask) == 0;
+            u64 h = 0;
+            if (take) {  // rare: the whole k-mer
+                h = 0x243f6a8885a308d3ull ^ (u64)k;
+                for (int j = 0; j < ng; j++) {
+                    const int nb = min(16, k - 16 * j);  // bases of this group inside the k-mer
+                    const u32 keep = nb == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb));
+                    const unsigned short bad =
+                        (unsigned short)(inval[base + j] & (nb == 16 ? 0xffffu : ~(0xffffu >> nb)));
+                    take = take && bad == 0;
+                    h = mix64(h ^ (u64)(codes[base + j] & keep) ^ ((u64)j << 40));
+                }
             }
-            const bool take = ok && (h & rmask) == 0;
             const u64 m = __ballot(take);
             if (!m) continue;
             u64 at = 0;

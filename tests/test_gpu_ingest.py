@@ -275,3 +275,59 @@ def test_gather_contexts_merges_on_first_device(kca, orc, k, mem):
         for c in ctxs:
             c.close()
     assert got == orc.count_fastq(b"".join(shards), k)
+
+
+@pytest.mark.parametrize("mode", ["fastq", "auto"])
+def test_count_file_blocks_larger_than_pending_room(kca, orc, tmp_path, monkeypatch, mode):
+    """Reader blocks holding more reads than the pending batch takes (a 4 MiB
+    working set, 1 MiB blocks of ~3300 reads): each block goes through the
+    two-pass index and is encoded batch by batch straight from its staging
+    buffer, asynchronously; the next upload into that buffer must wait for
+    those encodes (stage_free). Same bytes as the oracle."""
+    monkeypatch.setenv("KC_FILE_BLOCK", str(1 << 20))
+    fq = kca.synth_fastq(40000, 150, seed=21, genome_length=2_000_000, n_rate=0.001)
+    p = tmp_path / "r.fq"
+    p.write_bytes(fq)
+    with kca.Context(kmer_length=31, line_length=150, gpu_memory_limit=4 << 20) as ctx:
+        assert ctx.count_file(str(p), mode=mode) == 40000
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["batches"] >= 4
+    assert got == orc.count_fastq(fq, 31)
+
+
+def test_rollback_forgets_accumulated_chunks(kca, orc):
+    """kc_count_chunk bytes accumulated after a checkpoint are forgotten by
+    kc_rollback together with the pending reads (include/kc.h)."""
+    L, k = 150, 31
+    a = kca.synth_fastq(3000, L, seed=22, n_rate=0.001)
+    b = kca.synth_fastq(2000, L, seed=23, n_rate=0.001)
+    ca = list(orc.chunks_of(a, orc.chunk_size(L, k, 2_000_000)))
+    cb = list(orc.chunks_of(b, orc.chunk_size(L, k, 2_000_000)))
+    with kca.Context(kmer_length=k, line_length=L) as ctx:
+        for chunk, ll in ca:
+            ctx.count_chunk(chunk, ll)
+        ctx.checkpoint()
+        for chunk, ll in cb:
+            ctx.count_chunk(chunk, ll)
+        ctx.rollback()
+        assert ctx.stats()["reads"] == 3000
+        got = ctx.records()
+    assert got == orc.count_chunks(ca, k)
+
+
+def test_check_fastq_has_no_side_effects(kca, orc):
+    """kc_check_fastq validates a block without reserving, encoding or
+    counting anything: a held checkpoint still rolls back, and the pending
+    batch is the one counted."""
+    a = kca.synth_fastq(3000, 150, seed=24, n_rate=0.002)
+    b = kca.synth_fastq(50000, 150, seed=25, n_rate=0.002)
+    with kca.Context(kmer_length=31, line_length=150, gpu_memory_limit=8 << 20) as ctx:
+        ctx.count_fastq(a)
+        ctx.checkpoint()
+        assert ctx.check_fastq(b) == 50000
+        ctx.rollback()
+        st = ctx.stats()
+        assert st["reads"] == 3000 and st["batches"] == 0
+        got = ctx.records()
+    assert got == orc.count_fastq(a, 31)

@@ -752,3 +752,56 @@ def test_merge_runs_device(kca, orc, k, nruns):
         got = ctx.records()
     want = orc.count_fastq(b"".join(shards), k)
     assert got == want and n * rs == len(want)
+
+
+@pytest.mark.parametrize("k", [31, 55])
+def test_key_range_hand_off_cuts_runs(kca, orc, monkeypatch, capfd, k):
+    """A hand-off in the first key-range pass with several passes left (a
+    cluster of reads sharing their first 12 bases, all starting with A): the
+    later passes count into records, which are cut into sorted runs between
+    passes whenever they outgrow half the working set, instead of growing
+    past it. Same bytes as the oracle."""
+    import numpy as np
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L = 150
+    n = 260000
+    rng = np.random.default_rng(k + 19)
+    reads = _hc_reads(rng, n, L)
+    reads[:12000, :12] = np.array([0, 0, 1, 2, 3, 0, 1, 2, 3, 3, 2, 1], dtype=np.uint8)
+    fq = _fastq_from_codes(reads[rng.permutation(n)])
+    mem = 128 << 20
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=mem) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    err = capfd.readouterr().err
+    direct = [x for x in err.splitlines() if "kc: P5s direct pass" in x]
+    assert st["key_passes"] >= 3, err[-3000:]
+    assert direct and "kept=0" in direct[0], err[-3000:]
+    assert st["spill_runs"] >= 2, (st, err[-3000:])
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_key_range_passes_skewed_prefixes(kca, orc, monkeypatch, capfd):
+    """High cardinality with a skewed base composition (A at 2/3): the keys'
+    two-base groups (word0 >> 60) are far from balanced, the AA group alone
+    holding ~44% of the keys. The planner gives an oversize group a pass of
+    its own instead of falling back to read batches. Same bytes as the
+    oracle."""
+    import numpy as np
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L, k = 150, 31
+    n = 200000
+    rng = np.random.default_rng(77)
+    reads = rng.choice(4, size=(n, L), p=[2 / 3, 1 / 9, 1 / 9, 1 / 9]).astype(np.uint8)
+    reads[5] = 0
+    fq = _fastq_from_codes(reads)
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=160 << 20) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    err = capfd.readouterr().err
+    assert st["key_passes"] >= 2, (st, err[-3000:])
+    assert got == orc.count_fastq(fq, k)

@@ -272,3 +272,30 @@ def test_release_build_ignores_ablation_variables(kca, orc, monkeypatch, engine)
         ctx.count_fastq(fq)
         got = ctx.records()
     assert got == orc.count_fastq(fq, 31)
+
+
+@pytest.mark.parametrize("k", [21, 31, 55])
+@pytest.mark.parametrize("genome", [0, 900_000], ids=["iid", "genome30x"])
+def test_coverage_sketch_estimate(kca, orc, monkeypatch, capfd, k, genome):
+    """The coverage sketch (sketch_k: k-mers sampled by a hash of their first
+    code word, fingerprinted whole) on cfg2's shape scaled down: reads from a
+    genome at 30x coverage give a distinct share near (1 - e^-1.8) / 1.8 =
+    0.46 and keep the super-k-mer engine; iid reads give ~1 and take the
+    key-prefix engine. Output identical to the oracle either way."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    n, L = 180_000, 150  # >= 2^24 windows at every k here: the sketch runs
+    fq = kca.synth_fastq(n, L, seed=80 + k, genome_length=genome)
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=4 << 30) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    err = capfd.readouterr().err
+    line = [x for x in err.splitlines() if x.startswith("kc: sketch ")]
+    assert line, err[-2000:]
+    d, m = int(line[0].split()[2]), int(line[0].split()[5])
+    assert m >= 4096
+    if genome:
+        assert 0.3 < d / m < 0.6 and st["engines_used"] == 1, (d, m, st["engines_used"])
+    else:
+        assert d / m > 0.95 and st["engines_used"] == 2, (d, m, st["engines_used"])
+    assert got == orc.count_fastq(fq, k)
