@@ -3367,16 +3367,29 @@ kc_status kc_exchange_contexts(kc_ctx* const* ctxs, uint32_t n) {
             return fail(ctxs[o], KC_ERR_HIP, hipGetErrorString(e));
         }
     }
-    for (uint32_t o = 0; o < n; o++) {
-        // owner o received one sorted slice from every context, in order
+    // owner o received one sorted slice from every context, in order; the
+    // owners merge concurrently, one host thread each (each context has its
+    // own stream and buffers; hipSetDevice is per thread)
+    std::vector<kc_status> ms(n, KC_OK);
+    auto merge_owner = [&](uint32_t o) {
         std::vector<uint64_t> rc(n);
         for (uint32_t r = 0; r < n; r++) rc[r] = cnt[r][o];
-        if ((s = kc_merge_runs_device(ctxs[o], recv[o], rc.data(), n))) {
-            release();
-            return s;
+        if (hipSetDevice(ctxs[o]->cfg.device) != hipSuccess) {
+            ms[o] = fail(ctxs[o], KC_ERR_HIP, "hipSetDevice(%d)", ctxs[o]->cfg.device);
+            return;
         }
+        ms[o] = kc_merge_runs_device(ctxs[o], recv[o], rc.data(), n);
+    };
+    if (n == 1) {
+        merge_owner(0);
+    } else {
+        std::vector<std::thread> th;
+        for (uint32_t o = 0; o < n; o++) th.emplace_back(merge_owner, o);
+        for (auto& t : th) t.join();
     }
     release();
+    for (uint32_t o = 0; o < n; o++)
+        if (ms[o]) return ms[o];
     return KC_OK;
 }
 

@@ -788,7 +788,9 @@ def test_key_range_passes_skewed_prefixes(kca, orc, monkeypatch, capfd):
     two-base groups (word0 >> 60) are far from balanced, the AA group alone
     holding ~44% of the keys. The planner gives an oversize group a pass of
     its own instead of falling back to read batches. Same bytes as the
-    oracle."""
+    oracle. Sizes: ~24M keys, a 210 MB working set (11.4M keys per batch):
+    3 passes of ~8M, the AA group ~10.7M, above the balanced cap (10M) and
+    within a batch."""
     import numpy as np
     monkeypatch.setenv("KC_P3B_MIN", "1")
     monkeypatch.setenv("KC_DEBUG", "1")
@@ -798,10 +800,68 @@ def test_key_range_passes_skewed_prefixes(kca, orc, monkeypatch, capfd):
     reads = rng.choice(4, size=(n, L), p=[2 / 3, 1 / 9, 1 / 9, 1 / 9]).astype(np.uint8)
     reads[5] = 0
     fq = _fastq_from_codes(reads)
-    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=160 << 20) as ctx:
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=210_000_000) as ctx:
         ctx.count_fastq(fq)
         got = ctx.records()
         st = ctx.stats()
     err = capfd.readouterr().err
     assert st["key_passes"] >= 2, (st, err[-3000:])
     assert got == orc.count_fastq(fq, k)
+
+
+def test_config1_full_size(kca, orc, tmp_path):
+    """BASELINE config 1 at its stated size: k=21, 10k x 100 bp iid reads with
+    N rate 0.002 (seed 1), through the block path (kc_count_fastq), the file
+    path (kc_count_file) and the reference's own chunks (kc_count_chunk at
+    gpuMemoryLimit=1e8): all three equal the oracle's spec form and the
+    reference-structured CPU pipeline (refcpu)."""
+    n, L, k = 10_000, 100, 21
+    fq = kca.synth_fastq(n, L, seed=1, n_rate=0.002)
+    p = tmp_path / "cfg1.fq"
+    p.write_bytes(fq)
+    outs = []
+    with kca.Context(kmer_length=k, line_length=L) as ctx:
+        assert ctx.count_fastq(fq) == n
+        outs.append(ctx.records())
+        ctx.reset()
+        assert ctx.count_file(str(p)) == n
+        outs.append(ctx.records())
+        ctx.reset()
+        for chunk, ll in orc.chunks_of(fq, orc.chunk_size(L, k, 100_000_000)):
+            ctx.count_chunk(chunk, ll)
+        outs.append(ctx.records())
+        st = ctx.stats()
+    assert st["reads"] == n and st["windows"] == n * (L - k + 1)
+    want, windows = orc.refcpu(fq, k, threads=4)
+    assert windows == n * (L - k + 1)
+    assert want == orc.count_fastq(fq, k)
+    assert outs[0] == outs[1] == outs[2] == want
+
+
+@pytest.mark.slow
+def test_config5_prefix_bit_exact_key_passes(kca, orc, monkeypatch, capfd):
+    """BASELINE config 5's read stream (k=55, iid 150 bp reads, seed 5), its
+    first 2M reads (1.92e8 k-mers, nearly all distinct), counted from HBM by
+    the default engine with a 2.4 GB working set: the keys are cut into 3
+    key-range passes (one P2 walk for the first two, the second pass's keys
+    staged in the run buffer), each P5s direct-written after the previous
+    ones; the run is their concatenation. Its sha256 equals that of the
+    reference-structured CPU pipeline (refcpu) on every usable core."""
+    import hashlib
+
+    monkeypatch.setenv("KC_DEBUG", "1")
+    n, L, k = 2_000_000, 150, 55
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=2_400_000_000) as ctx:
+        ptr, nb = ctx.synth_device(n, L, 5, 0, 0.0, 0)
+        fq = ctx.copy_to_host(ptr, nb)
+        assert ctx.count_fastq_device(ptr, nb) == n
+        ctx.free_device(ptr)
+        got = hashlib.sha256(ctx.records()).hexdigest()
+        st = ctx.stats()
+    err = capfd.readouterr().err
+    direct = [x for x in err.splitlines() if "kc: P5s direct pass" in x]
+    assert st["key_passes"] >= 3 and st["insert_launches"] < st["key_passes"], (st, err[-2000:])
+    assert len(direct) == st["key_passes"] and all("kept=1" in x for x in direct), err[-2000:]
+    want, windows = orc.refcpu(fq, k, threads=_usable_cpus())
+    assert windows == n * (L - k + 1) == st["windows"]
+    assert got == hashlib.sha256(want).hexdigest()
