@@ -448,7 +448,10 @@ def e2e_leg(kca, ctx, D, args, state, ptr, nbytes, exchange, windows_of_step):
     (barrier + synchronize on both sides) and summed, so at most one output
     file exists at a time whatever --steps is."""
     out_est = int(nbytes * 0.3) + (64 << 20)  # records <= ~22% of the FASTQ bytes at cfg2/cfg5
-    need = nbytes + 2 * out_est + (1 << 30)
+    # every rank of this node writes its own input file and output part into
+    # the same directory: room for all of them (at N = 8, cfg2: ~160 GB)
+    local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", str(D.world)))
+    need = local_ranks * (nbytes + 2 * out_est) + (1 << 30)
     workdir, free, tried = pick_workdir(args.workdir, need)
     if workdir is None:
         return {"skipped": f"no directory with {need / 1e9:.1f} GB free for the input file and one output file",

@@ -638,6 +638,14 @@ static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vecto
     return KC_OK;
 }
 
+// Smallest batch (keys) that takes the P3b pre-split (high cardinality);
+// KC_P3B_MIN: path selector for tests, same counts either way
+static uint64_t p3b_min_of() {
+    uint64_t m = 1ull << 22;
+    if (const char* e = getenv("KC_P3B_MIN")) m = strtoull(e, nullptr, 10);
+    return m;
+}
+
 // Engine "partition": per batch of reads
 //   P1 hist   : digit (word0 >> 48) & 255 per segment of reads
 //   P2 scatter: keys to their digit's region (LDS counting sort per tile)
@@ -824,6 +832,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
             c->part_ms[3] += t;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+            uint8_t* p3b_digs = nullptr;  // P3b digit bytes written by P3 (else P3b reads word 0)
             // P3's scatter is the regional radix scatter (digit word0 >> 56 over
             // the 256 P2 regions, same tiles; next tile's run starts prefetched,
             // XCD-aware tile walk); KC_P3_SCATTER: the older p3_scatter_k
@@ -832,8 +841,12 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, launch_p3_scatter(W, c->keys_a, c->keys_b, c->key_cap, p3t, p3t + 257, ntiles, p3h,
                                             2 * c->n_cu, c->stream));
             } else {
+                // a P3b pass follows (high cardinality): P3 writes each key's P3b
+                // digit byte (bits 40..47) into the free P2 digit array, so P3b's
+                // histogram reads 1 B per key, not word 0
+                p3b_digs = c->hc_hint && n >= p3b_min_of() && !getenv("KC_NO_P3B") ? c->digs : nullptr;
                 HIPCHK(c, launch_rp_scatter(W, false, p2_keys, p2_stride, c->keys_b, c->key_cap, nullptr, nullptr, p3t,
-                                            p3t + 257, 256, ntiles, p3h, 56, nullptr, 0, 2 * c->n_cu, c->stream));
+                                            p3t + 257, 256, ntiles, p3h, 56, p3b_digs, 40, 2 * c->n_cu, c->stream));
             }
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
@@ -859,10 +872,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             uint64_t* p5_keys = c->keys_b;
             uint64_t* p5_spill = c->keys_a;
             const uint64_t* sub_starts = nullptr;
-            // (KC_P3B_MIN: path selector for tests, same counts either way)
-            uint64_t p3b_min = 1ull << 22;
-            if (const char* e = getenv("KC_P3B_MIN")) p3b_min = strtoull(e, nullptr, 10);
-            if (c->hc_hint && n >= p3b_min && !getenv("KC_NO_P3B")) {
+            if (c->hc_hint && n >= p3b_min_of() && !getenv("KC_NO_P3B")) {
                 std::vector<uint64_t> rs((size_t)nb + 1);
                 HIPCHK(c, hipMemcpyAsync(rs.data(), c->part_starts.p, rs.size() * 8, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -883,7 +893,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, hipMemcpyAsync(rtd, rt.data(), rt.size() * 8, hipMemcpyHostToDevice, c->stream));
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                 HIPCHK(c, launch_rp_hist_regional(c->keys_b, 40, rtd, rtd + nb + 1, (int)nb, nt, (uint32_t)tile, pos,
-                                                  cnt_t, 2 * c->n_cu, c->stream));
+                                                  cnt_t, 2 * c->n_cu, c->stream, p3b_digs));
                 HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, c->key_cap, c->keys_a, c->key_cap, nullptr, nullptr,
                                             rtd, rtd + nb + 1, (int)nb, nt, pos, 40, nullptr, 0, 2 * c->n_cu,
                                             c->stream));

@@ -306,7 +306,7 @@ hipError_t launch_rp_hist(const uint8_t* digs, const uint64_t* w0, int shift, co
 // 256 * ntiles u32 scratch, pos: 256 * ntiles run starts
 hipError_t launch_rp_hist_regional(const uint64_t* w0, int shift, const uint64_t* rstart, const uint64_t* tpre,
                                    int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos, uint32_t* cnt_t, int grid,
-                                   hipStream_t s);
+                                   hipStream_t s, const uint8_t* digs = nullptr);
 hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t istride, uint64_t* kout,
                              uint64_t ostride, const uint32_t* pin, uint32_t* pout, const uint64_t* rstart,
                              const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,

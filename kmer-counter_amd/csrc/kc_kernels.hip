@@ -2394,9 +2394,13 @@ hipError_t launch_sub_starts(const uint64_t* rstart, const uint64_t* tpre, const
 // adjacent. A run holding one sub-bucket of more than SP keys, or a bin of
 // more than kMaxSortBin keys (clustered keys), is flagged for the LDS hash
 // table path (count_buckets over the flagged runs only).
-constexpr int kSrBlock = 1024;
+// 512-thread workgroups, two per CU (LDS ~75 KB and <= 128 VGPRs each): one
+// workgroup's loads and stores overlap the other's LDS sort (one 1024-thread
+// workgroup per CU left every run's load latency and store drain exposed)
+constexpr int kSrBlock = 512;
 constexpr int kSrWaves = kSrBlock / 64;
 constexpr u32 kSrBins = 2048;
+constexpr u32 kSrBpt = kSrBins / kSrBlock;  // bins per thread in the bin scan
 constexpr u32 kMaxSortBin = 48;
 
 template <int W>
@@ -2445,7 +2449,7 @@ __device__ __forceinline__ void put_packed(u32* __restrict__ packed, u64 pos, co
 }
 
 template <int W>
-__global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
+__global__ __launch_bounds__(kSrBlock) __attribute__((amdgpu_waves_per_eu(4))) void sort_runs_k(SortRunArgs a) {
     constexpr int SP = SortRunCfg<W>::SP;
     constexpr int R = SortRunCfg<W>::R;
     constexpr u64 M48 = 0xffffffffffffull;
@@ -2539,9 +2543,15 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
             }
             __syncthreads();
             SR_MARK(2);
-            // bin starts: 2 bins per thread, block-wide exclusive scan
-            const u32 c0 = bins[2 * tid], c1 = bins[2 * tid + 1];
-            const u32 sum = c0 + c1;
+            // bin starts: kSrBpt bins per thread, block-wide exclusive scan
+            u32 cb[kSrBpt];
+            u32 sum = 0, cmax = 0;
+#pragma unroll
+            for (u32 x = 0; x < kSrBpt; x++) {
+                cb[x] = bins[kSrBpt * tid + x];
+                sum += cb[x];
+                cmax = max(cmax, cb[x]);
+            }
             u32 inc = sum;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -2549,7 +2559,7 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
                 if (lane >= o) inc += y;
             }
             if (lane == 63) misc[1 + wave] = inc;
-            if (max(c0, c1) > kMaxSortBin) misc[0] = 1u;
+            if (cmax > kMaxSortBin) misc[0] = 1u;
             __syncthreads();
             if (uni32(misc[0])) {  // clustered keys: hash path
                 if (tid == 0) {
@@ -2562,9 +2572,12 @@ __global__ __launch_bounds__(kSrBlock) void sort_runs_k(SortRunArgs a) {
             }
             u32 wpre = 0;
             for (int w = 0; w < wave; w++) wpre += misc[1 + w];
-            const u32 bs = wpre + inc - sum;
-            bins[2 * tid] = bs;
-            bins[2 * tid + 1] = bs + c0;
+            u32 bs = wpre + inc - sum;
+#pragma unroll
+            for (u32 x = 0; x < kSrBpt; x++) {
+                bins[kSrBpt * tid + x] = bs;
+                bs += cb[x];
+            }
             __syncthreads();
             SR_MARK(3);
             u32 qs[R];  // each key's LDS slot (ties between equal keys)
@@ -4714,56 +4727,111 @@ __device__ __forceinline__ u32 sketch_mix32(u32 h) {  // murmur3 finaliser
     return h;
 }
 
+// One thread per read, every read's code row loaded at once (G u32 words,
+// 8-byte aligned rows when G is even: G/2 dwordx2 loads) so a thread waits for
+// one load latency per read, not one per aligned position (GC = 0: other
+// row lengths, the words one by one, 64 positions at a time). The samples are
+// gathered per workgroup in LDS and appended with one global atomic per
+// workgroup: the earlier form took one atomic on the single output counter
+// per wave that sampled anything (~2e5 same-address atomics at cfg2, which
+// serialise and set the kernel's time at ~2.4 ms).
+constexpr u32 kSketchBuf = 1024;  // samples a workgroup holds in LDS (~100 expected at the default rate)
+
+template <int GC>
 __global__ __launch_bounds__(kBlock) void sketch_k(const u32* __restrict__ codes, const unsigned short* __restrict__ inval,
                                                   u64 n_reads, int G, int k, int rate_bits, u64* __restrict__ out,
                                                   u64 cap, u64* __restrict__ counter) {
+    __shared__ u64 sbuf[kSketchBuf];
+    __shared__ u32 scnt;
+    __shared__ u64 sbase;
     const int ng = (k + 15) >> 4;  // groups a k-mer spans from a group start
     const int per = G - ng + 1;    // aligned k-mers per read
     const u32 rmask = (1u << rate_bits) - 1;
     const int nb0 = min(16, k);
     const u32 keep0 = nb0 == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb0));
     const u32 seed = 0x9e3779b9u ^ (u32)k;
-    // one read per thread (no division per item); a wave takes one counter
-    // add per aligned position that sampled anything
+    if (threadIdx.x == 0) scnt = 0;
+    __syncthreads();
     for (u64 r0 = (u64)blockIdx.x * kBlock; r0 < n_reads; r0 += (u64)gridDim.x * kBlock) {
         const u64 r = r0 + threadIdx.x;
         const bool live = r < n_reads;
         const u64 row = (live ? r : 0) * (u64)G;
-        for (int g = 0; g < per; g++) {
-            const u64 base = row + (u64)g;
-            bool take = live && (sketch_mix32((codes[base] & keep0) ^ seed) & rmask) == 0;
-            u64 h = 0;
-            if (take) {  // rare: the whole k-mer
-                h = 0x243f6a8885a308d3ull ^ (u64)k;
+        for (int g0 = 0; g0 < (GC > 0 ? 1 : per); g0 += 64) {
+            // the candidates' first words: a bit per aligned position g0 + bit
+            u64 cand = 0;
+            if constexpr (GC > 0) {
+                u32 cw[GC];
+                const u64* rp = (const u64*)(codes + row);
+#pragma unroll
+                for (int j = 0; j < GC / 2; j++) {
+                    const u64 v = __builtin_nontemporal_load(rp + j);
+                    cw[2 * j] = (u32)v;
+                    cw[2 * j + 1] = (u32)(v >> 32);
+                }
+#pragma unroll
+                for (int g = 0; g < GC; g++)
+                    if (g < per && live && (sketch_mix32((cw[g] & keep0) ^ seed) & rmask) == 0) cand |= 1ull << g;
+            } else {
+                for (int g = g0; g < min(per, g0 + 64); g++)
+                    if (live && (sketch_mix32((codes[row + (u64)g] & keep0) ^ seed) & rmask) == 0)
+                        cand |= 1ull << (g - g0);
+            }
+            // rare: the sampled k-mers whole (their words and not-ACGT masks)
+            while (cand) {
+                const int g = g0 + __ffsll((long long)cand) - 1;
+                cand &= cand - 1;
+                const u64 base = row + (u64)g;
+                u64 h = 0x243f6a8885a308d3ull ^ (u64)k;
+                bool ok = true;
                 for (int j = 0; j < ng; j++) {
                     const int nb = min(16, k - 16 * j);  // bases of this group inside the k-mer
                     const u32 keep = nb == 16 ? 0xffffffffu : ~(0xffffffffu >> (2 * nb));
                     const unsigned short bad =
                         (unsigned short)(inval[base + j] & (nb == 16 ? 0xffffu : ~(0xffffu >> nb)));
-                    take = take && bad == 0;
+                    ok = ok && bad == 0;
                     h = mix64(h ^ (u64)(codes[base + j] & keep) ^ ((u64)j << 40));
                 }
-            }
-            const u64 m = __ballot(take);
-            if (!m) continue;
-            u64 at = 0;
-            const int lead = __ffsll((long long)m) - 1;
-            if (lane_id() == lead) at = atomicAdd((unsigned long long*)counter, (unsigned long long)__popcll(m));
-            at = __shfl(at, lead);
-            if (take) {
-                const u64 q = at + (u64)__popcll(m & lanemask_lt());
-                if (q < cap) out[q] = h >> 8;
+                if (!ok) continue;
+                const u32 i = atomicAdd(&scnt, 1u);
+                if (i < kSketchBuf) {
+                    sbuf[i] = h >> 8;
+                } else {  // a full buffer: straight out (not expected at the planned rates)
+                    const u64 q = atomicAdd((unsigned long long*)counter, 1ull);
+                    if (q < cap) out[q] = h >> 8;
+                }
             }
         }
     }
+    __syncthreads();
+    const u32 m = min(scnt, kSketchBuf);
+    if (threadIdx.x == 0) sbase = m ? atomicAdd((unsigned long long*)counter, (unsigned long long)m) : 0ull;
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < m; i += kBlock)
+        if (sbase + i < cap) out[sbase + i] = sbuf[i];
 }
 
 hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, int rate_bits,
                          uint64_t* out, uint64_t cap, uint64_t* counter, hipStream_t s) {
     const int G = groups_per_read(L);
     if (G <= 0 || n_reads == 0) return hipSuccess;
-    hipLaunchKernelGGL(sketch_k, dim3(grid_for(n_reads)), dim3(kBlock), 0, s, codes, (const unsigned short*)inval,
-                       n_reads, G, k, rate_bits, out, cap, counter);
+    // 8 workgroups per CU (the LDS sample buffers allow them), each walking
+    // its share of the reads
+    const int grid = grid_for(n_reads, 2048);
+#define KC_SKETCH(GCV) \
+    hipLaunchKernelGGL(sketch_k<GCV>, dim3(grid), dim3(kBlock), 0, s, codes, (const unsigned short*)inval, n_reads, G, \
+                       k, rate_bits, out, cap, counter)
+    switch (G) {  // common read lengths: the row in registers (G even: 8-byte aligned rows)
+    case 2: KC_SKETCH(2); break;
+    case 4: KC_SKETCH(4); break;
+    case 6: KC_SKETCH(6); break;
+    case 8: KC_SKETCH(8); break;
+    case 10: KC_SKETCH(10); break;
+    case 12: KC_SKETCH(12); break;
+    case 14: KC_SKETCH(14); break;
+    case 16: KC_SKETCH(16); break;
+    default: KC_SKETCH(0); break;
+    }
+#undef KC_SKETCH
     return hipGetLastError();
 }
 

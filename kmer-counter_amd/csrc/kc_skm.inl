@@ -1822,11 +1822,13 @@ __global__ __launch_bounds__(256) void rp_region_pos_k(const u32* __restrict__ c
 
 hipError_t launch_rp_hist_regional(const uint64_t* w0, int shift, const uint64_t* rstart, const uint64_t* tpre,
                                    int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos, uint32_t* cnt_t, int grid,
-                                   hipStream_t s) {
+                                   hipStream_t s, const uint8_t* digs) {
     if (ntiles == 0) return hipSuccess;
     const int gu = (int)hmin(ntiles, (u64)grid * 4);
-    hipLaunchKernelGGL(rp_upsweep_k, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)nullptr, w0, shift, rstart,
-                       tpre, nreg, ntiles, tile, cnt_t);
+    // digs: the digit byte of every item, written by the pass that placed
+    // them (1 B read per item instead of word 0)
+    hipLaunchKernelGGL(rp_upsweep_k, dim3(gu), dim3(kBlock), 0, s, (const unsigned char*)digs, digs ? nullptr : w0,
+                       shift, rstart, tpre, nreg, ntiles, tile, cnt_t);
     hipLaunchKernelGGL(rp_region_pos_k, dim3((u32)hmin((u64)nreg, 65536)), dim3(256), 0, s, (const u32*)cnt_t, rstart,
                        tpre, (u32)nreg, pos);
     return hipGetLastError();
