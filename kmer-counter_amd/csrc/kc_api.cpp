@@ -698,6 +698,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
     size_t kp_u_pass = ~(size_t)0;  // the pass whose P2 output is at kp_u_keys
     uint64_t* kp_u_keys = nullptr;
     uint64_t kp_u_n = 0;
+    // KC_P2_NO_DIGS (measurement): P2 writes no digit bytes (P3 reads word 0)
+    const bool p2_no_digs = getenv("KC_P2_NO_DIGS") != nullptr && !getenv("KC_P3_SCATTER");
     if (pre0 >= 0 && c->hc_hint && nw * n_reads > c->key_cap && c->rec_n == 0 && c->batches == 0 &&
         c->stats_h[ST_CLAIMED] == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES") &&
         !getenv("KC_NO_P3B") && !getenv("KC_NO_SORT_RUNS") && !getenv("KC_NO_P5S_DIRECT")) {
@@ -787,9 +789,11 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 l.fhi = kp[kpi + 2];  // the walk keeps both passes' ranges
             }
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48, c->digs,
-                                          c->stream, u ? (const uint64_t*)c->part_base2.p : nullptr, u,
-                                          u ? n2 : 0, u ? (uint8_t*)(u + (size_t)W * n2) : nullptr,
+            // (p2_no_digs: P2 writes no digit bytes, P3's histogram reads word 0)
+            HIPCHK(c, launch_part_scatter(l, pg, (const uint64_t*)c->part_base.p, c->keys_a, c->key_cap, 48,
+                                          p2_no_digs ? nullptr : c->digs, c->stream,
+                                          u ? (const uint64_t*)c->part_base2.p : nullptr, u, u ? n2 : 0,
+                                          u && !p2_no_digs ? (uint8_t*)(u + (size_t)W * n2) : nullptr,
                                           u ? kp[kpi + 1] : 256u));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
@@ -825,8 +829,12 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             uint64_t* p3t = p3h + 256 * ntiles + p3_tmp_elems(ntiles);
             HIPCHK(c, hipMemcpyAsync(p3t, rt.data(), 2 * 257 * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_p3_hist(W, p2_digs, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
-                                     c->stream));
+            if (p2_no_digs)
+                HIPCHK(c, launch_rp_hist(nullptr, p2_keys, 56, p3t, p3t + 257, 256, ntiles, (uint32_t)tile, p3h,
+                                         p3h + 256 * ntiles, 2 * c->n_cu, c->stream));
+            else
+                HIPCHK(c, launch_p3_hist(W, p2_digs, p3t, p3t + 257, ntiles, p3h, p3h + 256 * ntiles, 2 * c->n_cu,
+                                         c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));

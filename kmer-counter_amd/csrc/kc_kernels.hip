@@ -777,7 +777,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                         o[g] = k0;
 #pragma unroll
                         for (int j = 1; j < W; j++) o[(u64)j * ost + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
-                        (sl >= 256u ? pa.digs2 : pa.digs)[g] = (unsigned char)(k0 >> 56);
+                        if (pa.digs) (sl >= 256u ? pa.digs2 : pa.digs)[g] = (unsigned char)(k0 >> 56);
                     }
                     __syncthreads();
                     if (tid < 512) {
@@ -1087,7 +1087,7 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa.flo = l.flo;
     pa.fhi = l.fhi;
     pa.no_stats = l.no_stats ? 1 : 0;
-    if (out2 && (!base2 || !digs2 || fmid <= l.flo || fmid >= l.fhi)) return hipErrorInvalidValue;
+    if (out2 && (!base2 || (!digs2 && digs) || fmid <= l.flo || fmid >= l.fhi)) return hipErrorInvalidValue;
     pa.out2 = out2;
     pa.out2_stride = out2_stride;
     pa.base2 = base2;
