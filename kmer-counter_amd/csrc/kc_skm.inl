@@ -1563,19 +1563,41 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
 #define KC_RP_WPC 1
 #endif
 
+// the radix scatter's write phase issues a fixed number of stores per tile
+// (see rp_scatter_k); KC_RP_DYNAMIC_STORES: the earlier loop over the tile
+#ifndef KC_RP_DYNAMIC_STORES
+#define KC_RP_STATIC_STORES
+#endif
+
+// threads per radix-scatter workgroup (variant builds: KC_RP_BLOCK=512 with
+// KC_RP_WPC=2 and half the LDS budget runs two workgroups per CU)
+#ifndef KC_RP_BLOCK
+#define KC_RP_BLOCK 1024
+#endif
+constexpr int kRpBlock = KC_RP_BLOCK;
+constexpr int kRpWaves = kRpBlock / 64;
+#ifdef KC_RP_STATIC_STORES
+constexpr int kRpGposN = 512;  // run starts of this tile and the next
+#else
+constexpr int kRpGposN = 256;
+#endif
+
+// (a payload tile gives up the second half of gpos, 2 KiB, to stay in 160 KiB)
+constexpr int rp_lds_budget(bool pay) { return pay && kRpGposN > 256 ? KC_RP_LDS - 2112 : KC_RP_LDS; }
+
 template <int NW, bool PAY>
 struct RpCfg {
     static constexpr int BYTES = 8 * NW + (PAY ? 4 : 0);
-    static constexpr int K0 = KC_RP_LDS / (BYTES * kP3Block);
+    static constexpr int K0 = rp_lds_budget(PAY) / (BYTES * kRpBlock);
     static constexpr int KPT = K0 > 16 ? 16 : K0;
-    static constexpr int TILE = kP3Block * KPT;
+    static constexpr int TILE = kRpBlock * KPT;
 };
 
 int rp_tile(int NW, bool pay) {
     const int bytes = 8 * NW + (pay ? 4 : 0);
-    int kpt = KC_RP_LDS / (bytes * kP3Block);
+    int kpt = rp_lds_budget(pay) / (bytes * kRpBlock);
     if (kpt > 16) kpt = 16;
-    return kP3Block * kpt;
+    return kRpBlock * kpt;
 }
 
 __device__ __forceinline__ void rp_tile_range(const u64* __restrict__ rstart, const u64* __restrict__ tpre, int nreg,
@@ -1634,8 +1656,14 @@ __global__ __launch_bounds__(kBlock) void rp_upsweep_k(const unsigned char* __re
     }
 }
 
+// KC_RP_ABL (timing ablations of tools/rp_bench, variant builds only): bit 1
+// no global stores, bit 2 no ranking / LDS scatter, bit 4 no global loads
+#ifndef KC_RP_ABL
+#define KC_RP_ABL 0
+#endif
+
 template <int NW, bool PAY>
-__global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__ kin, u64 istride,
+__global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__ kin, u64 istride,
                                                          u64* __restrict__ kout, u64 ostride,
                                                          const u32* __restrict__ pin, u32* __restrict__ pout,
                                                          const u64* __restrict__ rstart, const u64* __restrict__ tpre,
@@ -1646,11 +1674,11 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* skey = (u64*)smem;                                    // NW x TILE
     u32* spay = (u32*)(skey + (size_t)NW * TILE);              // TILE (PAY)
-    u32* wc = spay + (PAY ? TILE : 0);                         // 16 waves x 128 words: two u16 counters each
-    unsigned short* woff = (unsigned short*)(wc + 16 * 128);   // 16 x 256
-    u32* dst = (u32*)(woff + 16 * 256);                        // 256 digit starts in the tile
-    u64* gpos = (u64*)(dst + 256);                             // 256 global run starts
-    u32* wsum = (u32*)(gpos + 256);                            // 16
+    u32* wc = spay + (PAY ? TILE : 0);                         // kRpWaves x 128 words: two u16 counters each
+    unsigned short* woff = (unsigned short*)(wc + kRpWaves * 128);  // kRpWaves x 256
+    u32* dst = (u32*)(woff + kRpWaves * 256);                        // 256 digit starts in the tile
+    u64* gpos = (u64*)(dst + 256);                             // 256 global run starts (x2: static variant)
+    u32* wsum = (u32*)(gpos + kRpGposN);                       // 16
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     u64 nk[KPT][NW];
     u32 np[KPT];
@@ -1665,19 +1693,55 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
     const u64 t_first = xcd_map ? (u64)(blockIdx.x & 7u) * tx + (blockIdx.x >> 3) : (u64)blockIdx.x;
     const u64 t_end = xcd_map ? min(ntiles, (u64)((blockIdx.x & 7u) + 1) * tx) : ntiles;
     auto load = [&](u64 t) {
+#ifdef KC_RP_STATIC_STORES
+        t = min(t, t_end - 1);  // unconditional (the last tile again past the end)
+#else
         if (t >= t_end) return;
+#endif
         u64 lo = 0, hi = 0;
         rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
         // unconditional loads (clamped into the tile, which is never empty):
         // a per-element select on a load makes hipcc wait for each one
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
-            const u64 q = min(lo + (u64)i * kP3Block + tid, hi - 1);
+            const u64 q = min(lo + (u64)i * kRpBlock + tid, hi - 1);
 #pragma unroll
-            for (int j = 0; j < NW; j++) nk[i][j] = __builtin_nontemporal_load(kin + (u64)j * istride + q);
-            if constexpr (PAY) np[i] = __builtin_nontemporal_load(pin + q);
+            for (int j = 0; j < NW; j++)
+                nk[i][j] = (KC_RP_ABL & 4) ? (q + 1) * 0x9e3779b97f4a7c15ull * (j + 1)
+                                           : __builtin_nontemporal_load(kin + (u64)j * istride + q);
+            if constexpr (PAY) np[i] = (KC_RP_ABL & 4) ? (u32)q : __builtin_nontemporal_load(pin + q);
         }
     };
+#ifdef KC_RP_STATIC_STORES
+    // Pipeline with in-order vmcnt in mind: the next tile's run starts (npos)
+    // and items (nk) are issued at the top of a tile; npos goes into the
+    // other half of gpos before this tile's write phase (its wait only drains
+    // the previous tile's stores, issued a whole rank/scatter phase earlier);
+    // nk is copied into key after the write phase, whose store count is fixed
+    // (fully unrolled, lanes past the tile end rewrite its last record), so
+    // that wait leaves the stores in flight instead of draining them.
+    if (t_first >= t_end) return;
+    u64 npos = pos[t_first * 256 + (tid & 255)];
+    load(t_first);
+    u64 key[KPT][NW];
+    u32 pv[KPT];
+#pragma unroll
+    for (int i = 0; i < KPT; i++) {
+#pragma unroll
+        for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
+        pv[i] = PAY ? np[i] : 0u;
+    }
+    if (tid < 256) gpos[tid] = npos;
+    int cur = 0;
+    for (u64 t = t_first; t < t_end; t += step) {
+        u64 lo, hi;
+        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
+        const u32 len = (u32)(hi - lo);
+        for (int i = tid; i < kRpWaves * 128; i += kRpBlock) wc[i] = 0;
+        __syncthreads();
+        npos = pos[min(t + step, t_end - 1) * 256 + (tid & 255)];
+        load(t + step);
+#else
     load(t_first);
     // this tile's 256 global run starts, loaded one tile ahead like the items
     u64 npos = (tid < 256 && t_first < t_end) ? pos[t_first * 256 + tid] : 0ull;
@@ -1693,17 +1757,18 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
             for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
             pv[i] = PAY ? np[i] : 0u;
         }
-        for (int i = tid; i < 16 * 128; i += kP3Block) wc[i] = 0;
+        for (int i = tid; i < kRpWaves * 128; i += kRpBlock) wc[i] = 0;
         if (tid < 256) gpos[tid] = npos;
         __syncthreads();
         load(t + step);
         if (tid < 256 && t + step < t_end) npos = pos[(t + step) * 256 + tid];
+#endif
         u32 rank[KPT];
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
-            const u32 q = (u32)i * kP3Block + (u32)tid;
+            const u32 q = (u32)i * kRpBlock + (u32)tid;
             rank[i] = 0;
-            if (q < len) {
+            if (q < len && !(KC_RP_ABL & 2)) {
                 const u32 d = (u32)(key[i][0] >> dshift) & 255u;
                 const u32 sh = 16 * (d & 1);
                 rank[i] = (atomicAdd(&wc[wave * 128 + (d >> 1)], 1u << sh) >> sh) & 0xffffu;
@@ -1712,7 +1777,7 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
         __syncthreads();
         if (tid < 256) {
             u32 run = 0;
-            for (int w = 0; w < 16; w++) {
+            for (int w = 0; w < kRpWaves; w++) {
                 woff[w * 256 + tid] = (unsigned short)run;
                 run += (wc[w * 128 + (tid >> 1)] >> (16 * (tid & 1))) & 0xffffu;
             }
@@ -1735,8 +1800,8 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
-            const u32 q = (u32)i * kP3Block + (u32)tid;
-            if (q < len) {
+            const u32 q = (u32)i * kRpBlock + (u32)tid;
+            if (q < len && !(KC_RP_ABL & 2)) {
                 const u32 d = (u32)(key[i][0] >> dshift) & 255u;
                 const u32 at = dst[d] + woff[wave * 256 + d] + rank[i];
 #pragma unroll
@@ -1744,25 +1809,57 @@ __global__ __launch_bounds__(kP3Block) void rp_scatter_k(const u64* __restrict__
                 if constexpr (PAY) spay[at] = pv[i];
             }
         }
+#ifdef KC_RP_STATIC_STORES
+        if (tid < 256) gpos[(cur ^ 1) * 256 + tid] = npos;
+        const u64* gp = gpos + cur * 256;
+#else
+        const u64* gp = gpos;
+#endif
         __syncthreads();
-        for (u32 q = tid; q < len; q += kP3Block) {
+#ifdef KC_RP_STATIC_STORES
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+            const u32 q = min((u32)i * kRpBlock + (u32)tid, len - 1);
+#else
+        for (u32 q = tid; q < len; q += kRpBlock) {
+#endif
             const u64 k0 = skey[q];
             const u32 d = (u32)(k0 >> dshift) & 255u;
-            const u64 g = gpos[d] + (q - dst[d]);
+            const u64 g = gp[d] + (q - dst[d]);
+            if (KC_RP_ABL & 1) {
+                if (g == ~0ull) kout[0] = k0;  // keeps the work, writes nothing
+                continue;
+            }
+#ifdef KC_RP_NTSTORE
+            __builtin_nontemporal_store(k0, kout + g);
+#pragma unroll
+            for (int j = 1; j < NW; j++) __builtin_nontemporal_store(skey[(size_t)j * TILE + q], kout + (u64)j * ostride + g);
+#else
             kout[g] = k0;
 #pragma unroll
             for (int j = 1; j < NW; j++) kout[(u64)j * ostride + g] = skey[(size_t)j * TILE + q];
+#endif
             if constexpr (PAY) pout[g] = spay[q];
             if (emit) emit[g] = (unsigned char)(k0 >> eshift);
         }
+#ifdef KC_RP_STATIC_STORES
+        // the next tile's items (their wait counts this tile's stores)
+#pragma unroll
+        for (int i = 0; i < KPT; i++) {
+#pragma unroll
+            for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
+            pv[i] = PAY ? np[i] : 0u;
+        }
+        cur ^= 1;
+#endif
         __syncthreads();
     }
 }
 
 static size_t rp_scatter_lds(int NW, bool pay) {
     const size_t tile = (size_t)rp_tile(NW, pay);
-    return (size_t)NW * tile * 8 + (pay ? tile * 4 : 0) + 16 * 128 * 4 + 16 * 256 * 2 + 256 * 4 + 256 * 8 + 16 * 4 +
-           16;
+    return (size_t)NW * tile * 8 + (pay ? tile * 4 : 0) + kRpWaves * 128 * 4 + kRpWaves * 256 * 2 + 256 * 4 +
+           kRpGposN * 8 + 16 * 4 + 16;
 }
 
 u64* rp_digit_base(u64* tmp, uint64_t ntiles) {
@@ -1845,7 +1942,7 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
     const int g = (int)hmin(ntiles, (u64)(grid / 2 > 0 ? KC_RP_WPC * grid / 2 : 1));
     const size_t lds = (rp_scatter_lds(NW, pay) + 15) & ~(size_t)15;
 #define KC_RPS(NWV, PAYV)                                                                                          \
-    hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kP3Block), lds, s, kin, istride, kout, ostride, pin, \
+    hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kRpBlock), lds, s, kin, istride, kout, ostride, pin, \
                        pout, rstart, tpre, nreg, ntiles, pos, dshift, (unsigned char*)emit, eshift)
     if (pay) {
         switch (NW) {

@@ -1,0 +1,80 @@
+// rp_bench: the radix scatter (rp_scatter_k, S / P3 / P3b) alone on random
+// records, timed with HIP events; run against variant builds of
+// libkc_hip.so (tools/build_variant.sh, KC_RP_ABL ablations) through
+// LD_LIBRARY_PATH. Usage: rp_bench [n_records] [NW] [reps]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "kc_device.h"
+
+__global__ void fill_k(uint64_t* a, uint64_t n, int NW, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        for (int j = 0; j < NW; j++) {
+            uint64_t x = (i + 1) * 0x9e3779b97f4a7c15ull + seed + (uint64_t)j * 0x632be59bd9b4e019ull;
+            x ^= x >> 31;
+            x *= 0xbf58476d1ce4e5b9ull;
+            x ^= x >> 29;
+            a[(uint64_t)j * n + i] = x;
+        }
+    }
+}
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "%s: %s (line %d)\n", #x, hipGetErrorString(e_), __LINE__); \
+            return 1;                                                                    \
+        }                                                                                \
+    } while (0)
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 592344064ull;
+    const int NW = argc > 2 ? atoi(argv[2]) : 2;
+    const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const bool with_emit = argc > 4 ? atoi(argv[4]) != 0 : true;  // digit bytes for the next level
+    const int dshift = argc > 5 ? atoi(argv[5]) : 48;  // 56 + 6 = 62: 4 digits, long runs
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int ncu = prop.multiProcessorCount;
+    const uint64_t tile = (uint64_t)kc::rp_tile(NW, false);
+    const uint64_t nt = (n + tile - 1) / tile;
+    uint64_t *a, *b, *rt, *pos, *tmp;
+    uint8_t* digs;
+    CK(hipMalloc(&a, n * 8 * NW));
+    CK(hipMalloc(&b, n * 8 * NW));
+    CK(hipMalloc(&digs, n + 64));
+    CK(hipMalloc(&rt, 64));
+    CK(hipMalloc(&pos, nt * 256 * 8));
+    CK(hipMalloc(&tmp, nt * 256 * 8 + (64 << 20)));
+    uint64_t h[4] = {0, n, 0, nt};
+    CK(hipMemcpy(rt, h, 32, hipMemcpyHostToDevice));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(fill_k, dim3(8192), dim3(256), 0, s, a, n, NW, 12345ull);
+    CK(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(kc::launch_rp_hist(nullptr, a, dshift, rt, rt + 2, 1, nt, (uint32_t)tile, pos, tmp, 2 * ncu, s));
+    float best = 1e30f, tot = 0.f;
+    for (int r = 0; r < reps + 1; r++) {
+        CK(hipEventRecord(e0, s));
+        CK(kc::launch_rp_scatter(NW, false, a, n, b, n, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift, with_emit ? digs : nullptr, 56,
+                                 2 * ncu, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        if (r > 0) {
+            tot += t;
+            if (t < best) best = t;
+        }
+    }
+    const double bytes = (double)n * (16.0 * NW + (with_emit ? 1.0 : 0.0));
+    printf("{\"dshift\": %d, \"n\": %llu, \"NW\": %d, \"emit\": %d, \"tile\": %llu, \"avg_ms\": %.3f, \"best_ms\": %.3f, \"GBps_avg\": %.1f}\n",
+           dshift, (unsigned long long)n, NW, with_emit ? 1 : 0, (unsigned long long)tile, tot / reps, best,
+           bytes / (tot / reps / 1e3) / 1e9);
+    return 0;
+}
