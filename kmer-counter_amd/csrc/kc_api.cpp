@@ -700,6 +700,11 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
     uint64_t kp_u_n = 0;
     // KC_P2_NO_DIGS (measurement): P2 writes no digit bytes (P3 reads word 0)
     const bool p2_no_digs = getenv("KC_P2_NO_DIGS") != nullptr && !getenv("KC_P3_SCATTER");
+    // P2 writes each key as W consecutive words (one stream per digit run
+    // instead of W) when P3 is the radix scatter, which reads them so
+    // (KC_P2_SOA: the SoA layout, for comparison)
+    const bool p2_aos =
+        !p2_no_digs && !getenv("KC_P2_SOA") && !getenv("KC_P3_SCATTER") && p3_tile(W) == rp_tile(W, false);
     if (pre0 >= 0 && c->hc_hint && nw * n_reads > c->key_cap && c->rec_n == 0 && c->batches == 0 &&
         c->stats_h[ST_CLAIMED] == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES") &&
         !getenv("KC_NO_P3B") && !getenv("KC_NO_SORT_RUNS") && !getenv("KC_NO_P5S_DIRECT")) {
@@ -794,7 +799,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                                           p2_no_digs ? nullptr : c->digs, c->stream,
                                           u ? (const uint64_t*)c->part_base2.p : nullptr, u, u ? n2 : 0,
                                           u && !p2_no_digs ? (uint8_t*)(u + (size_t)W * n2) : nullptr,
-                                          u ? kp[kpi + 1] : 256u));
+                                          u ? kp[kpi + 1] : 256u, p2_aos));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -841,6 +846,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             c->part_ms[3] += t;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
             uint8_t* p3b_digs = nullptr;  // P3b digit bytes written by P3 (else P3b reads word 0)
+            bool p3_aos = false;          // P3's output keys AoS (only when P3b follows)
             // P3's scatter is the regional radix scatter (digit word0 >> 56 over
             // the 256 P2 regions, same tiles; next tile's run starts prefetched,
             // XCD-aware tile walk); KC_P3_SCATTER: the older p3_scatter_k
@@ -853,8 +859,11 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 // digit byte (bits 40..47) into the free P2 digit array, so P3b's
                 // histogram reads 1 B per key, not word 0
                 p3b_digs = c->hc_hint && n >= p3b_min_of() && !getenv("KC_NO_P3B") ? c->digs : nullptr;
-                HIPCHK(c, launch_rp_scatter(W, false, p2_keys, p2_stride, c->keys_b, c->key_cap, nullptr, nullptr, p3t,
-                                            p3t + 257, 256, ntiles, p3h, 56, p3b_digs, 40, 2 * c->n_cu, c->stream));
+                // ... and writes the keys AoS for it (P3b reads them so)
+                p3_aos = p3b_digs && !getenv("KC_P3_SOA");
+                HIPCHK(c, launch_rp_scatter(W, false, p2_keys, p2_aos ? 0 : p2_stride, c->keys_b,
+                                            p3_aos ? 0 : c->key_cap, nullptr, nullptr, p3t, p3t + 257, 256, ntiles,
+                                            p3h, 56, p3b_digs, 40, 2 * c->n_cu, c->stream));
             }
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
@@ -865,8 +874,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             uint32_t nb = 1u << kBucketBits;
             if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8))) return s;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-            HIPCHK(c, launch_bucket_bounds(W, c->keys_b, c->key_cap, n, kBucketBits, (uint64_t*)c->part_starts.p,
-                                           c->stream));
+            HIPCHK(c, launch_bucket_bounds(W, c->keys_b, p3_aos ? 0 : c->key_cap, n, kBucketBits,
+                                           (uint64_t*)c->part_starts.p, c->stream));
             HIPCHK(c, hipEventRecord(c->ev1, c->stream));
             HIPCHK(c, hipEventSynchronize(c->ev1));
             HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -902,7 +911,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                 HIPCHK(c, launch_rp_hist_regional(c->keys_b, 40, rtd, rtd + nb + 1, (int)nb, nt, (uint32_t)tile, pos,
                                                   cnt_t, 2 * c->n_cu, c->stream, p3b_digs));
-                HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, c->key_cap, c->keys_a, c->key_cap, nullptr, nullptr,
+                HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, p3_aos ? 0 : c->key_cap, c->keys_a, c->key_cap,
+                                            nullptr, nullptr,
                                             rtd, rtd + nb + 1, (int)nb, nt, pos, 40, nullptr, 0, 2 * c->n_cu,
                                             c->stream));
                 HIPCHK(c, launch_sub_starts(rtd, rtd + nb + 1, pos, nb, n, (uint64_t*)c->sub_starts.p, c->stream));

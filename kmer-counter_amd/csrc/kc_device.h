@@ -128,7 +128,8 @@ hipError_t launch_hist_group_totals(const uint64_t* h, uint64_t nseg, uint32_t g
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
                                uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s,
                                const uint64_t* base2 = nullptr, uint64_t* out2 = nullptr,
-                               uint64_t out2_stride = 0, uint8_t* digs2 = nullptr, uint32_t fmid = 256);
+                               uint64_t out2_stride = 0, uint8_t* digs2 = nullptr, uint32_t fmid = 256,
+                               bool aos = false);
 // P3 (regional scatter, see kc_kernels.hip): rstart[257] region bounds,
 // tpre[257] tile prefix per region (tiles of p3_tile(W) keys); hist holds
 // 256 * ntiles u64, tmp scan_tmp_elems(256 * ntiles) u64.
@@ -307,6 +308,8 @@ hipError_t launch_rp_hist(const uint8_t* digs, const uint64_t* w0, int shift, co
 hipError_t launch_rp_hist_regional(const uint64_t* w0, int shift, const uint64_t* rstart, const uint64_t* tpre,
                                    int nreg, uint64_t ntiles, uint32_t tile, uint64_t* pos, uint32_t* cnt_t, int grid,
                                    hipStream_t s, const uint8_t* digs = nullptr);
+// istride / ostride 0: the input / output items are NW consecutive words each
+// (AoS, as P2 writes them and P3b reads P3's output), else NW word arrays
 hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t istride, uint64_t* kout,
                              uint64_t ostride, const uint32_t* pin, uint32_t* pout, const uint64_t* rstart,
                              const uint64_t* tpre, int nreg, uint64_t ntiles, const uint64_t* pos, int dshift,

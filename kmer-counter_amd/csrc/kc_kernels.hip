@@ -317,6 +317,7 @@ struct PartArgs {
     unsigned char* digs2;
     u32 fmid;
     int no_stats;     // key-range pass after the first: valid / key-0 statistics not counted again
+    int aos;          // SCATTER: keys written as W consecutive words (16-byte stores at W = 2), not SoA
 };
 
 static size_t sink_lds_host(int W, int sink, int scap) {
@@ -774,9 +775,24 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                         if (pa.skip & 1) continue;
                         u64* __restrict__ o = sl >= 256u ? pa.out2 : pa.out;
                         const u64 ost = sl >= 256u ? pa.out2_stride : pa.out_stride;
-                        o[g] = k0;
+                        if (pa.aos) {
+                            // one record per lane: a digit run is one contiguous
+                            // stream, half the partial lines of two word arrays
+                            if constexpr (W == 2) {
+                                v2u64 v;
+                                v.x = k0;
+                                v.y = s_stage[(size_t)(pa.scap + 1) + i];
+                                *(v2u64*)(o + 2 * g) = v;
+                            } else {
+                                o[g * W] = k0;
 #pragma unroll
-                        for (int j = 1; j < W; j++) o[(u64)j * ost + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
+                                for (int j = 1; j < W; j++) o[g * W + j] = s_stage[(size_t)j * (pa.scap + 1) + i];
+                            }
+                        } else {
+                            o[g] = k0;
+#pragma unroll
+                            for (int j = 1; j < W; j++) o[(u64)j * ost + g] = s_stage[(size_t)j * (pa.scap + 1) + i];
+                        }
                         if (pa.digs) (sl >= 256u ? pa.digs2 : pa.digs)[g] = (unsigned char)(k0 >> 56);
                     }
                     __syncthreads();
@@ -1066,7 +1082,7 @@ hipError_t launch_part_hist(const CountLaunch& l, const PartGeom& pg, uint64_t* 
 
 hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const uint64_t* base, uint64_t* out,
                                uint64_t out_stride, int shift, uint8_t* digs, hipStream_t s, const uint64_t* base2,
-                               uint64_t* out2, uint64_t out2_stride, uint8_t* digs2, uint32_t fmid) {
+                               uint64_t* out2, uint64_t out2_stride, uint8_t* digs2, uint32_t fmid, bool aos) {
     if (l.n_reads == 0) return hipSuccess;
     const CountGeom& g = pg.geom;
     CountArgs a = make_args(l, g);
@@ -1077,6 +1093,7 @@ hipError_t launch_part_scatter(const CountLaunch& l, const PartGeom& pg, const u
     pa.base = base;
     pa.out = out;
     pa.digs = (unsigned char*)digs;
+    pa.aos = aos ? 1 : 0;
     pa.out_stride = out_stride;
     pa.codes = l.codes;
     pa.inval = (const unsigned short*)l.inval;
@@ -1818,10 +1835,8 @@ __global__ __launch_bounds__(kBlock) void bucket_bounds_k(const u64* __restrict_
         u64 lo = 0, hi = n;
         while (lo < hi) {
             u64 mid = (lo + hi) >> 1;
-            u64 k[W];
-#pragma unroll
-            for (int j = 0; j < W; j++) k[j] = keys[(u64)j * stride + mid];
-            if ((k[0] >> (64 - bits)) < b)
+            const u64 k0 = keys[stride ? mid : mid * W];  // (stride 0: W consecutive words per key)
+            if ((k0 >> (64 - bits)) < b)
                 lo = mid + 1;
             else
                 hi = mid;

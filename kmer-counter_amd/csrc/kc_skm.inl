@@ -1563,12 +1563,6 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
 #define KC_RP_WPC 1
 #endif
 
-// the radix scatter's write phase issues a fixed number of stores per tile
-// (see rp_scatter_k); KC_RP_DYNAMIC_STORES: the earlier loop over the tile
-#ifndef KC_RP_DYNAMIC_STORES
-#define KC_RP_STATIC_STORES
-#endif
-
 // threads per radix-scatter workgroup (variant builds: KC_RP_BLOCK=512 with
 // KC_RP_WPC=2 and half the LDS budget runs two workgroups per CU)
 #ifndef KC_RP_BLOCK
@@ -1576,26 +1570,18 @@ hipError_t launch_skm_front(const CountLaunch& l, const SkmGeom& g, uint64_t* po
 #endif
 constexpr int kRpBlock = KC_RP_BLOCK;
 constexpr int kRpWaves = kRpBlock / 64;
-#ifdef KC_RP_STATIC_STORES
-constexpr int kRpGposN = 512;  // run starts of this tile and the next
-#else
-constexpr int kRpGposN = 256;
-#endif
-
-// (a payload tile gives up the second half of gpos, 2 KiB, to stay in 160 KiB)
-constexpr int rp_lds_budget(bool pay) { return pay && kRpGposN > 256 ? KC_RP_LDS - 2112 : KC_RP_LDS; }
 
 template <int NW, bool PAY>
 struct RpCfg {
     static constexpr int BYTES = 8 * NW + (PAY ? 4 : 0);
-    static constexpr int K0 = rp_lds_budget(PAY) / (BYTES * kRpBlock);
+    static constexpr int K0 = KC_RP_LDS / (BYTES * kRpBlock);
     static constexpr int KPT = K0 > 16 ? 16 : K0;
     static constexpr int TILE = kRpBlock * KPT;
 };
 
 int rp_tile(int NW, bool pay) {
     const int bytes = 8 * NW + (pay ? 4 : 0);
-    int kpt = rp_lds_budget(pay) / (bytes * kRpBlock);
+    int kpt = KC_RP_LDS / (bytes * kRpBlock);
     if (kpt > 16) kpt = 16;
     return kRpBlock * kpt;
 }
@@ -1677,8 +1663,8 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
     u32* wc = spay + (PAY ? TILE : 0);                         // kRpWaves x 128 words: two u16 counters each
     unsigned short* woff = (unsigned short*)(wc + kRpWaves * 128);  // kRpWaves x 256
     u32* dst = (u32*)(woff + kRpWaves * 256);                        // 256 digit starts in the tile
-    u64* gpos = (u64*)(dst + 256);                             // 256 global run starts (x2: static variant)
-    u32* wsum = (u32*)(gpos + kRpGposN);                       // 16
+    u64* gpos = (u64*)(dst + 256);                             // 256 global run starts
+    u32* wsum = (u32*)(gpos + 256);                            // 16
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     u64 nk[KPT][NW];
     u32 np[KPT];
@@ -1693,11 +1679,7 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
     const u64 t_first = xcd_map ? (u64)(blockIdx.x & 7u) * tx + (blockIdx.x >> 3) : (u64)blockIdx.x;
     const u64 t_end = xcd_map ? min(ntiles, (u64)((blockIdx.x & 7u) + 1) * tx) : ntiles;
     auto load = [&](u64 t) {
-#ifdef KC_RP_STATIC_STORES
-        t = min(t, t_end - 1);  // unconditional (the last tile again past the end)
-#else
         if (t >= t_end) return;
-#endif
         u64 lo = 0, hi = 0;
         rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
         // unconditional loads (clamped into the tile, which is never empty):
@@ -1705,43 +1687,24 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
             const u64 q = min(lo + (u64)i * kRpBlock + tid, hi - 1);
+            if (istride == 0) {  // AoS items (uniform branch)
+                if constexpr (NW == 2) {
+                    const v2u64 v = __builtin_nontemporal_load((const v2u64*)(kin + 2 * q));
+                    nk[i][0] = v.x;
+                    nk[i][1] = v.y;
+                } else {
 #pragma unroll
-            for (int j = 0; j < NW; j++)
-                nk[i][j] = (KC_RP_ABL & 4) ? (q + 1) * 0x9e3779b97f4a7c15ull * (j + 1)
-                                           : __builtin_nontemporal_load(kin + (u64)j * istride + q);
+                    for (int j = 0; j < NW; j++) nk[i][j] = __builtin_nontemporal_load(kin + q * NW + j);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NW; j++)
+                    nk[i][j] = (KC_RP_ABL & 4) ? (q + 1) * 0x9e3779b97f4a7c15ull * (j + 1)
+                                               : __builtin_nontemporal_load(kin + (u64)j * istride + q);
+            }
             if constexpr (PAY) np[i] = (KC_RP_ABL & 4) ? (u32)q : __builtin_nontemporal_load(pin + q);
         }
     };
-#ifdef KC_RP_STATIC_STORES
-    // Pipeline with in-order vmcnt in mind: the next tile's run starts (npos)
-    // and items (nk) are issued at the top of a tile; npos goes into the
-    // other half of gpos before this tile's write phase (its wait only drains
-    // the previous tile's stores, issued a whole rank/scatter phase earlier);
-    // nk is copied into key after the write phase, whose store count is fixed
-    // (fully unrolled, lanes past the tile end rewrite its last record), so
-    // that wait leaves the stores in flight instead of draining them.
-    if (t_first >= t_end) return;
-    u64 npos = pos[t_first * 256 + (tid & 255)];
-    load(t_first);
-    u64 key[KPT][NW];
-    u32 pv[KPT];
-#pragma unroll
-    for (int i = 0; i < KPT; i++) {
-#pragma unroll
-        for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
-        pv[i] = PAY ? np[i] : 0u;
-    }
-    if (tid < 256) gpos[tid] = npos;
-    int cur = 0;
-    for (u64 t = t_first; t < t_end; t += step) {
-        u64 lo, hi;
-        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
-        const u32 len = (u32)(hi - lo);
-        for (int i = tid; i < kRpWaves * 128; i += kRpBlock) wc[i] = 0;
-        __syncthreads();
-        npos = pos[min(t + step, t_end - 1) * 256 + (tid & 255)];
-        load(t + step);
-#else
     load(t_first);
     // this tile's 256 global run starts, loaded one tile ahead like the items
     u64 npos = (tid < 256 && t_first < t_end) ? pos[t_first * 256 + tid] : 0ull;
@@ -1762,7 +1725,6 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
         __syncthreads();
         load(t + step);
         if (tid < 256 && t + step < t_end) npos = pos[(t + step) * 256 + tid];
-#endif
         u32 rank[KPT];
 #pragma unroll
         for (int i = 0; i < KPT; i++) {
@@ -1809,49 +1771,34 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
                 if constexpr (PAY) spay[at] = pv[i];
             }
         }
-#ifdef KC_RP_STATIC_STORES
-        if (tid < 256) gpos[(cur ^ 1) * 256 + tid] = npos;
-        const u64* gp = gpos + cur * 256;
-#else
-        const u64* gp = gpos;
-#endif
         __syncthreads();
-#ifdef KC_RP_STATIC_STORES
-#pragma unroll
-        for (int i = 0; i < KPT; i++) {
-            const u32 q = min((u32)i * kRpBlock + (u32)tid, len - 1);
-#else
         for (u32 q = tid; q < len; q += kRpBlock) {
-#endif
             const u64 k0 = skey[q];
             const u32 d = (u32)(k0 >> dshift) & 255u;
-            const u64 g = gp[d] + (q - dst[d]);
+            const u64 g = gpos[d] + (q - dst[d]);
             if (KC_RP_ABL & 1) {
                 if (g == ~0ull) kout[0] = k0;  // keeps the work, writes nothing
                 continue;
             }
-#ifdef KC_RP_NTSTORE
-            __builtin_nontemporal_store(k0, kout + g);
+            if (ostride == 0) {  // AoS output (uniform branch)
+                if constexpr (NW == 2) {
+                    v2u64 v;
+                    v.x = k0;
+                    v.y = skey[(size_t)TILE + q];
+                    *(v2u64*)(kout + 2 * g) = v;
+                } else {
+                    kout[g * NW] = k0;
 #pragma unroll
-            for (int j = 1; j < NW; j++) __builtin_nontemporal_store(skey[(size_t)j * TILE + q], kout + (u64)j * ostride + g);
-#else
-            kout[g] = k0;
+                    for (int j = 1; j < NW; j++) kout[g * NW + j] = skey[(size_t)j * TILE + q];
+                }
+            } else {
+                kout[g] = k0;
 #pragma unroll
-            for (int j = 1; j < NW; j++) kout[(u64)j * ostride + g] = skey[(size_t)j * TILE + q];
-#endif
+                for (int j = 1; j < NW; j++) kout[(u64)j * ostride + g] = skey[(size_t)j * TILE + q];
+            }
             if constexpr (PAY) pout[g] = spay[q];
             if (emit) emit[g] = (unsigned char)(k0 >> eshift);
         }
-#ifdef KC_RP_STATIC_STORES
-        // the next tile's items (their wait counts this tile's stores)
-#pragma unroll
-        for (int i = 0; i < KPT; i++) {
-#pragma unroll
-            for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
-            pv[i] = PAY ? np[i] : 0u;
-        }
-        cur ^= 1;
-#endif
         __syncthreads();
     }
 }
@@ -1859,7 +1806,7 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
 static size_t rp_scatter_lds(int NW, bool pay) {
     const size_t tile = (size_t)rp_tile(NW, pay);
     return (size_t)NW * tile * 8 + (pay ? tile * 4 : 0) + kRpWaves * 128 * 4 + kRpWaves * 256 * 2 + 256 * 4 +
-           kRpGposN * 8 + 16 * 4 + 16;
+           256 * 8 + 16 * 4 + 16;
 }
 
 u64* rp_digit_base(u64* tmp, uint64_t ntiles) {
