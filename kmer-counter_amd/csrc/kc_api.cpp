@@ -498,7 +498,8 @@ static const double kSkmDistinctMax = 0.35;
 // kept and the caller counts it into records as usual. `total` sizes
 // fin_packed on the first pass (keys of all passes).
 static kc_status direct_keep(kc_ctx* c, uint64_t nrec);
-static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub_starts, uint32_t nb, uint64_t n,
+static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, uint64_t kstride, const uint64_t* sub_starts, uint32_t nb,
+                            uint64_t n,
                             uint8_t* rf, size_t fl, bool* done, uint64_t* records, float* ms, uint64_t pk_at = 0,
                             uint64_t total = 0, bool last = true) {
     kc_status s;
@@ -514,7 +515,7 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, const uint64_t* sub
     if (c->fin_packed.bytes < (off0 + pk_at + n) * rs) return fail(c, KC_ERR_INTERNAL, "key-range pass overflows its run");
     HIPCHK(c, hipMemsetAsync(rf, 0, fl, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_sort_runs(W, keys, c->key_cap, sub_starts, nb, c->rec_keys, c->rec_cnts, c->rec_cap,
+    HIPCHK(c, launch_sort_runs(W, keys, kstride, sub_starts, nb, c->rec_keys, c->rec_cnts, c->rec_cap,
                                c->rec_cursor, c->stats, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,
                                (uint32_t*)c->desc_len.p, kDescCap, rf, bf, nflag, 2 * c->n_cu, c->stream,
                                c->fin_packed.p, off0 + pk_at));
@@ -847,6 +848,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
             uint8_t* p3b_digs = nullptr;  // P3b digit bytes written by P3 (else P3b reads word 0)
             bool p3_aos = false;          // P3's output keys AoS (only when P3b follows)
+            bool p3b_aos = false;         // P3b's output keys AoS
             // P3's scatter is the regional radix scatter (digit word0 >> 56 over
             // the 256 P2 regions, same tiles; next tile's run starts prefetched,
             // XCD-aware tile walk); KC_P3_SCATTER: the older p3_scatter_k
@@ -887,6 +889,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             // consecutive sub-buckets in one pass each and reads every key
             // once instead of once per sub-range pass
             uint64_t* p5_keys = c->keys_b;
+            uint64_t p5_stride = c->key_cap;  // 0: AoS (P3b's output)
             uint64_t* p5_spill = c->keys_a;
             const uint64_t* sub_starts = nullptr;
             if (c->hc_hint && n >= p3b_min_of() && !getenv("KC_NO_P3B")) {
@@ -911,8 +914,10 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                 HIPCHK(c, launch_rp_hist_regional(c->keys_b, 40, rtd, rtd + nb + 1, (int)nb, nt, (uint32_t)tile, pos,
                                                   cnt_t, 2 * c->n_cu, c->stream, p3b_digs));
-                HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, p3_aos ? 0 : c->key_cap, c->keys_a, c->key_cap,
-                                            nullptr, nullptr,
+                // (its output AoS too, for P5s / the hash path; KC_P3B_SOA: arrays)
+                p3b_aos = !getenv("KC_P3B_SOA");
+                HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, p3_aos ? 0 : c->key_cap, c->keys_a,
+                                            p3b_aos ? 0 : c->key_cap, nullptr, nullptr,
                                             rtd, rtd + nb + 1, (int)nb, nt, pos, 40, nullptr, 0, 2 * c->n_cu,
                                             c->stream));
                 HIPCHK(c, launch_sub_starts(rtd, rtd + nb + 1, pos, nb, n, (uint64_t*)c->sub_starts.p, c->stream));
@@ -923,6 +928,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 c->presplit_ms += t;
                 c->presplit_batches++;
                 p5_keys = c->keys_a;
+                p5_stride = p3b_aos ? 0 : c->key_cap;
                 p5_spill = c->keys_b;
                 sub_starts = (const uint64_t*)c->sub_starts.p;
             }
@@ -955,7 +961,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 if (sort_runs) {
                     const size_t fl = ((size_t)nb << 8) + nb + 16;
                     if ((s = ensure(c, c->run_flags, fl))) return s;
-                    if ((s = p5s_direct(c, p5_keys, sub_starts, nb, n, (uint8_t*)c->run_flags.p, fl, &dd, &R, &t5,
+                    if ((s = p5s_direct(c, p5_keys, p5_stride, sub_starts, nb, n, (uint8_t*)c->run_flags.p, fl, &dd, &R, &t5,
                                         kp_out, kp_keys, last)))
                         return s;
                     c->part_ms[4] += t5;
@@ -987,7 +993,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 bool dd = false;
                 uint64_t R = 0;
                 float t5 = 0.f;
-                if ((s = p5s_direct(c, p5_keys, sub_starts, nb, n, (uint8_t*)c->run_flags.p, fl, &dd, &R, &t5)))
+                if ((s = p5s_direct(c, p5_keys, p5_stride, sub_starts, nb, n, (uint8_t*)c->run_flags.p, fl, &dd, &R, &t5)))
                     return s;
                 c->part_ms[4] += t5;
                 c->p5_launches++;
@@ -1011,7 +1017,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 uint32_t* nflag = (uint32_t*)(bf + nb);
                 HIPCHK(c, hipMemsetAsync(rf, 0, fl, c->stream));
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-                HIPCHK(c, launch_sort_runs(W, p5_keys, c->key_cap, sub_starts, nb, c->rec_keys, c->rec_cnts,
+                HIPCHK(c, launch_sort_runs(W, p5_keys, p5_stride, sub_starts, nb, c->rec_keys, c->rec_cnts,
                                            c->rec_cap, c->rec_cursor, c->stats, (uint64_t*)c->desc_key.p,
                                            (uint64_t*)c->desc_start.p, (uint32_t*)c->desc_len.p, kDescCap, rf, bf,
                                            nflag, 2 * c->n_cu, c->stream));
@@ -1019,7 +1025,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, hipMemcpyAsync(&nf, nflag, 4, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
                 if (nf)
-                    HIPCHK(c, launch_count_buckets(W, p5_keys, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
+                    HIPCHK(c, launch_count_buckets(W, p5_keys, p5_stride, (const uint64_t*)c->part_starts.p, nb,
                                                    c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table,
                                                    c->cap, p5_spill, c->key_cap, c->stats, l.probe_limit,
                                                    c->cfg.lds_slots, c->n_cu, (uint64_t*)c->desc_key.p,
@@ -1043,7 +1049,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 if ((s = grow_records(c, rec0 + bound))) return s;
                 // keys_a is free after P3: it takes P5's spills (capacity >= n)
                 HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-                HIPCHK(c, launch_count_buckets(W, p5_keys, c->key_cap, (const uint64_t*)c->part_starts.p, nb,
+                HIPCHK(c, launch_count_buckets(W, p5_keys, p5_stride, (const uint64_t*)c->part_starts.p, nb,
                                                c->rec_keys, c->rec_cnts, c->rec_cap, c->rec_cursor, c->table, c->cap,
                                                p5_spill, c->key_cap, c->stats, l.probe_limit, c->cfg.lds_slots,
                                                c->n_cu, (uint64_t*)c->desc_key.p, (uint64_t*)c->desc_start.p,

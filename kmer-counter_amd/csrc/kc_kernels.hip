@@ -24,6 +24,25 @@ typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 // space, which a generic volatile pointer loses (it would become a FLAT load)
 typedef __attribute__((address_space(3))) volatile v2u64 lds_v2u64;
 
+// key i of a key array into k: W word arrays at `stride`, or (stride 0) W
+// consecutive words per key (AoS; one 16-byte load at W = 2)
+template <int W>
+__device__ __forceinline__ void load_key(const u64* __restrict__ keys, u64 stride, u64 i, u64 (&k)[W]) {
+    if (stride == 0) {
+        if constexpr (W == 2) {
+            const v2u64 v = *(const v2u64*)(keys + 2 * i);
+            k[0] = v.x;
+            k[1] = v.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; j++) k[j] = keys[i * W + j];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < W; j++) k[j] = keys[(u64)j * stride + i];
+    }
+}
+
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWave = 64;
 
@@ -2139,8 +2158,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                 for (int j = 0; j < W; j++) qk[j] = 0;
                 if (act) {
                     const u64 gi = lo + wq[lane];
-#pragma unroll
-                    for (int j = 0; j < W; j++) qk[j] = a.keys[(u64)j * a.stride + gi];
+                    load_key<W>(a.keys, a.stride, gi, qk);
                 }
                 bool done = true, claimed = false, lclaim = false, full = false;
                 if (act) {
@@ -2186,8 +2204,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const u64 i = lo + (u64)u * kBucketBlock + tid;
-#pragma unroll
-                for (int j = 0; j < W; j++) nkey[u][j] = a.keys[(u64)j * a.stride + min(i, hi - 1)];
+                load_key<W>(a.keys, a.stride, min(i, hi - 1), nkey[u]);
             }
             for (u64 base = lo; base < hi; base += (u64)U * kBucketBlock) {
                 if (!last && __hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
@@ -2205,8 +2222,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const u64 i = nbase + (u64)u * kBucketBlock + tid;
-#pragma unroll
-                    for (int j = 0; j < W; j++) nkey[u][j] = a.keys[(u64)j * a.stride + min(i, hi - 1)];
+                    load_key<W>(a.keys, a.stride, min(i, hi - 1), nkey[u]);
                 }
                 // fast path, branch-light: a key already in its home group (W=1)
                 // or home slot (W>=2) is counted in place; every other wanted
@@ -2529,8 +2545,7 @@ __global__ __launch_bounds__(kSrBlock) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 const u32 p = min((u32)tid + (u32)i * kSrBlock, len - 1);
-#pragma unroll
-                for (int j = 0; j < W; j++) k[i][j] = a.keys[(u64)j * a.stride + lo + p];
+                load_key<W>(a.keys, a.stride, lo + p, k[i]);
             }
             u32 l2 = 0;
             while ((1u << l2) < e - s0) l2++;
