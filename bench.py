@@ -657,7 +657,7 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
         ]
         if pre_b:
             # P3b: word 0 read for the regional histogram + one scatter pass
-            specs.append(("P3b", f"rp_upsweep_k + rp_scatter_k<{W},false>", pre_ms, steps * pre_b,
+            specs.append(("P3b", f"rp_scatter_k<{W},false> + rp_upsweep_k", pre_ms, steps * pre_b,
                           keys_step * pre_b / nb, "keys", 8 + 16 * W))
         if st.get("sorted_run_batches", 0):
             # P5s: keys read once, records written (packed, or SoA + segment copy)
@@ -689,7 +689,8 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
         except (OSError, ValueError):
             continue
         if not varlen and traffic.get("reads_per_gpu") == args.reads and traffic.get("k") == k:
-            t_bytes = traffic.get("kernels", {}).get(d["kernel"].replace(" ", ""), {}).get("bytes_per_launch")
+            # (a composite entry is keyed by its first kernel, the one the PMC passes measured)
+            t_bytes = traffic.get("kernels", {}).get(d["kernel"].split(" ")[0], {}).get("bytes_per_launch")
             break
     b_path = nbytes / windows_step + 8 * W + 8
     path_achieved = b_path * windows_step / (dev_el / steps) / 1e9
