@@ -523,9 +523,12 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="SURVEY §8d preset: 2 = k=31, 50M x 150 bp from a 250 Mbp genome (the metric's "
-                         "config); 5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality) with a "
+                         "config); 3 = cfg3's shard, 50M reads per GPU (400M over 8 GPUs, seed 3), read-shard "
+                         "(--exchange none at N > 1); 4 = cfg4's shard, 125M reads per GPU (1B over 8 GPUs, "
+                         "seed 4), key-space all-to-all at N > 1; "
+                         "5 = k=55, 20M x 150 bp iid reads (~1.9e9 distinct, high cardinality) with a "
                          "48 GiB working set: the keys outgrow one batch and are counted in key-range passes "
                          "(the spill -> sort -> merge path)")
     ap.add_argument("--value", default="device", choices=["device", "e2e"],
@@ -549,7 +552,7 @@ def parse_args(argv=None):
                                                     "whichever has the space)")
     ap.add_argument("--min-read-length", type=int, default=0,
                     help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
-    ap.add_argument("--exchange", default="alltoall", choices=["alltoall", "none"],
+    ap.add_argument("--exchange", default=None, choices=["alltoall", "none"],
                     help="N>1: key-space all-to-all (cfg4) or read-shard + merge on rank 0 (cfg3)")
     args = ap.parse_args(argv)
     if args.mode:
@@ -557,7 +560,10 @@ def parse_args(argv=None):
         if args.mode == "e2e" and args.e2e is None:
             args.e2e = True
     preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
+              3: dict(reads=50_000_000, k=31, genome=250_000_000, seed=3, mem=160 << 30, exchange="none"),
+              4: dict(reads=125_000_000, k=31, genome=250_000_000, seed=4, mem=160 << 30, exchange="alltoall"),
               5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=48 << 30)}[args.config]
+    preset.setdefault("exchange", "alltoall")
     for key, v in preset.items():
         if getattr(args, key) is None:
             setattr(args, key, v)
