@@ -68,6 +68,7 @@ struct kc_ctx {
     bool skm_used = false;         // a batch went through the skm engine since the last reset
     bool skm_force = false;        // KC_FLAG_ENGINE_SKM: no cardinality sample
     bool skm_checked = false;      // the skm cardinality sample has run since the last reset
+    bool skm_big_off = false;      // a large skm batch overflowed the spill buffer: safe batches only
     uint32_t engines_used = 0;     // kc_stats.engines_used
     bool skm_hc = false;           // high cardinality seen: the key-prefix engine counts
     bool hc_hint = false;          // most keys were distinct (the skm sample or the last key-prefix batch):
@@ -1182,6 +1183,14 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
     return KC_OK;
 }
 
+// Reads of nw windows one skm batch may take beyond key_cap windows (see
+// count_reads_skm): the record pool at nw / 4 records per read, while the
+// global table is empty; 0 when only safe batches apply
+static uint64_t skm_big_reads(const kc_ctx* c, uint64_t nw, uint64_t pool_cap) {
+    if (c->skm_big_off || c->stats_h[ST_CLAIMED] || c->table_dirty || getenv("KC_SKM_SAFE_BATCH")) return 0;
+    return pool_cap / std::max<uint64_t>(1, nw / 4);
+}
+
 // part_ms slots for this engine: [0] E + F, [1] F, [2] S1/S2 scatters,
 // [3] S1/S2 histograms + scans + P4, [4] P5.
 static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t* seq_off, uint64_t n_reads,
@@ -1196,14 +1205,27 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         const uint64_t v = strtoull(e, nullptr, 10);
         if (v > 0 && v < pool_cap) pool_cap = v;
     }
-    uint64_t max_reads = c->key_cap / nw;
-    if (max_reads == 0) return fail(c, KC_ERR_ARG, "gpu_memory_limit too small for one read's windows");
+    // P5's spills go to keys_b (key_cap keys), which a batch of at most
+    // key_cap windows can never overflow. While the global table is still
+    // empty a batch may be larger, up to what the record pool holds at nw / 4
+    // records per read (F's pool-overflow retry catches denser reads): fewer
+    // batches, so fewer runs for the finish to merge (SURVEY cfg4: 125M reads
+    // per GPU in one batch). A spill overflow in such a batch undoes it (table
+    // cleared, records and statistics restored) and retries it at the safe size.
+    const uint64_t safe_reads = c->key_cap / nw;
+    if (safe_reads == 0) return fail(c, KC_ERR_ARG, "gpu_memory_limit too small for one read's windows");
+    uint64_t max_reads = std::max(safe_reads, skm_big_reads(c, nw, pool_cap));
     kc_status s;
     uint64_t done = 0;
     float t = 0.f;
     while (done < n_reads) {
         uint64_t nr = n_reads - done;
         if (nr > max_reads) nr = max_reads;
+        if (nr > safe_reads && (c->stats_h[ST_CLAIMED] || c->table_dirty)) {
+            nr = safe_reads;  // the table holds keys already: only a safe batch
+            max_reads = safe_reads;
+        }
+        const bool big = nr > safe_reads;
         CountLaunch l;
         l.base = base;
         l.seq_off = seq_off;
@@ -1382,6 +1404,20 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             }
             c->skm_used = true;
             c->engines_used |= 1u;
+            if ((c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) && big) {
+                // undo the large batch and count its reads in safe batches
+                if (getenv("KC_DEBUG")) fprintf(stderr, "kc: skm batch of %llu reads overflowed the spill buffer: retried\n", (unsigned long long)nr);
+                HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->stats, saved.data(), ST_N * 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec_batch0, 8, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                memcpy(c->stats_h, saved.data(), ST_N * 8);
+                c->rec_n = rec_batch0;
+                c->part_keys -= np;
+                c->skm_big_off = true;
+                max_reads = safe_reads;
+                continue;
+            }
             if (c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) return fail(c, KC_ERR_INTERNAL, "spill buffer overflow");
             uint64_t n2 = c->stats_h[ST_SPILL2_FILL];
             if (n2) {
@@ -1562,8 +1598,14 @@ static kc_status pend_flush(kc_ctx* c) {
             const bool passes = c->hc_hint && c->part && (!c->skm || c->skm_hc) && c->rec_n == 0 &&
                                 c->batches == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES");
             if (!passes) {
-                for (uint64_t r0 = 0; r0 < n; r0 += b) {
-                    if ((s = count_reads(c, nullptr, nullptr, n - r0 < b ? n - r0 : b, L, (int64_t)r0))) return s;
+                // the skm engine may take a large batch (count_reads_skm)
+                uint64_t bs = b;
+                if (c->skm && !c->skm_hc && skm_geometry((int)L, (int)c->k).ok) {
+                    const uint64_t nw = (uint64_t)(L - c->k + 1);
+                    bs = std::max(b, skm_big_reads(c, nw, (uint64_t)c->W * c->key_cap / (c->W + 1)));
+                }
+                for (uint64_t r0 = 0; r0 < n; r0 += bs) {
+                    if ((s = count_reads(c, nullptr, nullptr, n - r0 < bs ? n - r0 : bs, L, (int64_t)r0))) return s;
                     if ((s = cut_run_if_full(c))) return s;
                 }
                 return KC_OK;
@@ -1976,6 +2018,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->p5_launches = 0;
     c->skm_used = false;
     c->skm_checked = false;
+    c->skm_big_off = false;
     c->skm_hc = false;
     c->hc_hint = false;
     c->engines_used = 0;

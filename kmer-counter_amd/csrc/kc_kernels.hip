@@ -4315,8 +4315,26 @@ __global__ __launch_bounds__(kBlock) void fq_validate_k(const u64* __restrict__ 
 // inval at the read's index. The sequence-length check of fq_validate_k is
 // done inline: no newline inside [s, s + L) and a newline at s + L, which is
 // exactly seq_end - seq_off == L. Nothing is written to seq_off / seq_end.
-constexpr int kFqHalf = 8192;
-constexpr int kFqStage = kFqHalf + 1024;
+#ifndef KC_FQ_HALF
+#define KC_FQ_HALF 8192  // bytes walked per step (a multiple of 4096 dividing kFqChunk)
+#endif
+#ifndef KC_FQ_XB
+#define KC_FQ_XB 16  // bytes per lane staged past the half (8 or 16)
+#endif
+#ifndef KC_FQ_BLOCK
+#define KC_FQ_BLOCK 256  // fq_encode_k workgroup (small groups: as many resident per CU as registers allow)
+#endif
+#ifndef KC_FQ_WPE
+#define KC_FQ_WPE 1  // fq_encode_k: minimum waves per SIMD asked of the register allocator (1 = no limit)
+#endif
+constexpr int kFqHalf = KC_FQ_HALF;
+constexpr int kFqRounds = kFqHalf / 4096;        // 64 lanes x 64 B per round
+constexpr int kFqParts = (int)(kFqChunk / kFqHalf);  // halves per fq_count chunk
+constexpr int kFqStage = kFqHalf + 64 * KC_FQ_XB;
+constexpr int kFqEncBlock = KC_FQ_BLOCK;
+constexpr int kFqEncWaves = kFqEncBlock / 64;
+static_assert(kFqRounds >= 1 && kFqHalf % 4096 == 0 && kFqChunk % kFqHalf == 0, "fq half size");
+static_assert(KC_FQ_XB == 8 || KC_FQ_XB == 16, "fq extra staging");
 
 int fq_encode_list_cap(int L) { return kFqHalf / (L + 6) + 2; }  // records with an L-base sequence are >= L + 6 bytes
 
@@ -4411,7 +4429,7 @@ __device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb
 // encode_reads_var_k). The list holds lcap records per half (records of >= 32
 // bytes); a denser half sets ERR_FQ_LIST.
 template <bool VAR>
-__global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
+__global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_FQ_WPE))) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                       const u64* __restrict__ line_base, u64 max_rec, int L, int G,
                                                       int lcap, u32* __restrict__ codes,
                                                       unsigned short* __restrict__ inval, u64* stats,
@@ -4440,24 +4458,29 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
     // the wave's halves in order: (c, 0), (c, 1), (c + stride, 0), ...; the
     // next half's text is loaded into registers while this one is walked and
     // encoded from LDS
-    const u64 cstride = (u64)gridDim.x * kFqWaves;
-    uint4 v[2][4], x;
+    const u64 cstride = (u64)gridDim.x * kFqEncWaves;
+    uint4 v[kFqRounds][4], x;
     auto issue = [&](u64 cc, int hh) {
         const uintptr_t hb = A + cc * kFqChunk + (u64)hh * kFqHalf;
         const long long hrel = (long long)(hb - (uintptr_t)base);
 #pragma unroll
-        for (int rd = 0; rd < 2; rd++)
+        for (int rd = 0; rd < kFqRounds; rd++)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int o = rd * 4096 + lane * 64 + i * 16;
                 const long long rel = hrel + o;
                 v[rd][i] = (rel + 16 <= 0 || rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
             }
-        const int o = kFqHalf + lane * 16;
+        const int o = kFqHalf + lane * KC_FQ_XB;
         const long long rel = hrel + o;
-        x = (rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+        if constexpr (KC_FQ_XB == 16) {
+            x = (rel >= (long long)n) ? make_uint4(0, 0, 0, 0) : fq_load16(hb + (u64)o);
+        } else {
+            const u64 y0 = rel >= (long long)n ? 0ull : *(const __attribute__((address_space(1))) u64*)(hb + (u64)o);
+            x = make_uint4((u32)y0, (u32)(y0 >> 32), 0u, 0u);  // bytes 8..15: no newline
+        }
     };
-    u64 c = (u64)blockIdx.x * kFqWaves + wave;
+    u64 c = (u64)blockIdx.x * kFqEncWaves + wave;
     int h = 0;
     u64 run = 0;
     if (c < nchunks) issue(c, 0);
@@ -4469,12 +4492,14 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
             // the next half: (c, 1) unless it starts past the block
             u64 cn = c;
             int hn = 1;
-            if (h == 1 || (long long)(hrel + kFqHalf) >= (long long)n) {
+            if (h == kFqParts - 1 || (long long)(hrel + kFqHalf) >= (long long)n) {
                 cn = c + cstride;
                 hn = 0;
+            } else {
+                hn = h + 1;
             }
 #pragma unroll
-            for (int rd = 0; rd < 2; rd++)
+            for (int rd = 0; rd < kFqRounds; rd++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     v4u w;
@@ -4484,17 +4509,19 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                     w.w = v[rd][i].w;
                     *(v4u*)(txt + rd * 4096 + lane * 64 + i * 16) = w;
                 }
-            {
+            if constexpr (KC_FQ_XB == 16) {
                 v4u w;
                 w.x = x.x;
                 w.y = x.y;
                 w.z = x.z;
                 w.w = x.w;
                 *(v4u*)(txt + kFqHalf + lane * 16) = w;
+            } else {
+                *(u64*)(txt + kFqHalf + lane * 8) = (u64)x.x | ((u64)x.y << 32);
             }
-            u64 mk[2];
+            u64 mk[kFqRounds];
 #pragma unroll
-            for (int rd = 0; rd < 2; rd++) {
+            for (int rd = 0; rd < kFqRounds; rd++) {
                 u64 m = 0;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
@@ -4513,7 +4540,7 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
             sync();
             const u64 rec0 = (run + 3) >> 2;  // first record whose header may end in this half
 #pragma unroll
-            for (int rd = 0; rd < 2; rd++) {
+            for (int rd = 0; rd < kFqRounds; rd++) {
                 u64 m = mk[rd];
                 const long long rel0 = hrel + rd * 4096 + lane * 64;
                 if (rel0 < 0) m = (rel0 <= -64) ? 0ull : (m & (~0ull << (u32)(-rel0)));
@@ -4578,7 +4605,7 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 int ex = -1;
                 if (bx) {
                     const int fl = __ffsll((long long)bx) - 1;
-                    ex = kFqHalf + 16 * fl + __builtin_ctz((u32)__builtin_amdgcn_readlane((int)mx, fl));
+                    ex = kFqHalf + KC_FQ_XB * fl + __builtin_ctz((u32)__builtin_amdgcn_readlane((int)mx, fl));
                 }
                 for (u32 li = (u32)lane; li < nrec; li += 64) {
                     const int s = (int)lst[li];
@@ -4607,6 +4634,7 @@ __global__ __launch_bounds__(kBlock) void fq_encode_k(const uint8_t* __restrict_
                 }
                 sync();
             }
+#pragma unroll 1
             for (u32 item = (u32)lane; item < nrec * (u32)G; item += 64) {
                 const u32 r = divg.div(item);
                 const int g = (int)(item - r * (u32)G);
@@ -4677,9 +4705,9 @@ hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* lin
     const int G = groups_per_read(L);
     const int lcap = fq_encode_list_cap(L);
     if ((u64)lcap * (u64)G >= 65536) return hipErrorInvalidValue;  // FastDivU range
-    const size_t lds = (size_t)kFqWaves * fq_encode_wave_lds(L);
-    int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
-    hipLaunchKernelGGL(fq_encode_k<false>, dim3(g ? g : 1), dim3(kBlock), lds, s, base, n, nch, line_base, max_rec,
+    const size_t lds = (size_t)kFqEncWaves * fq_encode_wave_lds(L);
+    int g = (int)hmin((nch + kFqEncWaves - 1) / kFqEncWaves, 16384);
+    hipLaunchKernelGGL(fq_encode_k<false>, dim3(g ? g : 1), dim3(kFqEncBlock), lds, s, base, n, nch, line_base, max_rec,
                        L, G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)nullptr, 0);
     return hipGetLastError();
 }
@@ -4700,9 +4728,9 @@ hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t*
     const int G = groups_per_read(L);
     const int lcap = kFqVarListCap;
     const size_t wl = (size_t)kFqStage + (((size_t)lcap * 4 + 15) & ~(size_t)15);
-    const size_t lds = (size_t)kFqWaves * wl;
-    int g = (int)hmin((nch + kFqWaves - 1) / kFqWaves, 16384);
-    hipLaunchKernelGGL(fq_encode_k<true>, dim3(g ? g : 1), dim3(kBlock), lds, s, base, n, nch, line_base, max_rec, L,
+    const size_t lds = (size_t)kFqEncWaves * wl;
+    int g = (int)hmin((nch + kFqEncWaves - 1) / kFqEncWaves, 16384);
+    hipLaunchKernelGGL(fq_encode_k<true>, dim3(g ? g : 1), dim3(kFqEncBlock), lds, s, base, n, nch, line_base, max_rec, L,
                        G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)rlen, k);
     return hipGetLastError();
 }

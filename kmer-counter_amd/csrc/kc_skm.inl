@@ -2619,6 +2619,14 @@ constexpr int kRecProbe = 8;  // P5a: groups probed per record
 #define KC_P5A_PD 4
 #endif
 constexpr int kRecPd = KC_P5A_PD;  // P5a: record batches in flight per wave
+#ifndef KC_P5A_BLOCK
+#define KC_P5A_BLOCK 1024  // P5a workgroup
+#endif
+#ifndef KC_P5A_LDS
+#define KC_P5A_LDS (160 * 1024)  // P5a LDS per workgroup (less: several workgroups per CU)
+#endif
+constexpr int kRecBlock = KC_P5A_BLOCK;
+constexpr int kRecWaves = kRecBlock / 64;
 
 struct RecDedupArgs {
     u64* recs;  // 2 x stride (SoA), grouped by bucket; distinct records written back in place
@@ -2641,14 +2649,14 @@ constexpr u32 kRecClaims = 4096;  // P5a: claimed entries listed for the write-b
 static size_t rec_dedup_lds(u32 ngrp) { return (size_t)ngrp * 40 + 64 * 4 + 16 + kRecClaims * 2; }
 
 u32 rec_dedup_groups() {
-    u32 g = (u32)((160 * 1024 - 64 * 4 - 16 - 64 - kRecClaims * 2) / 40);
+    u32 g = (u32)((KC_P5A_LDS - 64 * 4 - 16 - 64 - kRecClaims * 2) / 40);
     return g & ~15u;
 }
 
 // starts_r: a.starts as a read-only kernel argument, so a bucket's range is a
 // scalar load that never waits behind the record loads and write-back stores
 // in flight (in-order vmcnt)
-__global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, const u64* __restrict__ starts_r) {
+__global__ __launch_bounds__(kRecBlock) void count_rec_k(RecDedupArgs a, const u64* __restrict__ starts_r) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64* tab = (u64*)smem;                        // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
     u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);  // 2 ngrp
@@ -2658,7 +2666,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
     const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
     const u32 nent = 2 * a.ngrp;
     const u64 lt = lanemask_lt();
-    for (u32 i = tid; i < nent; i += kBucketBlock) {
+    for (u32 i = tid; i < nent; i += kRecBlock) {
         tab[2 * (size_t)i] = 0ull;
         tab[2 * (size_t)i + 1] = 0ull;
         cnt[i] = 0;
@@ -2676,7 +2684,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
     u64 n0[kRecPd], n1[kRecPd];
     auto share = [&](u32 bb, u64* wlo, u64* whi) {
         const u64 lo = starts_r[bb], hi = starts_r[bb + 1];
-        const u64 nr = hi - lo, per_w = (nr + kBucketWaves - 1) / kBucketWaves;
+        const u64 nr = hi - lo, per_w = (nr + kRecWaves - 1) / kRecWaves;
         *wlo = lo + min(nr, (u64)wave * per_w);
         *whi = lo + min(nr, (u64)(wave + 1) * per_w);
     };
@@ -2754,13 +2762,13 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
         if (lane == 0) misc[1 + wave] = claims;
         __syncthreads();
         u32 total = 0;
-        for (int w = 0; w < kBucketWaves; w++) total += misc[1 + w];
+        for (int w = 0; w < kRecWaves; w++) total += misc[1 + w];
         if (tid == 0) a.dlen[b] = raw ? kRawList : total;
         const u64 pos0 = starts_r[b];
         if (total <= kRecClaims) {
             // the claimed entries in claim order: distinct record i goes to
             // pos0 + i, its entry is cleared
-            for (u32 i = (u32)tid; i < total; i += kBucketBlock) {
+            for (u32 i = (u32)tid; i < total; i += kRecBlock) {
                 const u32 e = clist[i];
                 if (!raw) {
                     const u64 q = pos0 + i;
@@ -2780,7 +2788,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_rec_k(RecDedupArgs a, cons
             __syncthreads();
             continue;
         }
-        const u32 spw = (nent + kBucketWaves - 1) / kBucketWaves;
+        const u32 spw = (nent + kRecWaves - 1) / kRecWaves;
         const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
         for (u32 c0 = s0; c0 < s1; c0 += 64) {
             const u32 i = c0 + (u32)lane;
@@ -2844,7 +2852,8 @@ hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* sta
     a.cnt = cnt;
     a.dlen = dlen;
     const size_t lds = (rec_dedup_lds(a.ngrp) + 15) & ~(size_t)15;
-    hipLaunchKernelGGL(count_rec_k, dim3(grid), dim3(kBucketBlock), lds, s, a, a.starts);
+    // grid: n_cu workgroups per 160 KiB of LDS per workgroup
+    hipLaunchKernelGGL(count_rec_k, dim3(grid * ((160 * 1024) / KC_P5A_LDS)), dim3(kRecBlock), lds, s, a, a.starts);
     return hipGetLastError();
 }
 

@@ -51,6 +51,40 @@ def test_skm_many_batches(kca, orc, k):
     assert got == orc.count_fastq(fq, k)
 
 
+def test_skm_large_batch_one_run(kca, orc, monkeypatch):
+    """While the global table is empty a skm batch may hold more than key_cap
+    windows (up to the record pool at nw / 4 records per read): 30000 reads
+    with a 44 MB working set (~19900 reads per safe batch) are one batch, so
+    the finish sorts one run; same bytes as two safe batches and the oracle."""
+    fq = kca.synth_fastq(30000, 150, seed=41, genome_length=500_000, n_rate=0.001)
+    outs, sts = [], []
+    for safe in (False, True):
+        if safe:
+            monkeypatch.setenv("KC_SKM_SAFE_BATCH", "1")
+        with kca.Context(kmer_length=31, line_length=150, gpu_memory_limit=44_000_000, engine="skm") as ctx:
+            ctx.count_fastq(fq)
+            outs.append(ctx.records())
+            sts.append(ctx.stats())
+    assert sts[0]["batches"] == 1 and sts[1]["batches"] == 2
+    assert outs[0] == outs[1] == orc.count_fastq(fq, 31)
+
+
+def test_skm_large_batch_spill_overflow_retried(kca, orc, tmp_path, monkeypatch, capfd):
+    """A large first batch (twice the safe size) whose spills overflow the
+    spill buffer (1-slot LDS table, 1 MiB working set: nearly every key goes
+    to the small global table, then to the spill buffer) is undone - table
+    cleared, records and statistics restored - and counted in safe batches."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    fq = kca.synth_fastq(20000, 150, seed=35, genome_length=60_000)
+    with kca.Context(kmer_length=31, line_length=150, gpu_memory_limit=1 << 20, engine="skm", lds_slots=1) as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.output_bytes(str(tmp_path))
+        st = ctx.stats()
+    assert "overflowed the spill buffer: retried" in capfd.readouterr().err
+    assert st["spilled_kmers"] > 0
+    assert got == orc.count_fastq(fq, 31)
+
+
 @pytest.mark.parametrize("cap,k", [(20000, 31), (20001, 31), (20007, 55)])
 def test_skm_pool_overflow_retry(kca, orc, monkeypatch, cap, k):
     """A pool smaller than one batch's records: the batch is undone and

@@ -7,7 +7,7 @@
 # usage: tools/build_variant.sh <name> "<hipcc flags>"
 set -e
 R=/root/repo/kmer-counter_amd
-make -C $R -s ARCH=gfx950 >/dev/null
+[ -n "$NO_MAKE" ] || make -C $R -s ARCH=gfx950 >/dev/null
 mkdir -p $R/variants/$1
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$R/../include -I$R/csrc -Wno-unused-function \
   -DKC_EXPERIMENTS $2 -c $R/csrc/kc_kernels.hip -o $R/variants/$1/kc_kernels.o

@@ -12,7 +12,7 @@ for v in ${LIBS:-main rpdyn}; do
     rc=$?; [ $rc -eq 0 ] || { echo "$v cfg$c rc=$rc"; tail -5 $O/$v.$c.$rep.err; exit $rc; }
     python3 -c "
 import json; d=json.loads(open('$O/$v.$c.$rep.json').read().splitlines()[-1])
-b=d['device_resident']['breakdown_ms_per_step']; print('$v cfg$c', round(d['ms_per_step'],2), b['partition_passes'], 'p3b', b['p3b_presplit (in partition_passes[2])'], 'fin', round(b['finish'],2))"
+b=d['device_resident']['breakdown_ms_per_step']; print('$v cfg$c', round(d['ms_per_step'],2), 'fq', round(b['fastq_index'],2), b['partition_passes'], 'p3b', b['p3b_presplit (in partition_passes[2])'], 'fin', round(b['finish'],2))"
   done
 done
 done
