@@ -1431,6 +1431,9 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         }
         c->batches++;
         done += nr;
+        // a call may span several batches (large batches, or safe ones once
+        // the table holds keys): runs are cut between them as between calls
+        if (done < n_reads && (s = cut_run_if_full(c))) return s;
     }
     c->st.valid_kmers = c->stats_h[ST_VALID];
     c->st.spilled_kmers = c->spilled_flushed + c->stats_h[ST_SPILL_FILL];
