@@ -1,7 +1,7 @@
 // rp_bench: the radix scatter (rp_scatter_k, S / P3 / P3b) alone on random
 // records, timed with HIP events; run against variant builds of
 // libkc_hip.so (tools/build_variant.sh, KC_RP_ABL ablations) through
-// LD_LIBRARY_PATH. Usage: rp_bench [n_records] [NW] [reps]
+// LD_LIBRARY_PATH. Usage: rp_bench [n_records] [NW] [reps] [emit] [dshift] [layout]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -42,8 +42,19 @@ int main(int argc, char** argv) {
     const uint64_t nt = (n + tile - 1) / tile;
     uint64_t *a, *b, *rt, *pos, *tmp;
     uint8_t* digs;
-    CK(hipMalloc(&a, n * 8 * NW));
-    CK(hipMalloc(&b, n * 8 * NW));
+    // layout -1: two allocations; -2: two physically contiguous ones; >= 0:
+    // one, b at a + its size + layout bytes
+    const long long layout = argc > 6 ? atoll(argv[6]) : -1;
+    if (layout == -2) {  // physically contiguous allocations
+        CK(hipExtMallocWithFlags((void**)&a, n * 8 * NW, hipDeviceMallocContiguous));
+        CK(hipExtMallocWithFlags((void**)&b, n * 8 * NW, hipDeviceMallocContiguous));
+    } else if (layout < 0) {
+        CK(hipMalloc(&a, n * 8 * NW));
+        CK(hipMalloc(&b, n * 8 * NW));
+    } else {
+        CK(hipMalloc(&a, 2 * n * 8 * NW + (uint64_t)layout + 256));
+        b = (uint64_t*)((char*)a + ((n * 8 * NW + (uint64_t)layout + 255) & ~255ull));
+    }
     CK(hipMalloc(&digs, n + 64));
     CK(hipMalloc(&rt, 64));
     CK(hipMalloc(&pos, nt * 256 * 8));
