@@ -42,10 +42,15 @@ int main(int argc, char** argv) {
     const uint64_t nt = (n + tile - 1) / tile;
     uint64_t *a, *b, *rt, *pos, *tmp;
     uint8_t* digs;
-    // layout -1: two allocations; -2: two physically contiguous ones; >= 0:
-    // one, b at a + its size + layout bytes
+    // layout -1: two allocations; -2: two physically contiguous ones; -3: two
+    // of three regions each, six (input, output) region pairs timed in one
+    // process; >= 0: one, b at a + its size + layout bytes
     const long long layout = argc > 6 ? atoll(argv[6]) : -1;
-    if (layout == -2) {  // physically contiguous allocations
+    const int nreg = layout == -3 ? 3 : 1;  // -3: three regions per buffer, pairs timed in one process
+    if (layout == -3) {
+        CK(hipMalloc(&a, 3 * n * 8 * NW));
+        CK(hipMalloc(&b, 3 * n * 8 * NW));
+    } else if (layout == -2) {  // physically contiguous allocations
         CK(hipExtMallocWithFlags((void**)&a, n * 8 * NW, hipDeviceMallocContiguous));
         CK(hipExtMallocWithFlags((void**)&b, n * 8 * NW, hipDeviceMallocContiguous));
     } else if (layout < 0) {
@@ -63,16 +68,21 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(rt, h, 32, hipMemcpyHostToDevice));
     hipStream_t s;
     CK(hipStreamCreate(&s));
-    hipLaunchKernelGGL(fill_k, dim3(8192), dim3(256), 0, s, a, n, NW, 12345ull);
+    for (int g = 0; g < nreg; g++)
+        hipLaunchKernelGGL(fill_k, dim3(8192), dim3(256), 0, s, a + (uint64_t)g * n * NW, n, NW, 12345ull);
     CK(hipStreamSynchronize(s));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(kc::launch_rp_hist(nullptr, a, dshift, rt, rt + 2, 1, nt, (uint32_t)tile, pos, tmp, 2 * ncu, s));
+    const int pairs[6][2] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {2, 2}, {2, 0}};
+    for (int pi = 0; pi < (nreg > 1 ? 6 : 1); pi++) {
+    uint64_t* ai = a + (uint64_t)pairs[pi][0] * n * NW;
+    uint64_t* bi = b + (uint64_t)pairs[pi][1] * n * NW;
     float best = 1e30f, tot = 0.f;
     for (int r = 0; r < reps + 1; r++) {
         CK(hipEventRecord(e0, s));
-        CK(kc::launch_rp_scatter(NW, false, a, n, b, n, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift, with_emit ? digs : nullptr, 56,
+        CK(kc::launch_rp_scatter(NW, false, ai, n, bi, n, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift, with_emit ? digs : nullptr, 56,
                                  2 * ncu, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
@@ -84,8 +94,9 @@ int main(int argc, char** argv) {
         }
     }
     const double bytes = (double)n * (16.0 * NW + (with_emit ? 1.0 : 0.0));
-    printf("{\"dshift\": %d, \"n\": %llu, \"NW\": %d, \"emit\": %d, \"tile\": %llu, \"avg_ms\": %.3f, \"best_ms\": %.3f, \"GBps_avg\": %.1f}\n",
-           dshift, (unsigned long long)n, NW, with_emit ? 1 : 0, (unsigned long long)tile, tot / reps, best,
+    printf("{\"pair\": [%d, %d], \"dshift\": %d, \"n\": %llu, \"NW\": %d, \"emit\": %d, \"tile\": %llu, \"avg_ms\": %.3f, \"best_ms\": %.3f, \"GBps_avg\": %.1f}\n",
+           pairs[pi][0], pairs[pi][1], dshift, (unsigned long long)n, NW, with_emit ? 1 : 0, (unsigned long long)tile, tot / reps, best,
            bytes / (tot / reps / 1e3) / 1e9);
+    }
     return 0;
 }
