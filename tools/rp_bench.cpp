@@ -76,7 +76,9 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     CK(kc::launch_rp_hist(nullptr, a, dshift, rt, rt + 2, 1, nt, (uint32_t)tile, pos, tmp, 2 * ncu, s));
     const int pairs[6][2] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {2, 2}, {2, 0}};
-    for (int pi = 0; pi < (nreg > 1 ? 6 : 1); pi++) {
+    const int sweeps = getenv("RP_SWEEPS") ? atoi(getenv("RP_SWEEPS")) : 1;  // repeat the pairs: stable?
+    for (int pk = 0; pk < (nreg > 1 ? 6 * sweeps : 1); pk++) {
+    const int pi = pk % 6;
     uint64_t* ai = a + (uint64_t)pairs[pi][0] * n * NW;
     uint64_t* bi = b + (uint64_t)pairs[pi][1] * n * NW;
     float best = 1e30f, tot = 0.f;
