@@ -646,6 +646,61 @@ static void* o_worker(void* arg) {
 int64_t oracle_refcpu_run(const char* fastq, int64_t n_bytes, int64_t k, int64_t gpu_memory_limit, int threads,
                           unsigned char** out, uint64_t* windows);
 
+/* Sort of the dumped (key words, u64 count) entries by key: one split by the
+ * top 8 bits of word 0 into 256 groups, each group qsorted by one of `threads`
+ * workers (the order is the same as one qsort of the whole array; keys are
+ * distinct here). Replaces *buf with the sorted copy. */
+typedef struct o_psort {
+    unsigned char* base;
+    const int64_t* start; /* 257 group bounds */
+    size_t ent;
+    int next; /* next group to take (under mu) */
+    pthread_mutex_t mu;
+} o_psort;
+
+static void* o_psort_worker(void* arg) {
+    o_psort* p = (o_psort*)arg;
+    for (;;) {
+        pthread_mutex_lock(&p->mu);
+        int g = p->next++;
+        pthread_mutex_unlock(&p->mu);
+        if (g >= 256) break;
+        int64_t n = p->start[g + 1] - p->start[g];
+        if (n > 1) qsort(p->base + (size_t)p->start[g] * p->ent, (size_t)n, p->ent, o_qcmp);
+    }
+    return NULL;
+}
+
+static void o_par_sort(unsigned char** buf, int64_t m, int W, int threads) {
+    size_t ent = (size_t)W * 8 + 8;
+    int64_t start[257] = {0}, pos[256];
+    for (int64_t i = 0; i < m; i++) start[1 + (o_ld64(*buf + (size_t)i * ent) >> 56)]++;
+    for (int g = 0; g < 256; g++) start[g + 1] += start[g];
+    memcpy(pos, start, sizeof(pos));
+    unsigned char* dst = (unsigned char*)malloc(ent * (size_t)(m ? m : 1));
+    for (int64_t i = 0; i < m; i++) {
+        const unsigned char* e = *buf + (size_t)i * ent;
+        memcpy(dst + (size_t)pos[o_ld64(e) >> 56]++ * ent, e, ent);
+    }
+    free(*buf);
+    *buf = dst;
+    pthread_mutex_lock(&g_sort_mu);
+    g_sort_w = W;
+    o_psort p;
+    p.base = dst;
+    p.start = start;
+    p.ent = ent;
+    p.next = 0;
+    pthread_mutex_init(&p.mu, NULL);
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, o_psort_worker, &p);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    free(th);
+    pthread_mutex_destroy(&p.mu);
+    pthread_mutex_unlock(&g_sort_mu);
+}
+
 /* Runs the whole reference count path over one in-memory FASTQ file with
  * `threads` workers. Writes the sorted SortedKMerFile bytes into *out (malloc;
  * caller frees with oracle_free) and returns the record count; *windows gets
@@ -745,10 +800,7 @@ int64_t oracle_refcpu_run(const char* fastq, int64_t n_bytes, int64_t k, int64_t
         pthread_mutex_destroy(&s->mu);
     }
     free(t);
-    pthread_mutex_lock(&g_sort_mu);
-    g_sort_w = W;
-    qsort(tmp, (size_t)m, ent, o_qcmp);
-    pthread_mutex_unlock(&g_sort_mu);
+    o_par_sort(&tmp, m, W, threads);
     unsigned char* res = (unsigned char*)malloc((size_t)(m * rs) + 1);
     for (int64_t i = 0; i < m; i++) {
         memcpy(res + i * rs, tmp + i * ent, (size_t)W * 8);
@@ -794,4 +846,203 @@ int64_t oracle_count_fastq(const char* fastq, int64_t n_bytes, int64_t k, int64_
     int64_t m = oracle_acc_finish(a, out);
     oracle_acc_free(a);
     return m;
+}
+
+/* ------------------------------------------------------------------------- */
+/* window checksums: a parity property for inputs too large to recount       */
+/* ------------------------------------------------------------------------- */
+/*
+ * For a full-size run the output is a multiset {key: count}. Two 64-bit hash
+ * functions h1, h2 (splitmix/murmur finalizers with different seeds) give
+ *     sum over every valid window w of h(key(w))   (mod 2^64)
+ *  == sum over every output record r of count(r) * h(key(r))   (mod 2^64)
+ * for a correct output; a count moved between keys, a wrong key, a lost or an
+ * extra window changes both sums unless the difference happens to cancel in
+ * both hashes (~2^-128 for errors independent of the hashes). Together with
+ * strictly ascending keys, the count sum and the key-0 rule below this pins the
+ * output at any size in seconds on the host's cores.
+ *
+ * Windows follow the spec form (o_spec_key, SURVEY Appendix A, which restates
+ * GPUHandler.cu:129-233): each read of well-formed 4-line FASTQ at its own
+ * length; a window holding a byte outside ACGT is invalid (the zeroed hole
+ * record of extractKMers: it only makes key 0^W present, count 0).
+ */
+
+static uint64_t o_ck_hash(const uint64_t* key, int W, uint64_t seed) {
+    uint64_t h = seed;
+    for (int j = 0; j < W; j++) h = o_mix64(h ^ key[j]) + 0x9e3779b97f4a7c15ull * (uint64_t)(j + 1);
+    return o_mix64(h ^ (uint64_t)W);
+}
+
+#define O_CK_SEED1 0x243f6a8885a308d3ull
+#define O_CK_SEED2 0x13198a2e03707344ull
+
+typedef struct o_ck_job {
+    const unsigned char* p;
+    int64_t n, lo, hi; /* records starting in [lo, hi) */
+    int64_t k;
+    uint64_t s1, s2, windows, valid, hole, reads;
+} o_ck_job;
+
+/* the first record start at or after `from`: a line starting with '@' whose
+ * next-but-one line starts with '+' (a quality line starting with '@' is
+ * followed by a header and a sequence, never by a '+' two lines on) */
+static int64_t o_ck_record_start(const unsigned char* p, int64_t n, int64_t from) {
+    int64_t i = from;
+    if (i > 0 && i < n && p[i - 1] != '\n') {
+        const unsigned char* nl = (const unsigned char*)memchr(p + i, '\n', (size_t)(n - i));
+        if (!nl) return n;
+        i = (nl - p) + 1;
+    }
+    while (i < n) {
+        if (p[i] == '@') {
+            const unsigned char* a = (const unsigned char*)memchr(p + i, '\n', (size_t)(n - i));
+            const unsigned char* b = a ? (const unsigned char*)memchr(a + 1, '\n', (size_t)(n - (a + 1 - p))) : NULL;
+            if (b && b + 1 < p + n && b[1] == '+') return i;
+            if (!a) return n;
+        }
+        const unsigned char* nl = (const unsigned char*)memchr(p + i, '\n', (size_t)(n - i));
+        if (!nl) return n;
+        i = (nl - p) + 1;
+    }
+    return n;
+}
+
+static void* o_ck_worker(void* arg) {
+    o_ck_job* j = (o_ck_job*)arg;
+    const unsigned char* p = j->p;
+    int64_t k = j->k, i = j->lo;
+    int W = o_words(k);
+    uint64_t mask_last = o_masks_last_word(k) ? (~0ull << (64 - 2 * (k % 32))) : ~0ull;
+    uint64_t* w = NULL;
+    int64_t wcap = 0;
+    uint64_t key[O_MAXW];
+    while (i < j->hi) {
+        const unsigned char* a = (const unsigned char*)memchr(p + i, '\n', (size_t)(j->n - i));
+        if (!a) break;
+        const unsigned char* s = a + 1;
+        const unsigned char* e = (const unsigned char*)memchr(s, '\n', (size_t)(j->n - (s - p)));
+        if (!e) break;
+        int64_t L = e - s;
+        /* skip the '+' line and the quality line */
+        const unsigned char* q = (const unsigned char*)memchr(e + 1, '\n', (size_t)(j->n - (e + 1 - p)));
+        const unsigned char* r = q ? (const unsigned char*)memchr(q + 1, '\n', (size_t)(j->n - (q + 1 - p))) : NULL;
+        i = r ? (r - p) + 1 : j->n;
+        j->reads++;
+        if (L < k) continue;
+        if (L + 32 * W + 1 > wcap) {
+            wcap = L + 32 * W + 64;
+            free(w);
+            w = (uint64_t*)calloc((size_t)wcap, 8);
+        }
+        /* w[x] = the 32 bases from x (MSB first), 0 past the read end */
+        for (int64_t x = L; x < L + 32 * W + 1; x++) w[x] = 0;
+        for (int64_t x = L - 1; x >= 0; x--) w[x] = ((uint64_t)o_code(s[x]) << 62) | (w[x + 1] >> 2);
+        int64_t last_bad = -1;
+        for (int64_t x = 0; x < k - 1; x++)
+            if (o_bad(s[x])) last_bad = x;
+        for (int64_t pp = 0; pp + k <= L; pp++) {
+            if (o_bad(s[pp + k - 1])) last_bad = pp + k - 1;
+            j->windows++;
+            if (last_bad >= pp) {
+                j->hole = 1;
+                continue;
+            }
+            j->valid++;
+            for (int t = 0; t < W; t++) key[t] = w[pp + 32 * t];
+            key[W - 1] &= mask_last;
+            j->s1 += o_ck_hash(key, W, O_CK_SEED1);
+            j->s2 += o_ck_hash(key, W, O_CK_SEED2);
+        }
+    }
+    free(w);
+    return NULL;
+}
+
+/* out[0..5] = sum h1, sum h2, windows, valid windows, any invalid window (0/1),
+ * reads. Returns 0, or -1 on bad arguments. */
+int oracle_window_checksum(const char* fastq, int64_t n_bytes, int64_t k, int threads, uint64_t* out) {
+    if (k < 1 || k > 32 * O_MAXW || threads < 1) return -1;
+    const unsigned char* p = (const unsigned char*)fastq;
+    o_ck_job* jobs = (o_ck_job*)calloc((size_t)threads, sizeof(o_ck_job));
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    int64_t prev = o_ck_record_start(p, n_bytes, 0);
+    for (int t = 0; t < threads; t++) {
+        int64_t hi = t + 1 == threads ? n_bytes : o_ck_record_start(p, n_bytes, n_bytes / threads * (t + 1));
+        if (hi < prev) hi = prev;
+        jobs[t].p = p;
+        jobs[t].n = n_bytes;
+        jobs[t].lo = prev;
+        jobs[t].hi = hi;
+        jobs[t].k = k;
+        prev = hi;
+        pthread_create(&th[t], NULL, o_ck_worker, &jobs[t]);
+    }
+    memset(out, 0, 6 * sizeof(uint64_t));
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        out[0] += jobs[t].s1;
+        out[1] += jobs[t].s2;
+        out[2] += jobs[t].windows;
+        out[3] += jobs[t].valid;
+        out[4] |= jobs[t].hole;
+        out[5] += jobs[t].reads;
+    }
+    free(th);
+    free(jobs);
+    return 0;
+}
+
+typedef struct o_rck_job {
+    const unsigned char* recs;
+    int64_t lo, hi;
+    int W;
+    uint64_t s1, s2, cnt, unordered;
+} o_rck_job;
+
+static void* o_rck_worker(void* arg) {
+    o_rck_job* j = (o_rck_job*)arg;
+    int W = j->W, rs = 8 * W + 4;
+    uint64_t key[O_MAXW], prev[O_MAXW];
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        const unsigned char* r = j->recs + (size_t)i * rs;
+        memcpy(key, r, (size_t)W * 8);
+        uint32_t c;
+        memcpy(&c, r + 8 * W, 4);
+        if (i > 0) {
+            memcpy(prev, r - rs, (size_t)W * 8);
+            if (o_cmp_words(prev, key, W) >= 0) j->unordered++;
+        }
+        j->s1 += (uint64_t)c * o_ck_hash(key, W, O_CK_SEED1);
+        j->s2 += (uint64_t)c * o_ck_hash(key, W, O_CK_SEED2);
+        j->cnt += c;
+    }
+    return NULL;
+}
+
+/* Over n SortedKMerFile records (W LE u64 words + LE u32 count):
+ * out[0..3] = sum count*h1, sum count*h2, sum count, adjacent pairs not
+ * strictly ascending. */
+int oracle_records_checksum(const unsigned char* recs, int64_t n, int64_t k, int threads, uint64_t* out) {
+    if (k < 1 || k > 32 * O_MAXW || threads < 1 || n < 0) return -1;
+    o_rck_job* jobs = (o_rck_job*)calloc((size_t)threads, sizeof(o_rck_job));
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    for (int t = 0; t < threads; t++) {
+        jobs[t].recs = recs;
+        jobs[t].lo = n / threads * t;
+        jobs[t].hi = t + 1 == threads ? n : n / threads * (t + 1);
+        jobs[t].W = o_words(k);
+        pthread_create(&th[t], NULL, o_rck_worker, &jobs[t]);
+    }
+    memset(out, 0, 4 * sizeof(uint64_t));
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        out[0] += jobs[t].s1;
+        out[1] += jobs[t].s2;
+        out[2] += jobs[t].cnt;
+        out[3] += jobs[t].unordered;
+    }
+    free(th);
+    free(jobs);
+    return 0;
 }

@@ -31,9 +31,9 @@ def lib():
         L.oracle_chunk_size.restype = i64
         L.oracle_count_fastq.argtypes = [ctypes.c_char_p, i64, i64, i64, ctypes.c_int, P(vp)]
         L.oracle_count_fastq.restype = i64
-        L.oracle_refcpu_count.argtypes = [ctypes.c_char_p, i64, i64, i64, ctypes.c_int, P(vp), P(u64)]
+        L.oracle_refcpu_count.argtypes = [vp, i64, i64, i64, ctypes.c_int, P(vp), P(u64)]
         L.oracle_refcpu_count.restype = i64
-        L.oracle_refcpu_run.argtypes = [ctypes.c_char_p, i64, i64, i64, ctypes.c_int, vp, P(u64)]
+        L.oracle_refcpu_run.argtypes = [vp, i64, i64, i64, ctypes.c_int, vp, P(u64)]
         L.oracle_refcpu_run.restype = i64
         L.oracle_free.argtypes = [vp]
         L.oracle_acc_new.argtypes = [i64]
@@ -52,6 +52,10 @@ def lib():
         L.oracle_reader_line_length.argtypes = [vp]
         L.oracle_reader_line_length.restype = i64
         L.oracle_reader_free.argtypes = [vp]
+        L.oracle_window_checksum.argtypes = [vp, i64, i64, ctypes.c_int, P(u64)]
+        L.oracle_window_checksum.restype = ctypes.c_int
+        L.oracle_records_checksum.argtypes = [vp, i64, i64, ctypes.c_int, P(u64)]
+        L.oracle_records_checksum.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -123,11 +127,15 @@ def count_fastq_varlen(data: bytes, k: int, mode: str = "spec") -> bytes:
 
 def refcpu(data: bytes, k: int, gpu_memory_limit: int = 100000000, threads: int = 1):
     """The reference pipeline on the CPU (chunker + ref-structured encode/extract
-    + adjacent reduce + sharded-lock hash + sort). Returns (bytes, windows)."""
+    + adjacent reduce + sharded-lock hash + sort). `data`: bytes, a numpy uint8
+    array or (address, nbytes). Returns (bytes, windows)."""
     L = lib()
     out = ctypes.c_void_p()
     win = ctypes.c_uint64()
-    n = L.oracle_refcpu_count(data, len(data), k, gpu_memory_limit, threads, ctypes.byref(out), ctypes.byref(win))
+    keep = data
+    addr, nb = _addr(data)
+    n = L.oracle_refcpu_count(addr, nb, k, gpu_memory_limit, threads, ctypes.byref(out), ctypes.byref(win))
+    del keep
     if n < 0:
         raise ValueError("bad oracle arguments")
     res = _take(out, n * rs_of(k)) if n else b""
@@ -140,10 +148,50 @@ def refcpu_count_only(data: bytes, k: int, gpu_memory_limit: int = 100000000, th
     (distinct keys, windows)."""
     L = lib()
     win = ctypes.c_uint64()
-    n = L.oracle_refcpu_run(data, len(data), k, gpu_memory_limit, threads, None, ctypes.byref(win))
+    keep = data
+    addr, nb = _addr(data)
+    n = L.oracle_refcpu_run(addr, nb, k, gpu_memory_limit, threads, None, ctypes.byref(win))
+    del keep
     if n < 0:
         raise ValueError("bad oracle arguments")
     return n, win.value
+
+
+def _addr(buf):
+    """(address, nbytes) of bytes / a numpy array / (address, nbytes)."""
+    if isinstance(buf, tuple):
+        return buf
+    if isinstance(buf, bytes):
+        return ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value, len(buf)
+    return buf.ctypes.data, buf.nbytes
+
+
+def window_checksum(fastq, k: int, threads: int = 1) -> dict:
+    """Size-independent parity property (kc_oracle.c, "window checksums"):
+    over every valid window of well-formed 4-line FASTQ (spec form, each read at
+    its own length) the sums of two 64-bit key hashes, plus windows, valid
+    windows, whether any window was invalid (key 0^W present) and reads.
+    `fastq`: bytes, a numpy uint8 array or (address, nbytes)."""
+    keep = fastq  # the buffer must outlive the call
+    addr, n = _addr(fastq)
+    out = (ctypes.c_uint64 * 6)()
+    if lib().oracle_window_checksum(addr, n, k, threads, out) != 0:
+        raise ValueError("bad oracle arguments")
+    del keep
+    return {"h1": out[0], "h2": out[1], "windows": out[2], "valid": out[3], "hole": bool(out[4]), "reads": out[5]}
+
+
+def records_checksum(recs, k: int, threads: int = 1) -> dict:
+    """The matching sums over SortedKMerFile records: sum count*h1, sum
+    count*h2, sum count, and the adjacent pairs that are not strictly
+    ascending. `recs`: bytes, a numpy uint8 array or (address, nbytes)."""
+    keep = recs
+    addr, n = _addr(recs)
+    out = (ctypes.c_uint64 * 4)()
+    if lib().oracle_records_checksum(addr, n // rs_of(k), k, threads, out) != 0:
+        raise ValueError("bad oracle arguments")
+    del keep
+    return {"h1": out[0], "h2": out[1], "count": out[2], "unordered": out[3]}
 
 
 def chunks_of(data: bytes, chunk: int):

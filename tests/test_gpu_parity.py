@@ -251,19 +251,25 @@ def test_cli_spill_and_merge_knobs(kca, orc, tmp_path):
 
 
 @pytest.mark.slow
-def test_config2_full_size_properties(kca):
-    """BASELINE config 2 (k=31, 50M x 150 bp from a 250 Mbp genome): properties
-    that do not need a full CPU recount — strictly ascending keys, counts sum
-    to the valid windows, and every k-mer of sampled reads is present with a
-    count no lower than its multiplicity in the sample."""
+def test_config2_full_size_properties(kca, orc):
+    """BASELINE config 2 (k=31, 50M x 150 bp from a 250 Mbp genome) with a
+    24 GiB working set (several batches whose runs are merged): the window
+    checksums of the whole input (CPU) equal the records' (a count moved
+    between keys fails it), strictly ascending keys, counts sum to the valid
+    windows, and every k-mer of sampled reads is present with a count no lower
+    than its multiplicity in the sample."""
     n, L, k = 50_000_000, 150, 31
     with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=24 << 30) as ctx:
         ptr, nb = ctx.synth_device(n, L, 2, 250_000_000, 0.0, 0)
+        fq = _host_fastq(ctx, ptr, nb)
         assert ctx.count_fastq_device(ptr, nb) == n
         ctx.free_device(ptr)
-        recs = np.frombuffer(ctx.records(), dtype=[("k", "<u8"), ("c", "<u4")])
+        raw = _host_records(ctx)
         st = ctx.stats()
-    assert st["spilled_kmers"] == 0
+    assert st["spilled_kmers"] == 0 and st["batches"] >= 2
+    _assert_window_checksum(orc, fq, raw, k, _usable_cpus())
+    del fq
+    recs = raw.view(dtype=[("k", "<u8"), ("c", "<u4")])
     assert np.all(recs["k"][1:] > recs["k"][:-1])
     assert int(recs["c"].astype(np.uint64).sum()) == n * (L - k + 1) == st["valid_kmers"]
     sample = kca.synth_fastq(2000, L, 2, genome_length=250_000_000, first_read=n - 2000).decode()
@@ -313,6 +319,100 @@ def test_config2_prefix_bit_exact_through_file_path(kca, orc, tmp_path):
     assert windows == n * (L - k + 1) == st["windows"]
     assert st["spilled_kmers"] == 0
     assert got == hashlib.sha256(want).hexdigest()
+
+
+def _host_records(ctx):
+    """The finished run's SortedKMerFile records as a host numpy uint8 array."""
+    import torch
+
+    n = ctx.finish()
+    t = torch.empty(max(1, n * ctx.rs), dtype=torch.uint8)
+    ctx.export_records(t)
+    return t.numpy()[: n * ctx.rs]
+
+
+def _host_fastq(ctx, ptr, nb):
+    host = np.empty(nb, dtype=np.uint8)
+    ctx.copy_to_host_addr(host.ctypes.data, ptr, nb)
+    return host
+
+
+def _assert_window_checksum(orc, fq, recs, k, threads):
+    """Full-size parity property (kc_oracle.c window checksums): the sums of two
+    64-bit key hashes over every valid window of the FASTQ (CPU, spec form)
+    equal the count-weighted sums over the GPU's records; keys strictly
+    ascending; key 0^W present when a window was invalid."""
+    a = orc.window_checksum(fq, k, threads=threads)
+    b = orc.records_checksum(recs, k, threads=threads)
+    assert b["unordered"] == 0
+    assert b["count"] == a["valid"]
+    assert (b["h1"], b["h2"]) == (a["h1"], a["h2"])
+    if a["hole"]:
+        assert not recs[: 8 * ((k + 31) // 32)].any()
+    return a
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_config2_benched_step_bit_exact(kca, orc):
+    """The configuration bench.py times, byte-compared at full size: BASELINE
+    config 2 (k=31, 50M x 150 bp from the 250 Mbp genome, seed 2) with the
+    bench's 160 GiB working set, through exactly bench.py's dev_step
+    (kc_reset, kc_count_fastq_device, kc_finish): all 50M reads are one
+    super-k-mer batch (5.9e8 records, ~9K per bucket against P5a's LDS table,
+    so its raw-bucket and sub-range fallbacks run at scale). The records'
+    sha256 equals that of the reference-structured CPU pipeline (oracle refcpu:
+    readData chunks at gpuMemoryLimit=1e8, bitEncode / extractKMers /
+    reduceKMers restated, hash aggregation, sorted; GPUHandler.cu:129-233,
+    KMerCounter.cpp:61-82,91-106) on every usable core; the window checksum
+    is checked first (seconds) so a mismatch is reported early."""
+    import hashlib
+
+    n, L, k = 50_000_000, 150, 31
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=160 << 30) as ctx:
+        ptr, nb = ctx.synth_device(n, L, 2, 250_000_000, 0.0, 0)
+        fq = _host_fastq(ctx, ptr, nb)
+        ctx.reset()
+        assert ctx.count_fastq_device(ptr, nb) == n
+        ctx.finish()
+        st = ctx.stats()
+        ctx.free_device(ptr)
+        recs = _host_records(ctx)
+    assert st["batches"] == 1 and st["engines_used"] == 1 and st["spilled_kmers"] == 0
+    threads = _usable_cpus()
+    a = _assert_window_checksum(orc, fq, recs, k, threads)
+    assert a["windows"] == n * (L - k + 1) == st["windows"]
+    got = hashlib.sha256(recs).hexdigest()
+    del recs
+    want, windows = orc.refcpu(fq, k, threads=threads)
+    assert windows == n * (L - k + 1)
+    assert got == hashlib.sha256(want).hexdigest()
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_config4_shard_one_batch_checksum(kca, orc):
+    """BASELINE config 4's per-GPU shard as bench.py --config 4 counts it:
+    k=31, 125M x 150 bp reads (seed 4, 250 Mbp genome), 160 GiB working set,
+    one super-k-mer batch up to the record pool (1.5e9 records, ~22.6K per
+    bucket: P5a's LDS table overflows in about half the buckets, which P5 then
+    counts raw). 15e9 k-mers are too many to recount by hash on the host in
+    the test's time, so the full-size parity property is checked: window
+    checksums over every valid window (CPU, spec form) equal the
+    count-weighted record checksums, keys strictly ascending."""
+    n, L, k = 125_000_000, 150, 31
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=160 << 30) as ctx:
+        ptr, nb = ctx.synth_device(n, L, 4, 250_000_000, 0.0, 0)
+        fq = _host_fastq(ctx, ptr, nb)
+        ctx.reset()
+        assert ctx.count_fastq_device(ptr, nb) == n
+        ctx.finish()
+        st = ctx.stats()
+        ctx.free_device(ptr)
+        recs = _host_records(ctx)
+    assert st["batches"] == 1 and st["engines_used"] == 1 and st["spilled_kmers"] == 0
+    a = _assert_window_checksum(orc, fq, recs, k, _usable_cpus())
+    assert a["windows"] == n * (L - k + 1) == st["windows"]
 
 
 def _owner_slices(kca, recs, rs, world):
@@ -648,14 +748,15 @@ def _u64_sortable(lo32, hi32):
 
 @pytest.mark.slow
 @pytest.mark.parametrize("batches", [False, True], ids=["key_passes", "read_batches"])
-def test_config5_full_size_properties(kca, monkeypatch, batches):
+def test_config5_full_size_properties(kca, orc, monkeypatch, batches):
     """BASELINE config 5 (k=55 two-word keys, 20M x 150 bp iid reads, ~1.92e9
     distinct) on the default engine with a working set below the distinct
     count: the records outgrow it, are cut into sorted runs (the reference's
     spill -> sort path) and kc_finish merges the runs on the device. Checked
     on the device: keys strictly ascending (two-word order), counts sum to the
     valid windows, and every k-mer of sampled reads is present with a count
-    no lower than its multiplicity in the sample. Default: key-range passes
+    no lower than its multiplicity in the sample; and on the host the window
+    checksums of the whole input equal the records'. Default: key-range passes
     (one run, concatenated); read_batches (KC_NO_KEY_PASSES): one sorted run
     per read batch, merged on the device."""
     import torch
@@ -666,6 +767,7 @@ def test_config5_full_size_properties(kca, monkeypatch, batches):
     dev = torch.device("cuda", 0)
     with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=24 << 30) as ctx:
         ptr, nb = ctx.synth_device(n, L, 5, 0, 0.0, 0)
+        checksum = (orc, _host_fastq(ctx, ptr, nb))
         assert ctx.count_fastq_device(ptr, nb) == n
         ctx.free_device(ptr)
         nrec = ctx.finish()
@@ -677,6 +779,10 @@ def test_config5_full_size_properties(kca, monkeypatch, batches):
             assert st["key_passes"] >= 2 and st["spill_runs"] == 1
         rec = torch.empty(nrec * 20, dtype=torch.uint8, device=dev)
         ctx.export_records(rec)
+    if checksum is not None:
+        # the full-size parity property over all 1.92e9 records (CPU)
+        _assert_window_checksum(checksum[0], checksum[1], rec.cpu().numpy(), k, _usable_cpus())
+        checksum = None
     words = rec.view(torch.int32).view(nrec, 5)
     total = 0
     prev = None

@@ -26,6 +26,48 @@ def test_oracle_matches_golden(orc, name):
     assert orc.refcpu(data, m["k"], threads=2)[0] == want
 
 
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_window_checksum_matches_golden(orc, name):
+    """The full-size parity property (window checksums, kc_oracle.c) agrees
+    with every golden output: the sums of two key hashes over the valid
+    windows equal the count-weighted sums over the records."""
+    m = MANIFEST[name]
+    data = open(os.path.join(GOLD, m["fastq"]), "rb").read()
+    want = open(os.path.join(GOLD, m["expected"]), "rb").read()
+    k = m["k"]
+    a = orc.window_checksum(data, k, threads=3)
+    b = orc.records_checksum(want, k, threads=2)
+    assert (a["h1"], a["h2"], a["valid"]) == (b["h1"], b["h2"], b["count"])
+    assert b["unordered"] == 0
+    rs = orc.rs_of(k)
+    zero_first = want[:rs - 4] == bytes(rs - 4)
+    assert a["hole"] <= zero_first  # an invalid window makes key 0^W present
+
+
+def test_window_checksum_detects_moved_count(orc):
+    """A count moved from one key to another, a dropped record or swapped
+    records all change the record sums (or the order check)."""
+    import numpy as np
+
+    data = open(os.path.join(GOLD, MANIFEST[sorted(MANIFEST)[0]]["fastq"]), "rb").read()
+    k = MANIFEST[sorted(MANIFEST)[0]]["k"]
+    want = orc.count_fastq(data, k)
+    rs = orc.rs_of(k)
+    good = orc.records_checksum(want, k)
+    recs = np.frombuffer(bytearray(want), dtype=np.uint8).reshape(-1, rs).copy()
+    c = recs[:, rs - 4:].copy().view("<u4")
+    i = int(np.argmax(c[:-1, 0] >= 1))
+    moved = recs.copy()
+    moved[i, rs - 4:] = np.frombuffer(np.uint32(c[i, 0] - 1).tobytes(), np.uint8)
+    moved[i + 1, rs - 4:] = np.frombuffer(np.uint32(c[i + 1, 0] + 1).tobytes(), np.uint8)
+    bad = orc.records_checksum(moved.tobytes(), k)
+    assert bad["count"] == good["count"] and (bad["h1"], bad["h2"]) != (good["h1"], good["h2"])
+    assert orc.records_checksum(np.delete(recs, i, axis=0).tobytes(), k)["h1"] != good["h1"]
+    swapped = recs.copy()
+    swapped[[3, 4]] = swapped[[4, 3]]
+    assert orc.records_checksum(swapped.tobytes(), k)["unordered"] > 0
+
+
 def _reads(rng, n, L, alphabet="ACGT", n_rate=0.0):
     out = []
     for _ in range(n):
