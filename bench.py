@@ -29,7 +29,7 @@ Sub-objects of the same line (same input, same context):
                     KMerCounter.cpp:193-212) through ~960 kc_count_chunk calls
                     vs one kc_count_chunk call of all of them, output in HBM;
   cpu_baseline    : the CPU port of the reference pipeline on a bounded sample
-                    (N = 1, rank 0).
+                    (rank 0, after the timed region, at every N).
 
 N GPUs (one process per GPU, torch.distributed; RCCL = backend nccl): rank r
 counts reads [r R, (r+1) R) of the one read stream (weak scaling).
@@ -37,11 +37,18 @@ counts reads [r R, (r+1) R) of the one read stream (weak scaling).
     exchanged by key-space owner (RCCL all-to-all) and merged on the device;
     rank r owns the r-th key range (in the e2e leg it writes it as its own part
     file); the parts in rank order are the node's SortedKMerFile.
-  --exchange none (cfg3, read-shard): the runs are gathered to rank 0's GPU
-    (RCCL) and merged there (device merge path), rank 0 writes the file.
+  --exchange files (default of --config 3; cfg3 as BASELINE.json states it:
+    read-shard, no RCCL, host KMerFileMerger k-way merge): every rank writes
+    its sorted run as a SortedKMerFile and rank 0 merges the N files on the
+    host (kc_merge_files: one k-way level, key ranges merged by all usable
+    CPUs); the step includes the run files and the merge.
+  --exchange none (read-shard variant over RCCL): the runs are gathered to
+    rank 0's GPU (RCCL) and merged there (device merge path), rank 0 writes
+    the file.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5] [--reads R] [--exchange alltoall|none]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--reads R]
                     [--value device|e2e] [--e2e|--no-e2e] [--no-cpu] [--no-variants] [--workdir DIR]
+                    [--exchange alltoall|none|files]
                     [--min-read-length M]
 
 Prints one JSON line on rank 0 (contract in the task statement); a failure
@@ -174,9 +181,12 @@ class Dist:
     def barrier_sync(self):
         if self.dist is not None:
             import torch
-            torch.cuda.synchronize()
+            gpu = torch.cuda.is_available()
+            if gpu:
+                torch.cuda.synchronize()
             self.dist.barrier()
-            torch.cuda.synchronize()
+            if gpu:
+                torch.cuda.synchronize()
 
     def max(self, v):
         return max_over_ranks(self.dist, float(v), self.xdev() if self.dist is not None else None)
@@ -223,6 +233,28 @@ def gather_runs_to_rank0(kca, ctx, D):
     return 0
 
 
+def host_merge_runs(kca, ctx, D, run_dir, out_path, k, fan_in=0, threads=0):
+    """cfg3 as BASELINE.json states it (read-shard, no RCCL, host
+    KMerFileMerger k-way merge; KMerFileMergeHandler.cpp:49-100,
+    KMerFileMerger.cpp:49-96): every rank writes its sorted run as a
+    SortedKMerFile into run_dir (kc_write_output), and rank 0 merges the N
+    files into out_path with kc_merge_files (fan-in noOfMergersAtOnce, default
+    N: one k-way level; noOfMergeThreads threads, default the usable CPUs:
+    the last level merges key ranges in parallel). The barriers only order the
+    ranks (no data moves through a collective). The files are overwritten in
+    place each step. Returns rank 0's merged record count (0 on other ranks)."""
+    run = os.path.join(run_dir, f"kc_cfg3.run{D.rank}")
+    ctx.write_output(run)
+    D.barrier_sync()
+    n = 0
+    if D.rank == 0:
+        runs = [os.path.join(run_dir, f"kc_cfg3.run{r}") for r in range(D.world)]
+        kca.merge_files(runs, out_path, k, fan_in or D.world, threads or usable_cpus())
+        n = os.path.getsize(out_path) // ctx.rs
+    D.barrier_sync()
+    return n
+
+
 def write_node_output(kca, ctx, D, path, exchange):
     """The node's SortedKMerFile from the ranks' finished runs (see the module
     docstring). Returns output bytes written by this rank.
@@ -240,6 +272,9 @@ def write_node_output(kca, ctx, D, path, exchange):
     if exchange == "alltoall":
         n = kca.keyspace_exchange(ctx, D.dist, D.xdev())
         ctx.write_output(f"{path}.part{D.rank}")
+        return n * ctx.rs
+    if exchange == "files":
+        n = host_merge_runs(kca, ctx, D, os.path.dirname(path) or ".", path, ctx.k)
         return n * ctx.rs
     n = gather_runs_to_rank0(kca, ctx, D)
     if D.rank == 0:
@@ -292,6 +327,17 @@ def main(args, D, state):
     ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first, lmin)
     state["ptr"] = ptr
     exchange = args.exchange if D.world > 1 else "none"
+    run_dir = None
+    if exchange == "files":
+        # the ranks' run files and rank 0's merged file (SortedKMerFile each)
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", str(D.world)))
+        est = int(nbytes * 0.3) + (64 << 20)
+        run_dir, free, tried = pick_workdir(args.workdir, local_ranks * est + (est if D.local == 0 else 0) * 2)
+        if run_dir is None:
+            raise RuntimeError(f"--exchange files: no directory with room for the run files ({tried})")
+        state.setdefault("files", []).extend(
+            [os.path.join(run_dir, f"kc_cfg3.run{D.rank}")] + ([os.path.join(run_dir, "kc_cfg3.out")]
+                                                              if D.rank == 0 else []))
 
     def windows_of_step(st):
         return st["windows"] if varlen else args.reads * (L - k + 1)
@@ -311,6 +357,10 @@ def main(args, D, state):
         elif exchange == "none" and D.world > 1:
             t = time.perf_counter()
             n = gather_runs_to_rank0(kca, ctx, D)
+            xch_ms[0] += (time.perf_counter() - t) * 1e3
+        elif exchange == "files":
+            t = time.perf_counter()
+            n = host_merge_runs(kca, ctx, D, run_dir, os.path.join(run_dir, "kc_cfg3.out"), k)
             xch_ms[0] += (time.perf_counter() - t) * 1e3
         return n
 
@@ -345,6 +395,7 @@ def main(args, D, state):
         "breakdown_ms_per_step": {"fastq_index": acc["decode_ms"] / args.steps,
                                   "finish": acc["finish_ms"] / args.steps,
                                   "exchange_rank0": xch_ms[0] / args.steps,
+                                  "exchange": exchange,
                                   "partition_passes": [round(x / args.steps, 3) for x in acc["part_ms"]],
                                   "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3),
                                   "p3b_presplit (in partition_passes[2])": round(acc["presplit_ms"] / args.steps, 3)},
@@ -374,7 +425,9 @@ def main(args, D, state):
     state["files"] = []
 
     cpu = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu:
+    # rank 0 times the CPU port after the timed region, at every N (the other
+    # ranks wait at the closing barrier)
+    if D.rank == 0 and not args.no_cpu:
         if varlen:
             cpu = cpu_baseline_varlen(kca, max(1, args.cpu_reads // 10), L, args.min_read_length, k, args.genome,
                                       args.seed)
@@ -393,6 +446,11 @@ def main(args, D, state):
                     f"(key, count) records (RCCL) + per-GPU merge: rank r owns the r-th key range "
                     f"(rank-order concatenation = the SortedKMerFile)")
         parallelism = f"read-shard count + key-space all-to-all x{D.world}"
+    elif exchange == "files":
+        workload = (f"cfg3 at {D.world} GPUs as BASELINE.json states it: {base}; read-shard, no RCCL: each rank's "
+                    f"sorted run written as a SortedKMerFile, rank 0's host k-way merge (kc_merge_files, "
+                    f"KMerFileMerger semantics) into the node's SortedKMerFile; step = count + run files + merge")
+        parallelism = f"read-shard x{D.world} + host k-way merge on rank 0"
     else:
         workload = (f"cfg3 pattern at {D.world} GPUs: {base}; {path_desc}; runs gathered to rank 0's GPU "
                     f"(RCCL) and merged there by merge path")
@@ -552,15 +610,17 @@ def parse_args(argv=None):
                                                     "whichever has the space)")
     ap.add_argument("--min-read-length", type=int, default=0,
                     help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
-    ap.add_argument("--exchange", default=None, choices=["alltoall", "none"],
-                    help="N>1: key-space all-to-all (cfg4) or read-shard + merge on rank 0 (cfg3)")
+    ap.add_argument("--exchange", default=None, choices=["alltoall", "none", "files"],
+                    help="N>1: key-space all-to-all (cfg4, RCCL), read-shard + RCCL gather and device merge on "
+                         "rank 0 (none), or read-shard + run files + host k-way merge on rank 0 (files: cfg3 as "
+                         "stated, no RCCL)")
     args = ap.parse_args(argv)
     if args.mode:
         args.value = args.mode
         if args.mode == "e2e" and args.e2e is None:
             args.e2e = True
     preset = {2: dict(reads=50_000_000, k=31, genome=250_000_000, seed=2, mem=160 << 30),
-              3: dict(reads=50_000_000, k=31, genome=250_000_000, seed=3, mem=160 << 30, exchange="none"),
+              3: dict(reads=50_000_000, k=31, genome=250_000_000, seed=3, mem=160 << 30, exchange="files"),
               4: dict(reads=125_000_000, k=31, genome=250_000_000, seed=4, mem=160 << 30, exchange="alltoall"),
               5: dict(reads=20_000_000, k=55, genome=0, seed=5, mem=48 << 30)}[args.config]
     preset.setdefault("exchange", "alltoall")
@@ -625,9 +685,10 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
         rb = 8 * (W + 1)
         nw = L - k + 1
         ng = max((L + 15) // 16 + 1, (nw - 1) // 16 + 5) | 1
+        hooks = os.environ.get("KC_TEST_HOOKS") == "1"  # the library reads KC_NO_F3/F2 only then
         f3 = (W == 1 and 19 <= k <= 32 and (320 + 64) * 8 + 256 + 256 * ng <= 40 * 1024
-              and not os.environ.get("KC_NO_F3"))
-        f2 = W == 1 and 18 <= k <= 32 and (nw + 7) // 8 <= 64 and not os.environ.get("KC_NO_F2")
+              and not (hooks and os.environ.get("KC_NO_F3")))
+        f2 = W == 1 and 18 <= k <= 32 and (nw + 7) // 8 <= 64 and not (hooks and os.environ.get("KC_NO_F2"))
         fname = f"skm_front3_k<{k}>" if f3 else (f"skm_front2_k<1,{k}>" if f2 else f"skm_front_k<{W}>")
         dd_step = st.get("dedup_records", 0)
         specs = [

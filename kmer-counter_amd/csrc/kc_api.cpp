@@ -68,7 +68,7 @@ struct kc_ctx {
     bool skm_used = false;         // a batch went through the skm engine since the last reset
     bool skm_force = false;        // KC_FLAG_ENGINE_SKM: no cardinality sample
     bool skm_checked = false;      // the skm cardinality sample has run since the last reset
-    bool skm_big_off = false;      // a large skm batch overflowed the spill buffer: safe batches only
+    bool skm_big_off = false;      // a large skm batch overflowed the spill or record buffer: safe batches only
     uint32_t engines_used = 0;     // kc_stats.engines_used
     bool skm_hc = false;           // high cardinality seen: the key-prefix engine counts
     bool hc_hint = false;          // most keys were distinct (the skm sample or the last key-prefix batch):
@@ -185,6 +185,44 @@ static kc_status fail(kc_ctx* c, kc_status s, const char* fmt, ...) {
         c->err = buf;
     }
     return s;
+}
+
+// The host-side counters one batch adds to (kc_stats timings and launch
+// counts, engine flags): snapshot before a batch that may be undone.
+struct HostCounters {
+    uint64_t insert_launches;
+    double insert_ms;
+    double part_ms[5];
+    double dedup_ms;
+    uint64_t p5_launches, part_keys;
+    bool skm_used, skm_checked;
+    uint32_t engines_used;
+};
+
+static HostCounters host_counters(const kc_ctx* c) {
+    HostCounters h;
+    h.insert_launches = c->st.insert_launches;
+    h.insert_ms = c->st.insert_ms;
+    memcpy(h.part_ms, c->part_ms, sizeof(h.part_ms));
+    h.dedup_ms = c->dedup_ms;
+    h.p5_launches = c->p5_launches;
+    h.part_keys = c->part_keys;
+    h.skm_used = c->skm_used;
+    h.skm_checked = c->skm_checked;
+    h.engines_used = c->engines_used;
+    return h;
+}
+
+static void restore_host_counters(kc_ctx* c, const HostCounters& h) {
+    c->st.insert_launches = h.insert_launches;
+    c->st.insert_ms = h.insert_ms;
+    memcpy(c->part_ms, h.part_ms, sizeof(h.part_ms));
+    c->dedup_ms = h.dedup_ms;
+    c->p5_launches = h.p5_launches;
+    c->part_keys = h.part_keys;
+    c->skm_used = h.skm_used;
+    c->skm_checked = h.skm_checked;
+    c->engines_used = h.engines_used;
 }
 
 #define HIPCHK(ctx, expr)                                                                                    \
@@ -617,7 +655,7 @@ static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vecto
     if (total <= c->key_cap) return KC_OK;
     uint64_t np = (total + c->key_cap - 1) / c->key_cap;
     // (KC_KEY_PASSES_MIN: path selector for tests and measurements, same counts)
-    if (const char* e = getenv("KC_KEY_PASSES_MIN")) np = std::max<uint64_t>(np, strtoull(e, nullptr, 10));
+    if (const char* e = test_hook("KC_KEY_PASSES_MIN")) np = std::max<uint64_t>(np, strtoull(e, nullptr, 10));
     const uint64_t cap = std::min<uint64_t>(c->key_cap, (total + np - 1) / np * 5 / 4);
     const uint64_t target = (total + np - 1) / np;
     std::vector<uint32_t> bounds{0};
@@ -644,7 +682,7 @@ static kc_status plan_key_passes(kc_ctx* c, CountLaunch l, int64_t L, std::vecto
 // KC_P3B_MIN: path selector for tests, same counts either way
 static uint64_t p3b_min_of() {
     uint64_t m = 1ull << 22;
-    if (const char* e = getenv("KC_P3B_MIN")) m = strtoull(e, nullptr, 10);
+    if (const char* e = test_hook("KC_P3B_MIN")) m = strtoull(e, nullptr, 10);
     return m;
 }
 
@@ -701,15 +739,15 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
     uint64_t* kp_u_keys = nullptr;
     uint64_t kp_u_n = 0;
     // KC_P2_NO_DIGS (measurement): P2 writes no digit bytes (P3 reads word 0)
-    const bool p2_no_digs = getenv("KC_P2_NO_DIGS") != nullptr && !getenv("KC_P3_SCATTER");
+    const bool p2_no_digs = test_hook("KC_P2_NO_DIGS") != nullptr && !test_hook("KC_P3_SCATTER");
     // P2 writes each key as W consecutive words (one stream per digit run
     // instead of W) when P3 is the radix scatter, which reads them so
     // (KC_P2_SOA: the SoA layout, for comparison)
     const bool p2_aos =
-        !p2_no_digs && !getenv("KC_P2_SOA") && !getenv("KC_P3_SCATTER") && p3_tile(W) == rp_tile(W, false);
+        !p2_no_digs && !test_hook("KC_P2_SOA") && !test_hook("KC_P3_SCATTER") && p3_tile(W) == rp_tile(W, false);
     if (pre0 >= 0 && c->hc_hint && nw * n_reads > c->key_cap && c->rec_n == 0 && c->batches == 0 &&
-        c->stats_h[ST_CLAIMED] == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES") &&
-        !getenv("KC_NO_P3B") && !getenv("KC_NO_SORT_RUNS") && !getenv("KC_NO_P5S_DIRECT")) {
+        c->stats_h[ST_CLAIMED] == 0 && !c->skm_used && c->runs.empty() && !test_hook("KC_NO_KEY_PASSES") &&
+        !test_hook("KC_NO_P3B") && !test_hook("KC_NO_SORT_RUNS") && !test_hook("KC_NO_P5S_DIRECT")) {
         if ((s = plan_key_passes(c, launch_args(0, n_reads), L, &kp, &kp_keys))) return s;
         kp_direct = !kp.empty();
         if (!kp.empty()) c->key_passes += kp.size() - 1;
@@ -750,8 +788,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         const uint64_t* p2_base = (const uint64_t*)(from_u ? c->part_base2.p : c->part_base.p);
         uint64_t n = from_u ? kp_u_n : 0;
         if (!from_u) {
-            const bool dual = kpass && kp_direct && kpi + 2 < kp.size() && !getenv("KC_NO_DUAL_PASS") &&
-                              !getenv("KC_P3_SCATTER");
+            const bool dual = kpass && kp_direct && kpi + 2 < kp.size() && !test_hook("KC_NO_DUAL_PASS") &&
+                              !test_hook("KC_P3_SCATTER");
             if (dual && (s = ensure(c, c->part_base2, hn * 8))) return s;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
             if (pre0 < 0)
@@ -850,10 +888,12 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             uint8_t* p3b_digs = nullptr;  // P3b digit bytes written by P3 (else P3b reads word 0)
             bool p3_aos = false;          // P3's output keys AoS (only when P3b follows)
             bool p3b_aos = false;         // P3b's output keys AoS
+            // decided once: P3's output layout and P5's input depend on it
+            const bool p3b = c->hc_hint && n >= p3b_min_of() && !test_hook("KC_NO_P3B");
             // P3's scatter is the regional radix scatter (digit word0 >> 56 over
             // the 256 P2 regions, same tiles; next tile's run starts prefetched,
             // XCD-aware tile walk); KC_P3_SCATTER: the older p3_scatter_k
-            if (getenv("KC_P3_SCATTER") || p3_tile(W) != rp_tile(W, false)) {
+            if (test_hook("KC_P3_SCATTER") || p3_tile(W) != rp_tile(W, false)) {
                 if (from_u) return fail(c, KC_ERR_INTERNAL, "p3_scatter_k reads keys_a only");
                 HIPCHK(c, launch_p3_scatter(W, c->keys_a, c->keys_b, c->key_cap, p3t, p3t + 257, ntiles, p3h,
                                             2 * c->n_cu, c->stream));
@@ -861,9 +901,9 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 // a P3b pass follows (high cardinality): P3 writes each key's P3b
                 // digit byte (bits 40..47) into the free P2 digit array, so P3b's
                 // histogram reads 1 B per key, not word 0
-                p3b_digs = c->hc_hint && n >= p3b_min_of() && !getenv("KC_NO_P3B") ? c->digs : nullptr;
+                p3b_digs = p3b ? c->digs : nullptr;
                 // ... and writes the keys AoS for it (P3b reads them so)
-                p3_aos = p3b_digs && !getenv("KC_P3_SOA");
+                p3_aos = p3b_digs && !test_hook("KC_P3_SOA");
                 HIPCHK(c, launch_rp_scatter(W, false, p2_keys, p2_aos ? 0 : p2_stride, c->keys_b,
                                             p3_aos ? 0 : c->key_cap, nullptr, nullptr, p3t, p3t + 257, 256, ntiles,
                                             p3h, 56, p3b_digs, 40, 2 * c->n_cu, c->stream));
@@ -890,10 +930,13 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             // consecutive sub-buckets in one pass each and reads every key
             // once instead of once per sub-range pass
             uint64_t* p5_keys = c->keys_b;
-            uint64_t p5_stride = c->key_cap;  // 0: AoS (P3b's output)
+            uint64_t p5_stride = p3_aos ? 0 : c->key_cap;  // 0: AoS (P3's or P3b's output)
             uint64_t* p5_spill = c->keys_a;
             const uint64_t* sub_starts = nullptr;
-            if (c->hc_hint && n >= p3b_min_of() && !getenv("KC_NO_P3B")) {
+            if (p3b) {
+                // P3's AoS output always comes with its digit bytes (the
+                // regional histogram reads word 0 from SoA keys only)
+                if (p3_aos && !p3b_digs) return fail(c, KC_ERR_INTERNAL, "P3b: AoS keys without digit bytes");
                 std::vector<uint64_t> rs((size_t)nb + 1);
                 HIPCHK(c, hipMemcpyAsync(rs.data(), c->part_starts.p, rs.size() * 8, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -916,7 +959,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 HIPCHK(c, launch_rp_hist_regional(c->keys_b, 40, rtd, rtd + nb + 1, (int)nb, nt, (uint32_t)tile, pos,
                                                   cnt_t, 2 * c->n_cu, c->stream, p3b_digs));
                 // (its output AoS too, for P5s / the hash path; KC_P3B_SOA: arrays)
-                p3b_aos = !getenv("KC_P3B_SOA");
+                p3b_aos = !test_hook("KC_P3B_SOA");
                 HIPCHK(c, launch_rp_scatter(W, false, c->keys_b, p3_aos ? 0 : c->key_cap, c->keys_a,
                                             p3b_aos ? 0 : c->key_cap, nullptr, nullptr,
                                             rtd, rtd + nb + 1, (int)nb, nt, pos, 40, nullptr, 0, 2 * c->n_cu,
@@ -950,9 +993,9 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
             // P5s: pre-split runs sorted in LDS (records <= keys, no overflow);
             // the runs it flags (a sub-bucket too big, clustered keys) take
             // the LDS hash table (KC_NO_SORT_RUNS: hash table for all runs)
-            const bool sort_runs = sub_starts && !getenv("KC_NO_SORT_RUNS");
+            const bool sort_runs = sub_starts && !test_hook("KC_NO_SORT_RUNS");
             uint64_t direct_min = 1ull << 22;  // (KC_P5S_DIRECT_MIN: path selector for tests)
-            if (const char* e = getenv("KC_P5S_DIRECT_MIN")) direct_min = strtoull(e, nullptr, 10);
+            if (const char* e = test_hook("KC_P5S_DIRECT_MIN")) direct_min = strtoull(e, nullptr, 10);
             if (kpass && kp_direct) {
                 // key-range pass: appended to the direct run of the earlier passes
                 bool dd = false;
@@ -988,7 +1031,7 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
                 if (kp_out > 0 && (s = direct_keep(c, kp_out))) return s;
             }
             if (!kpass && sort_runs && c->rec_n == 0 && c->batches == 0 && c->stats_h[ST_CLAIMED] == 0 && !c->skm_used &&
-                c->runs.empty() && n >= direct_min && !getenv("KC_NO_P5S_DIRECT")) {
+                c->runs.empty() && n >= direct_min && !test_hook("KC_NO_P5S_DIRECT")) {
                 const size_t fl = ((size_t)nb << 8) + nb + 16;
                 if ((s = ensure(c, c->run_flags, fl))) return s;
                 bool dd = false;
@@ -1187,7 +1230,7 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
 // count_reads_skm): the record pool at nw / 4 records per read, while the
 // global table is empty; 0 when only safe batches apply
 static uint64_t skm_big_reads(const kc_ctx* c, uint64_t nw, uint64_t pool_cap) {
-    if (c->skm_big_off || c->stats_h[ST_CLAIMED] || c->table_dirty || getenv("KC_SKM_SAFE_BATCH")) return 0;
+    if (c->skm_big_off || c->stats_h[ST_CLAIMED] || c->table_dirty || test_hook("KC_SKM_SAFE_BATCH")) return 0;
     return pool_cap / std::max<uint64_t>(1, nw / 4);
 }
 
@@ -1201,7 +1244,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
     const uint64_t nw = (uint64_t)(L - c->k + 1);
     // keys_a / keys_b hold RW x pool_cap record words each; digs holds a byte per record
     uint64_t pool_cap = (uint64_t)W * c->key_cap / RW;
-    if (const char* e = getenv("KC_SKM_POOL_CAP")) {  // tests: force the pool-overflow retry
+    if (const char* e = test_hook("KC_SKM_POOL_CAP")) {  // tests: force the pool-overflow retry
         const uint64_t v = strtoull(e, nullptr, 10);
         if (v > 0 && v < pool_cap) pool_cap = v;
     }
@@ -1249,6 +1292,9 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         l.rlen = (pre0 >= 0 && c->var_rlen) ? c->var_rlen + (uint64_t)pre0 + done : nullptr;
         if ((s = sync_stats(c))) return s;
         std::vector<uint64_t> saved(c->stats_h, c->stats_h + ST_N);
+        // host-side counters of the batch, restored with the device ones when
+        // the batch is undone (so kc_stats describes only the work kept)
+        const HostCounters hsaved = host_counters(c);
         HIPCHK(c, hipMemsetAsync(c->pool_cursor, 0, 8, c->stream));
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
         if (pre0 < 0)
@@ -1279,6 +1325,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             HIPCHK(c, hipMemcpyAsync(c->stats, saved.data(), ST_N * 8, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             memcpy(c->stats_h, saved.data(), ST_N * 8);
+            restore_host_counters(c, hsaved);
             if (nr <= 1) return fail(c, KC_ERR_INTERNAL, "skm pool overflow on one read");
             max_reads = nr / 2;
             continue;
@@ -1311,17 +1358,26 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             // the front of its range, multiplicities into the digit bytes
             // (free after S2, read as u32 indexed like the pool); P5 walks them
             SkmDedup dd = {};
-            const bool dedup = W == 1 && !getenv("KC_NO_DEDUP") && np <= c->digs_bytes / 4;
+            const bool dedup = W == 1 && !test_hook("KC_NO_DEDUP") && np <= c->digs_bytes / 4;
             if (dedup) {
                 if ((s = ensure(c, c->part_dedup, ((size_t)nb + 1) * 4 + 64))) return s;
                 dd.cnt = (const uint32_t*)c->digs;
                 dd.len = (const uint32_t*)c->part_dedup.p;
             }
             // P5 over buckets [b0, b1); reruns with a bigger record buffer on
-            // overflow (safe while nothing went to the global table or spill)
+            // overflow (safe while nothing went to the global table or spill).
+            // A large batch (more than key_cap windows) does not grow the
+            // buffer to its window count, which can be far past the working
+            // set: it sets rec_retry, and the batch is undone and counted in
+            // safe batches like a spill overflow
+            bool rec_retry = false;
             auto p5_range = [&](uint32_t b0, uint32_t b1, bool count_keys) -> kc_status {
                 uint64_t bound = (uint64_t)(b1 - b0) * (uint64_t)skm_lds_slots(W);
                 if (bound > kbound) bound = kbound;
+                if (const char* e = test_hook("KC_P5_REC_BOUND")) {  // tests: force the overflow path
+                    const uint64_t v = strtoull(e, nullptr, 10);
+                    if (v > 0 && v < bound) bound = v;
+                }
                 const uint64_t rec0 = c->rec_n;
                 const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
                 kc_status s2;
@@ -1356,6 +1412,10 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                                 (unsigned long long)c->stats_h[ST_P5_ABORTS],
                                 (unsigned long long)c->stats_h[ST_P5_MAXM], (unsigned long long)c->rec_n, t);
                     if (!(c->stats_h[ST_ERR] & ERR_REC_OVERFLOW)) return KC_OK;
+                    if (big) {
+                        rec_retry = true;
+                        return KC_OK;
+                    }
                     if (bound >= kbound || c->stats_h[ST_CLAIMED] != claimed0 || c->stats_h[ST_SPILL2_FILL])
                         return fail(c, KC_ERR_INTERNAL, "record buffer overflow");
                     bound = kbound;
@@ -1379,7 +1439,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 if ((s = p5_range(0, bs, true))) return s;
                 c->skm_checked = true;
                 const uint64_t keys_s = c->stats_h[ST_P5_KEYS], dist_s = c->rec_n - rec_batch0;
-                if (keys_s > 0 && (double)dist_s > kSkmDistinctMax * (double)keys_s &&
+                if (!rec_retry && keys_s > 0 && (double)dist_s > kSkmDistinctMax * (double)keys_s &&
                     c->stats_h[ST_CLAIMED] == saved[ST_CLAIMED] && c->stats_h[ST_SPILL2_FILL] == 0) {
                     HIPCHK(c, hipMemcpyAsync(c->stats, saved.data(), ST_N * 8, hipMemcpyHostToDevice, c->stream));
                     HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec_batch0, 8, hipMemcpyHostToDevice, c->stream));
@@ -1396,24 +1456,26 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                                             pre0 < 0 ? -1 : pre0 + (int64_t)done);
                 }
             }
-            if ((s = p5_range(bs, nbk, false))) return s;
-            if (dedup) {
+            if (!rec_retry && (s = p5_range(bs, nbk, false))) return s;
+            if (dedup && !rec_retry) {
                 HIPCHK(c, launch_dedup_total((const uint32_t*)c->part_dedup.p, (const uint64_t*)c->part_starts.p, nbk,
                                              c->stats, c->stream));
                 if ((s = sync_stats(c))) return s;
             }
             c->skm_used = true;
             c->engines_used |= 1u;
-            if ((c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) && big) {
+            if (((c->stats_h[ST_ERR] & ERR_SPILL_OVERFLOW) || rec_retry) && big) {
                 // undo the large batch and count its reads in safe batches
-                if (getenv("KC_DEBUG")) fprintf(stderr, "kc: skm batch of %llu reads overflowed the spill buffer: retried\n", (unsigned long long)nr);
+                if (getenv("KC_DEBUG"))
+                    fprintf(stderr, "kc: skm batch of %llu reads overflowed the %s buffer: retried\n",
+                            (unsigned long long)nr, rec_retry ? "record" : "spill");
                 HIPCHK(c, hipMemsetAsync(c->table, 0, c->table_bytes, c->stream));
                 HIPCHK(c, hipMemcpyAsync(c->stats, saved.data(), ST_N * 8, hipMemcpyHostToDevice, c->stream));
                 HIPCHK(c, hipMemcpyAsync(c->rec_cursor, &rec_batch0, 8, hipMemcpyHostToDevice, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
                 memcpy(c->stats_h, saved.data(), ST_N * 8);
+                restore_host_counters(c, hsaved);
                 c->rec_n = rec_batch0;
-                c->part_keys -= np;
                 c->skm_big_off = true;
                 max_reads = safe_reads;
                 continue;
@@ -1503,7 +1565,7 @@ static kc_status sketch_gate(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre
     const bool sketch_skm = c->skm && !c->skm_hc && !c->skm_force && skm_ok;
     // (the key-prefix engine: chosen, or the default engine's only one for this (L, k))
     const bool sketch_part = c->part && !c->hc_hint && !(c->skm && !c->skm_hc && skm_ok);
-    if ((sketch_skm || sketch_part) && !c->skm_checked && pre0 >= 0 && !getenv("KC_NO_SKETCH") &&
+    if ((sketch_skm || sketch_part) && !c->skm_checked && pre0 >= 0 && !test_hook("KC_NO_SKETCH") &&
         n_reads * (uint64_t)(L - c->k + 1) >= kSkmSampleMinKeys) {
         kc_status s = sketch_engine(c, n_reads, L, pre0);
         if (s) return s;
@@ -1599,7 +1661,7 @@ static kc_status pend_flush(kc_ctx* c) {
             // the records outgrow half the working set
             if ((s = sketch_gate(c, n, L, 0))) return s;
             const bool passes = c->hc_hint && c->part && (!c->skm || c->skm_hc) && c->rec_n == 0 &&
-                                c->batches == 0 && !c->skm_used && c->runs.empty() && !getenv("KC_NO_KEY_PASSES");
+                                c->batches == 0 && !c->skm_used && c->runs.empty() && !test_hook("KC_NO_KEY_PASSES");
             if (!passes) {
                 // the skm engine may take a large batch (count_reads_skm)
                 uint64_t bs = b;
@@ -1746,7 +1808,7 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     // nothing is reserved, encoded or flushed: a validation has no side effects)
     const bool into_pend = count && codes && n_rec > 0 && n_rec <= pend_room(c, L, var);
     if (into_pend && (s = pend_reserve(c, L, var, n_rec, &off))) return s;
-    const bool no_fuse = getenv("KC_NO_FQ_ENCODE") != nullptr;  // path selector (tests): same bytes either way
+    const bool no_fuse = test_hook("KC_NO_FQ_ENCODE") != nullptr;  // path selector (tests): same bytes either way
     const bool fused = into_pend && !var && !no_fuse;                               // fq_encode_k
     const bool whole_var = into_pend && var;                                         // the block encoded whole
     const bool fused_var = whole_var && !two_pass && !no_fuse && fq_encode_var_ok((int)L);  // fq_encode_k<true>
@@ -2243,7 +2305,7 @@ static const size_t kFileBlock = (size_t)256 << 20;
 // Block size of the file reader; KC_FILE_BLOCK (bytes) is a path selector for
 // tests (many blocks from small files: cut search, carries; same counts).
 static size_t file_block_bytes() {
-    if (const char* e = getenv("KC_FILE_BLOCK")) {
+    if (const char* e = test_hook("KC_FILE_BLOCK")) {
         const long long v = atoll(e);
         if (v >= 4096) return (size_t)v;
     }
@@ -2610,7 +2672,7 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
     uint64_t* k0 = (uint64_t*)c->fin_keys[0].p;
     uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
     const uint32_t nb = 1u << kBucketBits;
-    bool grouped = n >= nb && n <= c->key_cap && !getenv("KC_NO_SEGSORT");
+    bool grouped = n >= nb && n <= c->key_cap && !test_hook("KC_NO_SEGSORT");
     std::vector<uint64_t> st;
     if (grouped) {
         double gm[2] = {0, 0};
@@ -2674,7 +2736,7 @@ static kc_status finish_part(kc_ctx* c, uint64_t* n_out) {
     kc::trace("finish_part: %llu records, %llu batches, %llu claimed, %zu host runs, %llu descriptors",
               (unsigned long long)nrec, (unsigned long long)c->batches, (unsigned long long)claimed, c->runs.size(),
               (unsigned long long)ndesc);
-    if (c->batches <= 1 && claimed == 0 && c->runs.empty() && ndesc <= kDescCap && !getenv("KC_NO_SEGSORT"))
+    if (c->batches <= 1 && claimed == 0 && c->runs.empty() && ndesc <= kDescCap && !test_hook("KC_NO_SEGSORT"))
         return finish_part_sorted(c, ndesc, n_out);
     const uint64_t out_cap = nrec + claimed + 1;
     for (int i = 0; i < 2; i++) {

@@ -20,6 +20,19 @@ inline int experiment_knob(const char* name) {
 #endif
 }
 
+// Path-selecting test hooks (KC_NO_P3B, KC_SKM_POOL_CAP, KC_NO_F3, ...):
+// they force fallbacks and alternative layouts so the tests can reach them,
+// and every one of them gives the same counts. A production caller never
+// meets them by accident: the library reads them only when KC_TEST_HOOKS=1
+// is set in the environment (tests/conftest.py sets it for the test suite).
+inline const char* test_hook(const char* name) {
+    static const bool on = [] {
+        const char* e = getenv("KC_TEST_HOOKS");
+        return e && e[0] == '1' && e[1] == 0;
+    }();
+    return on ? getenv(name) : nullptr;
+}
+
 // Device counters, one uint64 each, in a small device array owned by the ctx.
 enum Stat : int {
     ST_VALID = 0,        // valid k-mer windows seen

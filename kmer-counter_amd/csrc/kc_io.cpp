@@ -5,12 +5,17 @@
 #include "kc_io.h"
 
 #include <errno.h>
+#include <fcntl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <queue>
 #include <thread>
 
@@ -182,6 +187,288 @@ bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int 
     return ok;
 }
 
+// ---------------------------------------------------------------------------
+// Key-range parallel k-way merge (the last level of the merge tree).
+//
+// The reference merges two (noOfMergersAtOnce) files at a time, one thread per
+// merge (KMerFileMergeHandler.cpp:49-100), so its last merge is one thread
+// reading every record. Here the key space is cut into ranges of about
+// kRangeRecs input records: a range starts at a splitter key, and each run's
+// part of it is found by binary search (pread of single records), so equal
+// keys always fall into one range and folding never crosses a range edge.
+// `threads` workers take the ranges in key order, read each run's slice with
+// pread (or from memory), merge and fold it in memory, and write the result
+// at its offset in the output once the ranges before it are merged (the
+// offsets are the prefix sums of the merged sizes). Same bytes as merge_runs.
+// ---------------------------------------------------------------------------
+
+static const uint64_t kRangeRecs = 4u << 20;
+
+// input records per range; KC_MERGE_RANGE_RECS (a test hook, honoured only
+// with KC_TEST_HOOKS=1 like the library's others) makes ranges small
+static uint64_t range_recs() {
+    const char* on = getenv("KC_TEST_HOOKS");
+    const char* e = on && strcmp(on, "1") == 0 ? getenv("KC_MERGE_RANGE_RECS") : nullptr;
+    const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return v ? v : kRangeRecs;
+}
+
+namespace {
+
+struct RunAccess {
+    int fd = -1;
+    const uint8_t* mem = nullptr;
+    uint64_t n = 0;  // records
+    int rs = 12;
+    ~RunAccess() {
+        if (fd >= 0) ::close(fd);
+    }
+    bool open_src(const RunSource& s, int rs_) {
+        rs = rs_;
+        if (!s.path.empty()) {
+            fd = ::open(s.path.c_str(), O_RDONLY);
+            if (fd < 0) return false;
+            struct stat st;
+            if (fstat(fd, &st) != 0) return false;
+            n = (uint64_t)st.st_size / (uint64_t)rs;
+        } else {
+            mem = s.mem;
+            n = s.bytes / (uint64_t)rs;
+        }
+        return true;
+    }
+    bool read(uint64_t i, uint64_t cnt, uint8_t* dst) const {
+        const size_t want = (size_t)(cnt * (uint64_t)rs);
+        if (mem) {
+            memcpy(dst, mem + i * (uint64_t)rs, want);
+            return true;
+        }
+        size_t got = 0;
+        while (got < want) {
+            ssize_t r = pread(fd, dst + got, want - got, (off_t)(i * (uint64_t)rs + got));
+            if (r <= 0) {
+                if (r < 0 && errno == EINTR) continue;
+                if (r == 0) errno = EIO;
+                return false;
+            }
+            got += (size_t)r;
+        }
+        return true;
+    }
+    // first record index in [lo, hi) whose key is >= key (hi if none)
+    bool lower_bound(const uint8_t* key, int W, uint64_t lo, uint64_t hi, uint64_t* res) const {
+        uint8_t rec[8 * 4 + 4];
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if (!read(mid, 1, rec)) return false;
+            if (key_compare(rec, key, W) < 0)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        *res = lo;
+        return true;
+    }
+};
+
+static inline uint64_t ld64(const uint8_t* p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+
+// a < b on W key words (word 0 first, unsigned)
+template <int W>
+static inline bool key_less(const uint8_t* a, const uint8_t* b) {
+    for (int j = 0; j < W; j++) {
+        const uint64_t x = ld64(a + 8 * j), y = ld64(b + 8 * j);
+        if (x != y) return x < y;
+    }
+    return false;
+}
+
+// Merges the slices (each sorted) into dst, folding equal keys (u32 sums; the
+// sum is commutative, so which run's copy of a key comes first does not
+// matter). The few runs of a merge level are scanned linearly for the
+// smallest head (an exhausted run is swapped out), cheaper than a heap at
+// m <= ~16 and without the heap's per-compare indirection.
+template <int W>
+static uint64_t merge_slices_w(const std::vector<const uint8_t*>& beg, const std::vector<const uint8_t*>& end,
+                               uint8_t* dst) {
+    const int rs = 8 * W + 4;
+    std::vector<const uint8_t*> cur, lim;
+    for (size_t i = 0; i < beg.size(); i++)
+        if (beg[i] < end[i]) cur.push_back(beg[i]), lim.push_back(end[i]);
+    int m = (int)cur.size();
+    uint8_t* o = dst;
+    while (m > 0) {
+        int bi = 0;
+        for (int i = 1; i < m; i++)
+            if (key_less<W>(cur[i], cur[bi])) bi = i;
+        const uint8_t* h = cur[bi];
+        if (o != dst && memcmp(o - rs, h, 8 * W) == 0) {
+            uint32_t a, b;
+            memcpy(&a, o - 4, 4);
+            memcpy(&b, h + 8 * W, 4);
+            a += b;
+            memcpy(o - 4, &a, 4);
+        } else {
+            memcpy(o, h, rs);
+            o += rs;
+        }
+        cur[bi] += rs;
+        if (cur[bi] >= lim[bi]) {
+            cur[bi] = cur[m - 1];
+            lim[bi] = lim[m - 1];
+            m--;
+        }
+    }
+    return (uint64_t)(o - dst);
+}
+
+static uint64_t merge_slices(const std::vector<const uint8_t*>& beg, const std::vector<const uint8_t*>& end, int W,
+                             uint8_t* dst) {
+    switch (W) {
+    case 1: return merge_slices_w<1>(beg, end, dst);
+    case 2: return merge_slices_w<2>(beg, end, dst);
+    case 3: return merge_slices_w<3>(beg, end, dst);
+    default: return merge_slices_w<4>(beg, end, dst);
+    }
+}
+
+}  // namespace
+
+bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t threads,
+                         int* err_no) {
+    const int rs = 8 * W + 4;
+    if (threads < 1) threads = 1;
+    std::vector<RunAccess> acc(runs.size());
+    uint64_t total = 0;
+    for (size_t i = 0; i < runs.size(); i++) {
+        if (!acc[i].open_src(runs[i], rs)) {
+            if (err_no) *err_no = errno ? errno : EIO;
+            return false;
+        }
+        total += acc[i].n;
+    }
+    const int m = (int)acc.size();
+    // ranges: bounds[r][i] = run i's first record of range r. Split the
+    // key space at keys of the run holding the most records of a range until
+    // every range holds about kRangeRecs records (a range of one repeated key
+    // cannot be split and stays whole).
+    std::vector<std::vector<uint64_t>> bounds;
+    const uint64_t rr = range_recs();
+    {
+        std::vector<uint64_t> lo(m, 0), hi(m);
+        for (int i = 0; i < m; i++) hi[i] = acc[i].n;
+        std::vector<std::pair<std::vector<uint64_t>, std::vector<uint64_t>>> todo;
+        todo.push_back({lo, hi});
+        std::vector<std::pair<std::vector<uint64_t>, std::vector<uint64_t>>> done;
+        uint8_t key[8 * 4 + 4];
+        while (!todo.empty()) {
+            auto rg = todo.back();
+            todo.pop_back();
+            uint64_t n = 0, best = 0;
+            int bi = 0;
+            for (int i = 0; i < m; i++) {
+                const uint64_t c = rg.second[i] - rg.first[i];
+                n += c;
+                if (c > best) best = c, bi = i;
+            }
+            bool split = false;
+            if (n > 2 * rr && best > 1) {
+                const uint64_t mid = rg.first[bi] + best / 2;
+                if (!acc[bi].read(mid, 1, key)) {
+                    if (err_no) *err_no = errno ? errno : EIO;
+                    return false;
+                }
+                std::vector<uint64_t> cut(m);
+                for (int i = 0; i < m; i++)
+                    if (!acc[i].lower_bound(key, W, rg.first[i], rg.second[i], &cut[i])) {
+                        if (err_no) *err_no = errno ? errno : EIO;
+                        return false;
+                    }
+                uint64_t left = 0, right = 0;
+                for (int i = 0; i < m; i++) left += cut[i] - rg.first[i], right += rg.second[i] - cut[i];
+                if (left > 0 && right > 0) {
+                    todo.push_back({cut, rg.second});  // right half later: ranges come out in key order
+                    todo.push_back({rg.first, cut});
+                    split = true;
+                }
+            }
+            if (!split) done.push_back(rg);
+        }
+        for (auto& d : done) bounds.push_back(d.first);
+        bounds.push_back(std::vector<uint64_t>(hi));
+    }
+    const size_t nr = bounds.size() - 1;
+    int fd = ::open(out.c_str(), O_WRONLY | O_CREAT, 0644);
+    if (fd < 0) {
+        if (err_no) *err_no = errno;
+        return false;
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t committed = 0;  // ranges whose output offset is known
+    uint64_t next_off = 0;
+    std::atomic<size_t> cursor(0);
+    std::atomic<int> bad(0);
+    auto work = [&]() {
+        std::vector<uint8_t> in, res;
+        for (;;) {
+            const size_t r = cursor.fetch_add(1);
+            if (r >= nr) break;
+            uint64_t cnt = 0;
+            for (int i = 0; i < m; i++) cnt += bounds[r + 1][i] - bounds[r][i];
+            in.resize((size_t)(cnt * (uint64_t)rs) + 1);
+            res.resize((size_t)(cnt * (uint64_t)rs) + 1);
+            std::vector<const uint8_t*> b(m), e(m);
+            uint64_t pos = 0;
+            bool ok = !bad.load();
+            for (int i = 0; i < m && ok; i++) {
+                const uint64_t c = bounds[r + 1][i] - bounds[r][i];
+                if (c && !acc[i].read(bounds[r][i], c, in.data() + pos * (uint64_t)rs)) {
+                    bad = errno ? errno : EIO;
+                    ok = false;
+                }
+                b[i] = in.data() + pos * (uint64_t)rs;
+                e[i] = b[i] + c * (uint64_t)rs;
+                pos += c;
+            }
+            const uint64_t nbytes = ok ? merge_slices(b, e, W, res.data()) : 0;
+            uint64_t off;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return committed == r; });
+                off = next_off;
+                next_off += nbytes;
+                committed = r + 1;
+            }
+            cv.notify_all();
+            size_t put = 0;
+            while (ok && put < nbytes) {
+                ssize_t w = pwrite(fd, res.data() + put, (size_t)(nbytes - put), (off_t)(off + put));
+                if (w <= 0) {
+                    if (w < 0 && errno == EINTR) continue;
+                    bad = errno ? errno : EIO;
+                    ok = false;
+                }
+                put += w > 0 ? (size_t)w : 0;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t t = 0; t < threads && t < nr; t++) pool.emplace_back(work);
+    for (auto& t : pool) t.join();
+    // written in place, cut to size (no truncation of an old file first)
+    bool ok = !bad.load();
+    if (ok && ftruncate(fd, (off_t)next_off) != 0) bad = errno, ok = false;
+    if (::close(fd) != 0 && ok) bad = errno, ok = false;
+    if (!ok && err_no) *err_no = bad.load();
+    (void)total;
+    return ok;
+}
+
 bool merge_tree(const std::vector<RunSource>& runs_in, const std::string& out, int W, uint32_t fan_in,
                 uint32_t threads, const std::string& tmp_prefix, std::string* err) {
     if (fan_in < 2) fan_in = 2;
@@ -232,7 +519,7 @@ bool merge_tree(const std::vector<RunSource>& runs_in, const std::string& out, i
     }
     if (ok) {
         int e = 0;
-        ok = merge_runs(runs, out, W, &e);
+        ok = threads > 1 ? merge_runs_parallel(runs, out, W, threads, &e) : merge_runs(runs, out, W, &e);
         if (!ok && err) *err = "cannot write output file " + out + ": " + strerror(e);
     }
     for (const auto& t : temps) unlink(t.c_str());

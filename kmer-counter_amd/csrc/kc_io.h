@@ -73,10 +73,17 @@ class RunWriter {
 // On failure *err_no (if given) holds the errno of the failing call.
 bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int W, int* err_no = nullptr);
 
+// The same merge by up to `threads` threads over disjoint key ranges (each
+// run's slice of a range found by binary search), written in place at each
+// range's offset; runs may be files or memory. Same bytes as merge_runs.
+bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t threads,
+                         int* err_no = nullptr);
+
 // Merge tree with the reference handler's knobs (KMerFileMergeHandler.cpp):
 // while more than fan_in runs remain, groups of fan_in runs are merged into
 // temporary files "<tmp_prefix>.m<i>" by up to `threads` threads; the rest is
-// merged into `out`. The bytes of `out` do not depend on fan_in/threads.
+// merged into `out` (by merge_runs_parallel when threads > 1). The bytes of
+// `out` do not depend on fan_in/threads.
 bool merge_tree(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t fan_in,
                 uint32_t threads, const std::string& tmp_prefix, std::string* err);
 

@@ -1316,7 +1316,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
 // F3 geometry: false when F3 does not apply
 static bool f3_args(const CountLaunch& l, const SkmGeom& g, F3Args* a, size_t* lds) {
     const int W = (l.k + 31) / 32;
-    if (W != 1 || g.m != 11 || l.k < 19 || l.k > 32 || getenv("KC_NO_F3")) return false;
+    if (W != 1 || g.m != 11 || l.k < 19 || l.k > 32 || test_hook("KC_NO_F3")) return false;
     if (((uintptr_t)l.inval & 3) || ((uintptr_t)l.codes & 3)) return false;  // dword DMA of the masks
     const int nw = l.L - l.k + 1;
     if (nw <= 0 || nw > 65535) return false;
@@ -1340,7 +1340,7 @@ static bool f3_args(const CountLaunch& l, const SkmGeom& g, F3Args* a, size_t* l
 // F2 geometry for (L, k) (W = 1, m = 11): false when F2 does not apply
 static bool f2_args(const CountLaunch& l, const SkmGeom& g, F2Args* a, size_t* lds) {
     const int W = (l.k + 31) / 32;
-    if (W != 1 || g.m != 11 || l.k < 18 || l.k > 32 || getenv("KC_NO_F2")) return false;
+    if (W != 1 || g.m != 11 || l.k < 18 || l.k > 32 || test_hook("KC_NO_F2")) return false;
     const int nw = l.L - l.k + 1;
     const int nchr = (nw + 7) / 8;
     if (nchr > 64 || nw <= 0) return false;
@@ -2845,7 +2845,7 @@ hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* sta
     a.b0 = b0;
     a.nbuckets = b1;
     a.ngrp = rec_dedup_groups();
-    if (const char* e = getenv("KC_P5A_GROUPS")) {  // tests: force full tables (raw buckets)
+    if (const char* e = test_hook("KC_P5A_GROUPS")) {  // tests: force full tables (raw buckets)
         const long v = atol(e);
         if (v > 0 && (u32)v < a.ngrp) a.ngrp = (u32)v;
     }

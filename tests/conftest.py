@@ -5,6 +5,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the library honours its path-selecting test hooks (KC_NO_P3B, KC_SKM_POOL_CAP,
+# ...) only with KC_TEST_HOOKS=1 (kc_device.h test_hook); the tests use them
+os.environ["KC_TEST_HOOKS"] = "1"
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

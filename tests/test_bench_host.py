@@ -19,7 +19,7 @@ def _bench():
 
 def test_presets():
     b = _bench()
-    want = {2: (50_000_000, 31, 2, "alltoall"), 3: (50_000_000, 31, 3, "none"),
+    want = {2: (50_000_000, 31, 2, "alltoall"), 3: (50_000_000, 31, 3, "files"),
             4: (125_000_000, 31, 4, "alltoall"), 5: (20_000_000, 55, 5, "alltoall")}
     for cfg, (reads, k, seed, xch) in want.items():
         a = b.parse_args(["--config", str(cfg)])

@@ -1,7 +1,7 @@
 """Multi-process (world size 2, gloo on the CPU) coverage of the read-shard
 path of bench.py / the CLI: disjoint shards whose sorted runs, k-way merged
-on the host, equal the count of the whole read stream; the step time is the
-max over ranks. The per-shard counts come from the CPU oracle here (no GPU in
+on the host (bench.host_merge_runs, cfg3 as stated), equal the count of the
+whole read stream; the step time is the max over ranks. The per-shard counts come from the CPU oracle here (no GPU in
 this container); the GPU side of the same path is covered by
 tests/test_gpu_parity.py::test_cli_multi_context."""
 import os
@@ -22,6 +22,26 @@ def _free_port():
     return p
 
 
+class _FileRun:
+    """Stand-in for a finished Context (no GPU here): its sorted run is the
+    oracle's, written as a SortedKMerFile by write_output."""
+
+    def __init__(self, records, k):
+        self.k, self.rs, self._r = k, 8 * ((k + 31) // 32) + 4, records
+
+    def write_output(self, path):
+        with open(path, "wb") as f:
+            f.write(self._r)
+
+
+class _GlooRanks:
+    def __init__(self, dist, rank, world):
+        self.dist, self.rank, self.world = dist, rank, world
+
+    def barrier_sync(self):
+        self.dist.barrier()
+
+
 def _worker(rank, world, port, tmpdir, per, k):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -39,8 +59,15 @@ def _worker(rank, world, port, tmpdir, per, k):
     kca = load_pkg()
     first = bench.shard_first(rank, per)
     fq = kca.synth_fastq(per, 150, 2, genome_length=400_000, first_read=first)
+    run = oracle.count_fastq(fq, k)
     with open(os.path.join(tmpdir, f"run{rank}"), "wb") as f:
-        f.write(oracle.count_fastq(fq, k))
+        f.write(run)
+    # bench's cfg3 step as stated (--exchange files): run files + rank 0's
+    # host k-way merge, the barriers only ordering the ranks
+    n = bench.host_merge_runs(kca, _FileRun(run, k), _GlooRanks(dist, rank, world), tmpdir,
+                              os.path.join(tmpdir, "node.bin"), k, threads=3)
+    with open(os.path.join(tmpdir, f"n{rank}"), "w") as f:
+        f.write(str(n))
     t = bench.max_over_ranks(dist, float(rank + 1), torch.device("cpu"))
     with open(os.path.join(tmpdir, f"t{rank}"), "w") as f:
         f.write(repr(t))
@@ -57,6 +84,8 @@ def test_read_shard_merge_equals_whole(kca, orc, tmp_path, k):
     kca.merge_files(runs, str(out), k)
     whole = kca.synth_fastq(world * per, 150, 2, genome_length=400_000)
     assert out.read_bytes() == orc.count_fastq(whole, k)
+    assert (tmp_path / "node.bin").read_bytes() == out.read_bytes()
+    assert int((tmp_path / "n0").read_text()) * (8 * ((k + 31) // 32) + 4) == out.stat().st_size
     for r in range(world):
         assert float((tmp_path / f"t{r}").read_text()) == float(world)
 

@@ -6,8 +6,10 @@ Each rank counts its own shard of the read stream on the GPU, then
   alltoall (cfg4): kca.keyspace_exchange; every rank writes its key range as
                    its own part file; the parts in rank order == the oracle's
                    count of the whole stream;
-  none (cfg3)    : bench.gather_runs_to_rank0 (rank 0 merges every rank's run
-                   on its GPU by merge path) and rank 0 writes the file.
+  none           : bench.gather_runs_to_rank0 (rank 0 merges every rank's run
+                   on its GPU by merge path) and rank 0 writes the file;
+  files (cfg3)   : bench.host_merge_runs (every rank writes its run as a
+                   SortedKMerFile, rank 0 k-way merges them on the host).
 Both go through bench.write_node_output, bench.Dist and bench.shard_first."""
 import os
 import socket
@@ -53,7 +55,7 @@ def _worker(rank, world, port, tmpdir, per, k, exchange, mem):
     D.dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["alltoall", "none"])
+@pytest.mark.parametrize("exchange", ["alltoall", "none", "files"])
 @pytest.mark.parametrize("world,k,mem", [(2, 31, 100_000_000), (3, 55, 1 << 20)])
 def test_bench_multirank_output(kca, orc, tmp_path, exchange, world, k, mem):
     """(mem 1 MiB at k = 55: every rank also cuts sorted runs, merged before

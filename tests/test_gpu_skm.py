@@ -6,6 +6,8 @@ repeats keep one minimizer), prefix skew beyond the segment sort, and every
 record width (W = 1..3, K' = k or 32W). Needs an MI355X."""
 import os
 import random
+import subprocess
+import sys
 
 import pytest
 
@@ -83,6 +85,51 @@ def test_skm_large_batch_spill_overflow_retried(kca, orc, tmp_path, monkeypatch,
     assert "overflowed the spill buffer: retried" in capfd.readouterr().err
     assert st["spilled_kmers"] > 0
     assert got == orc.count_fastq(fq, 31)
+
+
+def test_skm_large_batch_record_overflow_retried(kca, orc, monkeypatch, capfd):
+    """A large first batch (more reads than key_cap windows allow, taken while
+    the global table is empty) whose P5 records overflow the record buffer is
+    undone and counted in safe batches, instead of growing the buffer to the
+    batch's window count (which can be far past gpu_memory_limit).
+    KC_P5_REC_BOUND forces the overflow; the counts stay exact and the
+    statistics count the kept work once."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    monkeypatch.setenv("KC_P5_REC_BOUND", "5000")
+    n, L, k = 80000, 150, 31
+    fq = kca.synth_fastq(n, L, seed=36, genome_length=400_000, n_rate=0.0005)
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=64 << 20, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    err = capfd.readouterr().err
+    assert "overflowed the record buffer: retried" in err
+    assert st["batches"] >= 2 and st["windows"] == n * (L - k + 1)
+    rs = 8 * ((k + 31) // 32) + 4
+    assert st["valid_kmers"] == sum(int.from_bytes(got[i + rs - 4:i + rs], "little") for i in range(0, len(got), rs))
+    assert got == orc.count_fastq(fq, k)
+
+
+def test_test_hooks_ignored_without_switch(kca, orc, tmp_path):
+    """The path-selecting variables are test hooks: without KC_TEST_HOOKS=1
+    the library ignores them (a production caller cannot meet them by
+    accident). Run in a child process: KC_SKM_POOL_CAP would force pool
+    overflow retries (several batches) if it were honoured."""
+    fq = kca.synth_fastq(20000, 150, seed=5, n_rate=0.002)
+    p = tmp_path / "in.fq"
+    p.write_bytes(fq)
+    code = (
+        "import importlib.util, json, sys\n"
+        f"spec = importlib.util.spec_from_file_location('kca', {kca.__file__!r})\n"
+        "m = importlib.util.module_from_spec(spec); spec.loader.exec_module(m)\n"
+        f"fq = open({str(p)!r}, 'rb').read()\n"
+        "with m.Context(kmer_length=31, line_length=150, engine='skm') as c:\n"
+        "    c.count_fastq(fq); sys.stdout.buffer.write(c.records()); sys.stderr.write(str(c.stats()['batches']))\n")
+    env = {kk: v for kk, v in os.environ.items() if kk != "KC_TEST_HOOKS"}
+    env["KC_SKM_POOL_CAP"] = "20000"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, check=True, timeout=300)
+    assert r.stderr.decode().strip().splitlines()[-1] == "1"
+    assert r.stdout == orc.count_fastq(fq, 31)
 
 
 @pytest.mark.parametrize("cap,k", [(20000, 31), (20001, 31), (20007, 55)])

@@ -142,6 +142,37 @@ def test_merge_matches_reference_merger(kca, orc, tmp_path, k, nruns, fan, thr):
         assert ref == mine
 
 
+@pytest.mark.parametrize("k,nruns,thr,rr", [(31, 8, 4, 500), (31, 3, 16, 64), (55, 5, 3, 300), (100, 2, 2, 50),
+                                            (31, 1, 4, 100)])
+def test_merge_key_ranges_parallel(kca, orc, tmp_path, monkeypatch, k, nruns, thr, rr):
+    """The last merge level by key ranges (kc_io.cpp merge_runs_parallel):
+    small ranges (KC_MERGE_RANGE_RECS) put many range edges among duplicate
+    keys inside and across runs, and a long stretch of one repeated key that
+    no edge may split; the bytes equal the single-threaded merge's and the
+    reference merger's."""
+    monkeypatch.setenv("KC_MERGE_RANGE_RECS", str(rr))
+    W = (k + 31) // 32
+    rng = random.Random(k * 7 + nruns + rr)
+    runs = _random_runs(rng, nruns, 4000, W, dup_frac=0.3, space=6000 if W == 1 else 50)
+    key = runs[0][len(runs[0]) // 2][0]
+    runs[0] = sorted(runs[0] + [(key, 3)] * (5 * rr))  # one key repeated across several ranges' worth
+    paths = []
+    for i, r in enumerate(runs):
+        p = tmp_path / f"run{i}"
+        _run_file(p, r, W)
+        paths.append(str(p))
+    out = tmp_path / "merged.bin"
+    (tmp_path / "merged.bin").write_bytes(b"x" * 10_000_000)  # an older, larger file is overwritten and cut
+    kca.merge_files(paths, str(out), k, max(2, nruns), thr)
+    mine = out.read_bytes()
+    assert mine == _expected(runs, W)
+    one = tmp_path / "one.bin"
+    kca.merge_files(paths, str(one), k, max(2, nruns), 1)
+    assert one.read_bytes() == mine
+    if orc.have_ref("ref_merge"):
+        assert orc.ref_merge(paths, str(tmp_path / "ref.bin"), k, len(paths) + 1, 1) == mine
+
+
 def test_merge_large_runs_cross_cache_refill(kca, orc, tmp_path):
     """Runs above the reference's 1M-record cache (SortedKMerFile.cpp:29)."""
     rng = np.random.default_rng(3)
