@@ -2,9 +2,13 @@
 // records, timed with HIP events; run against variant builds of
 // libkc_hip.so (tools/build_variant.sh, KC_RP_ABL ablations) through
 // LD_LIBRARY_PATH. Usage: rp_bench [n_records] [NW] [reps] [emit] [dshift] [layout]
+// Every run checks its output (digits ascending, items' hash sum equal to the
+// input's, emitted digit bytes).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <vector>
 
 #include "kc_device.h"
 
@@ -84,8 +88,8 @@ int main(int argc, char** argv) {
     float best = 1e30f, tot = 0.f;
     for (int r = 0; r < reps + 1; r++) {
         CK(hipEventRecord(e0, s));
-        CK(kc::launch_rp_scatter(NW, false, ai, n, bi, n, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift, with_emit ? digs : nullptr, 56,
-                                 2 * ncu, s));
+        CK(kc::launch_rp_scatter(NW, false, ai, n, bi, n, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift,
+                                 with_emit ? digs : nullptr, 56, 2 * ncu, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
         float t;
@@ -93,6 +97,32 @@ int main(int argc, char** argv) {
         if (r > 0) {
             tot += t;
             if (t < best) best = t;
+        }
+    }
+    // check: output digits ascending, every item once (hash sums), emitted digit bytes
+    {
+        std::vector<uint64_t> hi((size_t)n * NW), ho((size_t)n * NW);
+        std::vector<uint8_t> hd(with_emit ? n : 1);
+        CK(hipMemcpy(hi.data(), ai, n * 8 * NW, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(ho.data(), bi, n * 8 * NW, hipMemcpyDeviceToHost));
+        if (with_emit) CK(hipMemcpy(hd.data(), digs, n, hipMemcpyDeviceToHost));
+        uint64_t si = 0, so = 0, bad = 0;
+        auto mix = [](uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; return x; };
+        for (uint64_t i = 0; i < n; i++) {
+            uint64_t x = 0, y = 0;
+            for (int j = 0; j < NW; j++) {
+                x = mix(x ^ hi[(size_t)j * n + i]) + (uint64_t)j;
+                y = mix(y ^ ho[(size_t)j * n + i]) + (uint64_t)j;
+            }
+            si += x;
+            so += y;
+            if (i && ((ho[i] >> dshift) & 255) < ((ho[i - 1] >> dshift) & 255)) bad++;
+            if (with_emit && hd[i] != (uint8_t)(ho[i] >> 56)) bad++;
+        }
+        if (si != so || bad) {
+            fprintf(stderr, "rp_bench: output check FAILED (hash %s, %llu misplaced)\n", si == so ? "ok" : "differs",
+                    (unsigned long long)bad);
+            return 2;
         }
     }
     const double bytes = (double)n * (16.0 * NW + (with_emit ? 1.0 : 0.0));
