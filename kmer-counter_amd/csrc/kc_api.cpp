@@ -1359,10 +1359,21 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             // (free after S2, read as u32 indexed like the pool); P5 walks them
             SkmDedup dd = {};
             const bool dedup = W == 1 && !test_hook("KC_NO_DEDUP") && np <= c->digs_bytes / 4;
+            // P5a's overflow lists (buckets whose distinct records overflow its
+            // LDS table, deduplicated again in hash-split passes) go to the
+            // pool's free tail: records [np, limit) of keys_a, their
+            // multiplicities at the same indices of the digit-byte buffer (u32)
+            const uint64_t over0 = (np + 63) & ~63ull;
+            uint64_t over_limit = std::min<uint64_t>(pool_cap, c->digs_bytes / 4);
+            if (const char* e = test_hook("KC_P5A_OVER_ROOM"))  // tests: little room, later buckets stay raw
+                over_limit = std::min<uint64_t>(over_limit, over0 + strtoull(e, nullptr, 10));
+            const size_t dpos_off = (((size_t)nb + 1) * 4 + 64 + 15) & ~(size_t)15;
             if (dedup) {
-                if ((s = ensure(c, c->part_dedup, ((size_t)nb + 1) * 4 + 64))) return s;
+                if ((s = ensure(c, c->part_dedup, dpos_off + (size_t)nb * 8))) return s;
                 dd.cnt = (const uint32_t*)c->digs;
                 dd.len = (const uint32_t*)c->part_dedup.p;
+                dd.pos = (const uint64_t*)((const uint8_t*)c->part_dedup.p + dpos_off);
+                HIPCHK(c, hipMemcpyAsync(c->pool_cursor, &over0, 8, hipMemcpyHostToDevice, c->stream));
             }
             // P5 over buckets [b0, b1); reruns with a bigger record buffer on
             // overflow (safe while nothing went to the global table or spill).
@@ -1384,7 +1395,9 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 if (dedup) {
                     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                     HIPCHK(c, launch_count_rec(c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, b0, b1,
-                                               (uint32_t*)c->digs, (uint32_t*)c->part_dedup.p, c->n_cu, c->stream));
+                                               (uint32_t*)c->digs, (uint32_t*)c->part_dedup.p, c->n_cu, c->stream,
+                                               over0 < over_limit ? c->pool_cursor : nullptr, over_limit,
+                                               (uint64_t*)dd.pos));
                     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                     HIPCHK(c, hipEventSynchronize(c->ev1));
                     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
@@ -1773,6 +1786,16 @@ static bool engine_reads_codes(const kc_ctx* c, int64_t L) {
 // The whole block is checked before any of its reads is pending or counted: a
 // malformed block changes nothing and returns KC_ERR_FORMAT. With count =
 // false only the checks run (kc_check_fastq).
+static std::string fq_errors(uint64_t e, bool var) {
+    std::string why;
+    if (e & ERR_FQ_NOT_AT) why += " record-does-not-start-with-@";
+    if (e & ERR_FQ_NO_PLUS) why += " no-+-line-after-sequence";
+    if (e & ERR_FQ_SEQ_LEN) why += var ? " sequence-longer-than-L" : " sequence-length-differs-from-L";
+    if (e & ERR_FQ_TOO_MANY) why += " index-overflow";
+    if (e & ERR_FQ_NO_FINAL_NL) why += " block-does-not-end-with-newline";
+    return why;
+}
+
 static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, bool var, bool count,
                               uint64_t* n_rec_out, bool two_pass = false) {
     kc_status s;
@@ -1783,6 +1806,14 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     if ((s = sync_stats(c))) return s;
     uint64_t snap[ST_N];
     memcpy(snap, c->stats_h, sizeof(snap));
+    auto restore = [&]() -> kc_status {
+        // the counters the index / encode kernels touched (errors, variable-length hole flag and windows)
+        snap[ST_ERR] = 0;
+        HIPCHK(c, hipMemcpyAsync(c->stats, snap, sizeof(snap), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        memcpy(c->stats_h, snap, sizeof(snap));
+        return KC_OK;
+    };
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
     HIPCHK(c, launch_fq_count(base, n, (uint64_t*)c->fq_counts.p, c->stream));
@@ -1838,26 +1869,13 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
     c->st.decode_ms += t;
     const uint64_t e = c->stats_h[ST_ERR];
-    auto restore = [&]() -> kc_status {
-        // the counters the index / encode kernels touched (errors, variable-length hole flag and windows)
-        snap[ST_ERR] = 0;
-        HIPCHK(c, hipMemcpyAsync(c->stats, snap, sizeof(snap), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        memcpy(c->stats_h, snap, sizeof(snap));
-        return KC_OK;
-    };
     if (fused_var && (e & ERR_FQ_LIST)) {
         // a half held more records than the fused list: the two-pass index
         if ((s = restore())) return s;
         return ingest_fastq(c, base, n, L, var, count, n_rec_out, true);
     }
     if (e) {
-        std::string why;
-        if (e & ERR_FQ_NOT_AT) why += " record-does-not-start-with-@";
-        if (e & ERR_FQ_NO_PLUS) why += " no-+-line-after-sequence";
-        if (e & ERR_FQ_SEQ_LEN) why += var ? " sequence-longer-than-L" : " sequence-length-differs-from-L";
-        if (e & ERR_FQ_TOO_MANY) why += " index-overflow";
-        if (e & ERR_FQ_NO_FINAL_NL) why += " block-does-not-end-with-newline";
+        const std::string why = fq_errors(e, var);
         if ((s = restore())) return s;
         return fail(c, KC_ERR_FORMAT, "FASTQ block is not 4-line records with %s%lld-base reads:%s",
                     var ? "at most " : "", (long long)L, why.c_str());

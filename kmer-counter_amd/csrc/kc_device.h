@@ -333,14 +333,20 @@ int seg_sort_cap(int W);  // longest segment seg_sort_k takes
 // place at the front of its range of recs (2 x stride SoA), their
 // multiplicities at the same indices of cnt; dlen[b] = their number
 // (kRawList 0xffffffff: the table filled, records left as they were)
+// A bucket whose distinct records overflow the LDS table is deduplicated
+// again in hash-split passes into a list reserved from *over_cursor (records
+// of recs / cnt below over_limit, free), dpos[b] its start, dlen[b] =
+// 0x80000000 | its length; no room or no over_cursor: left raw.
 hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
-                            uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s);
+                            uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s, uint64_t* over_cursor = nullptr,
+                            uint64_t over_limit = 0, uint64_t* dpos = nullptr);
 // stats[ST_DEDUP] += sum over buckets [0, nb) of dlen[b] (raw: the bucket's records)
 hipError_t launch_dedup_total(const uint32_t* dlen, const uint64_t* starts, uint32_t nb, uint64_t* stats,
                               hipStream_t s);
 struct SkmDedup {
     const uint32_t* cnt;  // P5a output
     const uint32_t* len;
+    const uint64_t* pos;  // overflow lists' starts (len flag 0x80000000)
 };
 // buckets [b0, b1); count_keys: add the buckets' key counts to stats[ST_P5_KEYS];
 // dd (optional): P5a's lists, walked instead of the buckets' records

@@ -1957,6 +1957,18 @@ __device__ __forceinline__ u64 slot_frac(const u64 (&key)[W]) {
     return h >> 16;
 }
 
+// LDS tables of one-word keys in groups of 4 slots (32 B, read as two 16-byte
+// halves): logical slot j of group g sits at physical slot 4g + (j ^ gswz(g)),
+// i.e. the two halves swap places in every other run of 8 groups. Unswizzled,
+// a half's 16 bytes start at one of only 8 of the 16 four-bank quads (32-byte
+// groups), so the 16 lanes of a ds_read_b128 lane group meet twice as often
+// on a quad; swizzled, the halves of random groups spread over all 16.
+#ifndef KC_NO_GSWZ
+__device__ __forceinline__ u32 gswz(u32 g) { return (g >> 2) & 2u; }
+#else
+__device__ __forceinline__ u32 gswz(u32) { return 0u; }  // variant builds: the unswizzled layout (A/B)
+#endif
+
 // `frac` is a 48-bit uniform hash fraction; slot = frac * lcap >> 48.
 // *claimed is set when this key took an empty slot.
 template <int W, int GS = 4>
@@ -1972,11 +1984,11 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
             const u32 ng = lcap / GS;
             u32 g = (u32)((frac * (u64)ng) >> 48);
             for (u32 pr = 0; pr < max_probe; pr += GS) {
-                const lds_v2u64* gp = (const lds_v2u64*)(lkeys + GS * g);
+                const u32 sw = GS == 4 ? gswz(g) : 0u;  // physical slot of logical j: GS g + (j ^ sw)
                 u64 v[GS];
 #pragma unroll
                 for (int h = 0; h < GS / 2; h++) {
-                    const v2u64 a = gp[h];
+                    const v2u64 a = *(const lds_v2u64*)(lkeys + GS * g + ((2u * (u32)h) ^ sw));
                     v[2 * h] = a.x;
                     v[2 * h + 1] = a.y;
                 }
@@ -1987,15 +1999,15 @@ __device__ __forceinline__ bool lds_insert(const u64 (&key)[W], u64 frac, u64* l
                     if (v[i] == 0ull) emp = i;
                 }
                 if (hit >= 0 && (emp < 0 || hit < emp)) {
-                    atomicAdd(&lcnt[GS * g + hit], w);
+                    atomicAdd(&lcnt[GS * g + ((u32)hit ^ sw)], w);
                     return true;
                 }
                 if (emp >= 0) {
                     // claim the first empty slot; a lost race re-reads the group
-                    const u64 old =
-                        atomicCAS((unsigned long long*)&lkeys[GS * g + emp], 0ull, (unsigned long long)key[0]);
+                    const u64 old = atomicCAS((unsigned long long*)&lkeys[GS * g + ((u32)emp ^ sw)], 0ull,
+                                              (unsigned long long)key[0]);
                     if (old == 0ull || old == key[0]) {
-                        atomicAdd(&lcnt[GS * g + emp], w);
+                        atomicAdd(&lcnt[GS * g + ((u32)emp ^ sw)], w);
                         *claimed = old == 0ull;
                         return true;
                     }
@@ -2244,8 +2256,9 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                     } else if constexpr (W == 1) {
                         if ((a.lcap & 3u) == 0) {
                             const u32 g = (u32)((fr * (u64)(a.lcap >> 2)) >> 48);
-                            const lds_v2u64* gp = (const lds_v2u64*)(lkeys + 4 * g);
-                            const v2u64 a0 = gp[0], a1 = gp[1];
+                            const u32 sw = gswz(g);
+                            const v2u64 a0 = *(const lds_v2u64*)(lkeys + 4 * g + sw);
+                            const v2u64 a1 = *(const lds_v2u64*)(lkeys + 4 * g + (2u ^ sw));
                             const u64 v[4] = {a0.x, a0.y, a1.x, a1.y};
                             int hit = -1, emp = -1;
 #pragma unroll
@@ -2254,7 +2267,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_buckets(BucketArgs a) {
                                 if (v[i] == 0ull) emp = i;
                             }
                             found = want && hit >= 0 && (emp < 0 || hit < emp);
-                            if (found) atomicAdd(&lcnt[4 * g + hit], 1u);
+                            if (found) atomicAdd(&lcnt[4 * g + ((u32)hit ^ sw)], 1u);
                         }
                     } else {
                         const u32 sl = (u32)((fr * (u64)a.lcap) >> 48);
@@ -4480,6 +4493,12 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
             x = make_uint4((u32)y0, (u32)(y0 >> 32), 0u, 0u);  // bytes 8..15: no newline
         }
     };
+    // a newline mask of 64 staged bytes limited to the block's bytes
+    auto trim = [&](u64 m, long long rel0) -> u64 {
+        if (rel0 < 0) m = (rel0 <= -64) ? 0ull : (m & (~0ull << (u32)(-rel0)));
+        if (rel0 + 64 > (long long)n) m = (rel0 >= (long long)n) ? 0ull : (m & (~0ull >> (u32)(rel0 + 64 - (long long)n)));
+        return m;
+    };
     u64 c = (u64)blockIdx.x * kFqEncWaves + wave;
     int h = 0;
     u64 run = 0;
@@ -4543,8 +4562,7 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
             for (int rd = 0; rd < kFqRounds; rd++) {
                 u64 m = mk[rd];
                 const long long rel0 = hrel + rd * 4096 + lane * 64;
-                if (rel0 < 0) m = (rel0 <= -64) ? 0ull : (m & (~0ull << (u32)(-rel0)));
-                if (rel0 + 64 > (long long)n) m = (rel0 >= (long long)n) ? 0ull : (m & (~0ull >> (u32)(rel0 + 64 - (long long)n)));
+                m = trim(m, rel0);
                 const u32 cnt = (u32)__popcll(m);
                 u32 ex = 0, tot = 0;
                 if (__ballot(cnt > 7u) == 0ull) {

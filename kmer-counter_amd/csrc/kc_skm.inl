@@ -1948,9 +1948,11 @@ struct SkmBucketArgs {
     // bucket's own records (multiplicity 1)
     const u32* dcnt;
     const u32* dlen;
+    const u64* dpos;  // kOverList buckets: their list's start
 };
 
 constexpr u32 kRawList = 0xffffffffu;  // P5a: bucket not deduplicated
+constexpr u32 kOverList = 0x80000000u;  // P5a: dlen flag, the list is at dpos[b] (overflow list), not at the bucket's start
 
 // key i of a record (see the record layout above)
 template <int W>
@@ -2167,8 +2169,8 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
             *rp = a.recs;
             *st = a.stride;
             *cp = a.dcnt;
-            *l0 = starts_r[bb];
-            *h0 = *l0 + dl;
+            *l0 = (dl & kOverList) ? a.dpos[bb] : starts_r[bb];  // overflow list: in the pool's tail
+            *h0 = *l0 + (dl & ~kOverList);
         } else {
             *rp = a.recs;
             *st = a.stride;
@@ -2331,17 +2333,18 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                     u64 key = win[0] & a.last_mask;
                     u32 kw = wcur;
                     bool act = s0 < s1;
+                    // (group halves swizzled: logical slot j at kSkmGroup g + (j ^ gswz(g)))
                     u32 g = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key), ng);
-                    v2u64 a0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[0];
-                    v2u64 a1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g))[1];
+                    v2u64 a0 = *(const lds_v2u64*)(lkeys + kSkmGroup * g + gswz(g));
+                    v2u64 a1 = *(const lds_v2u64*)(lkeys + kSkmGroup * g + (2u ^ gswz(g)));
                     for (u32 t = 0; t < per; t++) {
                         advance(t);
                         const bool act_n = s0 + t + 1 < s1;
                         const u64 key_n = win[0] & a.last_mask;
                         const u32 kw_n = wcur;
                         const u32 g_n = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key_n), ng);
-                        const v2u64 b0 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[0];
-                        const v2u64 b1 = ((const lds_v2u64*)(lkeys + kSkmGroup * g_n))[1];
+                        const v2u64 b0 = *(const lds_v2u64*)(lkeys + kSkmGroup * g_n + gswz(g_n));
+                        const v2u64 b1 = *(const lds_v2u64*)(lkeys + kSkmGroup * g_n + (2u ^ gswz(g_n)));
                         bool want = act && !a.skip;
                         want = want && ((u32)(key >> msh) & (m - 1u)) == sub;
                         my_keys += want ? 1u : 0u;
@@ -2350,7 +2353,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                         const bool e0 = a0.x == key, e1 = a0.y == key, e2 = a1.x == key, e3 = a1.y == key;
                         const int hit = e0 ? 0 : (e1 ? 1 : (e2 ? 2 : 3));
                         const bool found = want && (e0 || e1 || e2 || e3);
-                        if (found) atomicAdd(&lcnt[kSkmGroup * g + hit], kw);
+                        if (found) atomicAdd(&lcnt[kSkmGroup * g + ((u32)hit ^ gswz(g))], kw);
                         bool pend = want && !found;
                         if constexpr (KC_P5_CLAIM) {
                             // a new key takes the first empty slot of its home
@@ -2359,7 +2362,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                             // a lost race goes to the slow path
                             const bool z0 = a0.x == 0ull, z1 = a0.y == 0ull, z2 = a1.x == 0ull, z3 = a1.y == 0ull;
                             if (pend && (z0 || z1 || z2 || z3)) {
-                                const u32 sl = kSkmGroup * g + (z0 ? 0u : (z1 ? 1u : (z2 ? 2u : 3u)));
+                                const u32 sl = kSkmGroup * g + ((z0 ? 0u : (z1 ? 1u : (z2 ? 2u : 3u))) ^ gswz(g));
                                 const u64 old = atomicCAS((unsigned long long*)&lkeys[sl], 0ull, (unsigned long long)key);
                                 if (old == 0ull || old == key) {
                                     atomicAdd(&lcnt[sl], kw);
@@ -2566,6 +2569,7 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
     SkmBucketArgs a;
     a.dcnt = dd ? dd->cnt : nullptr;
     a.dlen = dd ? dd->len : nullptr;
+    a.dpos = dd ? dd->pos : nullptr;
     a.skip = experiment_knob("KC_P5_SKIP");
     const bool mask_last = ((k + 3) / 4) < 8 * W;
     a.last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
@@ -2627,6 +2631,7 @@ constexpr int kRecPd = KC_P5A_PD;  // P5a: record batches in flight per wave
 #endif
 constexpr int kRecBlock = KC_P5A_BLOCK;
 constexpr int kRecWaves = kRecBlock / 64;
+constexpr u32 kRecMaxSplit = 16;  // P5a: most hash-split passes of an overflowing bucket
 
 struct RecDedupArgs {
     u64* recs;  // 2 x stride (SoA), grouped by bucket; distinct records written back in place
@@ -2636,6 +2641,14 @@ struct RecDedupArgs {
     u32 ngrp;  // LDS groups of 2 entries
     u32* cnt;  // multiplicities, indexed like recs
     u32* dlen;
+    // overflow lists: a bucket whose distinct records overflow the table is
+    // deduplicated again in 2, 4, .. kRecMaxSplit passes, each taking the
+    // records of one hash class, into a list reserved in the pool's free tail
+    // [*over_cursor, over_limit) of recs (and cnt); dpos[b] = its start,
+    // dlen[b] = kOverList | its length. over_cursor == nullptr: raw instead
+    u64* over_cursor;
+    u64 over_limit;
+    u64* dpos;
 };
 
 __device__ __forceinline__ u32 rec_hash(u64 k0, u64 k1) {
@@ -2661,7 +2674,7 @@ __global__ __launch_bounds__(kRecBlock) void count_rec_k(RecDedupArgs a, const u
     u64* tab = (u64*)smem;                        // entry e: tab[2e] = marked word 0, tab[2e + 1] = word 1
     u32* cnt = (u32*)(tab + 4 * (size_t)a.ngrp);  // 2 ngrp
     u32* misc = cnt + 2 * (size_t)a.ngrp;         // [0] overflow, [1..16] wave totals, [17] write-back cursor,
-                                                  // [18] claims listed
+                                                  // [18] claims listed, [20..21] overflow list start (u64)
     unsigned short* clist = (unsigned short*)(misc + 64);  // entries in claim order (kRecClaims)
     const int tid = threadIdx.x, lane = (int)lane_id(), wave = tid >> 6;
     const u32 nent = 2 * a.ngrp;
@@ -2698,13 +2711,123 @@ __global__ __launch_bounds__(kRecBlock) void count_rec_k(RecDedupArgs a, const u
             n1[d] = i < whi ? __builtin_nontemporal_load(a.recs + a.stride + i) : 0ull;
         }
     };
+    // one record into the table (probing kRecProbe groups; a lost claim race
+    // reads the group again): false when it found no place
+    auto insert = [&](u64 k0, u64 k1, bool act, u32* claims) -> bool {
+        u32 g = __umulhi(rec_hash(k0, k1), a.ngrp);
+        bool done = !act;
+        for (int pr = 0; pr < kRecProbe; pr++) {
+            if (!__ballot(!done)) break;
+            if (!done) {
+                // (entry j of group g is entry 2g + (j ^ sw): the group's two
+                // 16-byte entries swap places in every other run of 8 groups,
+                // spreading a wave's loads over all 16 four-bank quads)
+                const u32 sw = gswz(g) >> 1;
+                const v2u64 e0 = *(const lds_v2u64*)(tab + 4 * (size_t)g + 2 * sw);
+                const v2u64 e1 = *(const lds_v2u64*)(tab + 4 * (size_t)g + 2 * (sw ^ 1u));
+                if (e0.x == k0 && e0.y == k1) {
+                    atomicAdd(&cnt[2 * g + sw], 1u);
+                    done = true;
+                } else if (e1.x == k0 && e1.y == k1) {
+                    atomicAdd(&cnt[2 * g + (sw ^ 1u)], 1u);
+                    done = true;
+                } else if (e0.x == 0ull || e1.x == 0ull) {
+                    const u32 e = e0.x == 0ull ? 2 * g + sw : 2 * g + (sw ^ 1u);
+                    const u64 old = atomicCAS((unsigned long long*)&tab[2 * (size_t)e], 0ull, (unsigned long long)k0);
+                    if (old == 0ull) {
+                        tab[2 * (size_t)e + 1] = k1;
+                        atomicAdd(&cnt[e], 1u);
+                        done = true;
+                        ++*claims;
+                        const u32 ci = atomicAdd(&misc[18], 1u);
+                        if (ci < kRecClaims) clist[ci] = (unsigned short)e;
+                    }
+                    // lost the entry: the group is read again
+                } else {
+                    g = g + 1 == a.ngrp ? 0 : g + 1;
+                }
+            }
+        }
+        return done;
+    };
+    // the table's distinct records (the entries taken) to recs / cnt from
+    // dst0 on, bucket bits b restored (put = false: only cleared); every
+    // entry is cleared. Returns their number. Ends with the table and the
+    // counters clear (two barriers inside).
+    auto write_back = [&](u32 b, u64 dst0, u32 claims, bool put) -> u32 {
+        for (int o2 = 32; o2 >= 1; o2 >>= 1) claims += (u32)__shfl_xor((int)claims, o2);
+        if (lane == 0) misc[1 + wave] = claims;
+        __syncthreads();
+        u32 total = 0;
+        for (int w = 0; w < kRecWaves; w++) total += misc[1 + w];
+        if (total <= kRecClaims) {
+            // the claimed entries in claim order: distinct record i goes to
+            // dst0 + i, its entry is cleared
+            for (u32 i = (u32)tid; i < total; i += kRecBlock) {
+                const u32 e = clist[i];
+                if (put) {
+                    const u64 q = dst0 + i;
+                    a.recs[q] = (tab[2 * (size_t)e] & kLow48) | ((u64)b << 48);
+                    a.recs[a.stride + q] = tab[2 * (size_t)e + 1];
+                    a.cnt[q] = cnt[e];
+                }
+                tab[2 * (size_t)e] = 0ull;
+                tab[2 * (size_t)e + 1] = 0ull;
+                cnt[e] = 0;
+            }
+        } else {
+            const u32 spw = (nent + kRecWaves - 1) / kRecWaves;
+            const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
+            for (u32 c0 = s0; c0 < s1; c0 += 64) {
+                const u32 i = c0 + (u32)lane;
+                const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
+                const u64 bm = __ballot(occ);
+                if (bm) {
+                    u32 wb = 0;
+                    if (lane == 0 && put) wb = atomicAdd(&misc[17], (u32)__popcll(bm));
+                    wb = (u32)__builtin_amdgcn_readfirstlane((int)wb);
+                    if (occ) {
+                        if (put) {
+                            const u64 q = dst0 + wb + (u64)__popcll(bm & lt);
+                            a.recs[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
+                            a.recs[a.stride + q] = tab[2 * (size_t)i + 1];
+                            a.cnt[q] = cnt[i];
+                        }
+                        tab[2 * (size_t)i] = 0ull;
+                        tab[2 * (size_t)i + 1] = 0ull;
+                        cnt[i] = 0;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            misc[0] = 0;
+            misc[17] = 0;
+            misc[18] = 0;
+        }
+        __syncthreads();
+        return total;
+    };
+    // buckets with more records than the table has entries: how many this
+    // workgroup has seen and how many of them held too many distinct records
+    // (uniform values); when most overflowed, such a bucket goes straight to
+    // the hash-split passes instead of a first attempt that fills the table
+    u32 big_seen = 0, big_over = 0;
+    bool room = true;  // the overflow lists' space was not found exhausted
     prefetch(a.b0 + blockIdx.x);
     for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x) {
         u64 wlo, whi;
         share(b, &wlo, &whi);
+        const u64 nrec_b = starts_r[b + 1] - starts_r[b];
+        const bool big = nrec_b > (u64)nent;
+        const bool skip_first = big && a.over_cursor && room && 2 * big_over > big_seen;
         bool over = false;
         u32 claims = 0;  // entries this lane took
-        for (u64 base = wlo; base < whi; base += 64) {
+        for (u64 base = wlo; base < whi && !skip_first; base += 64) {
+            // a full table (any wave) ends the attempt: the bucket is split
+            // or left raw, its remaining records are not needed now
+            if (__hip_atomic_load(&misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
             const bool act = base + lane < whi;
             const u64 k0 = (n0[0] & kLow48) | kMark, k1 = n1[0];
 #pragma unroll
@@ -2717,107 +2840,79 @@ __global__ __launch_bounds__(kRecBlock) void count_rec_k(RecDedupArgs a, const u
                 n0[kRecPd - 1] = i < whi ? __builtin_nontemporal_load(a.recs + i) : 0ull;
                 n1[kRecPd - 1] = i < whi ? __builtin_nontemporal_load(a.recs + a.stride + i) : 0ull;
             }
-            u32 g = __umulhi(rec_hash(k0, k1), a.ngrp);
-            bool done = !act;
-            for (int pr = 0; pr < kRecProbe; pr++) {
-                if (!__ballot(!done)) break;
-                if (!done) {
-                    const v2u64 e0 = ((const lds_v2u64*)(tab + 4 * (size_t)g))[0];
-                    const v2u64 e1 = ((const lds_v2u64*)(tab + 4 * (size_t)g))[1];
-                    if (e0.x == k0 && e0.y == k1) {
-                        atomicAdd(&cnt[2 * g], 1u);
-                        done = true;
-                    } else if (e1.x == k0 && e1.y == k1) {
-                        atomicAdd(&cnt[2 * g + 1], 1u);
-                        done = true;
-                    } else if (e0.x == 0ull || e1.x == 0ull) {
-                        const u32 e = e0.x == 0ull ? 2 * g : 2 * g + 1;
-                        const u64 old = atomicCAS((unsigned long long*)&tab[2 * (size_t)e], 0ull, (unsigned long long)k0);
-                        if (old == 0ull) {
-                            tab[2 * (size_t)e + 1] = k1;
-                            atomicAdd(&cnt[e], 1u);
-                            done = true;
-                            ++claims;
-                            const u32 ci = atomicAdd(&misc[18], 1u);
-                            if (ci < kRecClaims) clist[ci] = (unsigned short)e;
-                        }
-                        // lost the entry: the group is read again
-                    } else {
-                        g = g + 1 == a.ngrp ? 0 : g + 1;
-                    }
-                }
-            }
-            over |= !done;
+            over |= !insert(k0, k1, act, &claims);
+            if (__ballot(over) && lane == 0) atomicOr(&misc[0], 1u);
         }
-        if (__ballot(over) && lane == 0) atomicOr(&misc[0], 1u);
         __syncthreads();
         // every record of the bucket is in the table: the next bucket's first
         // batches go in flight, then the distinct records are written back
         prefetch(b + gridDim.x);
-        const bool raw = misc[0] != 0u;
-        // the distinct records = the entries taken (every taken entry holds a
-        // record); one pass over the table writes them back, each wave's
-        // occupied entries at positions from an LDS counter
-        for (int o2 = 32; o2 >= 1; o2 >>= 1) claims += (u32)__shfl_xor((int)claims, o2);
-        if (lane == 0) misc[1 + wave] = claims;
-        __syncthreads();
-        u32 total = 0;
-        for (int w = 0; w < kRecWaves; w++) total += misc[1 + w];
-        if (tid == 0) a.dlen[b] = raw ? kRawList : total;
+        const bool raw = skip_first || misc[0] != 0u;
         const u64 pos0 = starts_r[b];
-        if (total <= kRecClaims) {
-            // the claimed entries in claim order: distinct record i goes to
-            // pos0 + i, its entry is cleared
-            for (u32 i = (u32)tid; i < total; i += kRecBlock) {
-                const u32 e = clist[i];
-                if (!raw) {
-                    const u64 q = pos0 + i;
-                    a.recs[q] = (tab[2 * (size_t)e] & kLow48) | ((u64)b << 48);
-                    a.recs[a.stride + q] = tab[2 * (size_t)e + 1];
-                    a.cnt[q] = cnt[e];
-                }
-                tab[2 * (size_t)e] = 0ull;
-                tab[2 * (size_t)e + 1] = 0ull;
-                cnt[e] = 0;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                misc[0] = 0;
-                misc[18] = 0;
-            }
-            __syncthreads();
+        if (!raw) {
+            const u32 total = write_back(b, pos0, claims, true);
+            if (tid == 0) a.dlen[b] = total;
+            big_seen += big ? 1u : 0u;
             continue;
         }
-        const u32 spw = (nent + kRecWaves - 1) / kRecWaves;
-        const u32 s0 = (u32)wave * spw, s1 = min(nent, s0 + spw);
-        for (u32 c0 = s0; c0 < s1; c0 += 64) {
-            const u32 i = c0 + (u32)lane;
-            const bool occ = i < s1 && tab[2 * (size_t)i] != 0ull;
-            const u64 bm = __ballot(occ);
-            if (bm) {
-                u32 wb = 0;
-                if (lane == 0 && !raw) wb = atomicAdd(&misc[17], (u32)__popcll(bm));
-                wb = (u32)__builtin_amdgcn_readfirstlane((int)wb);
-                if (occ) {
-                    if (!raw) {
-                        const u64 q = pos0 + wb + (u64)__popcll(bm & lt);
-                        a.recs[q] = (tab[2 * (size_t)i] & kLow48) | ((u64)b << 48);
-                        a.recs[a.stride + q] = tab[2 * (size_t)i + 1];
-                        a.cnt[q] = cnt[i];
-                    }
-                    tab[2 * (size_t)i] = 0ull;
-                    tab[2 * (size_t)i + 1] = 0ull;
-                    cnt[i] = 0;
-                }
-            }
-        }
-        __syncthreads();
+        if (!skip_first) write_back(b, 0, claims, false);  // (clears the partial table)
+        // overflow: the bucket's records again, in m passes by hash class,
+        // into a list reserved in the pool's free tail (the bucket's own range
+        // must stay intact for the later passes)
+        const u64 nrec = starts_r[b + 1] - pos0;
         if (tid == 0) {
-            misc[0] = 0;
-            misc[17] = 0;
-            misc[18] = 0;
+            u64 at = ~0ull;
+            if (a.over_cursor) {
+                at = atomicAdd((unsigned long long*)a.over_cursor, (unsigned long long)nrec);
+                if (at + nrec > a.over_limit) at = ~0ull;  // no room: the bucket stays raw
+            }
+            *(u64*)(misc + 20) = at;
         }
         __syncthreads();
+        const u64 lst = *(const u64*)(misc + 20);
+        u32 m = 2, written = 0;
+        bool ok = lst != ~0ull;
+        room = room && ok;
+        while (ok) {
+            written = 0;
+            bool again = false;
+            for (u32 sub = 0; sub < m && !again; sub++) {
+                bool ov = false;
+                u32 cl = 0;
+                // the wave's share again, the next batch's records in flight
+                u64 p0 = wlo + lane < whi ? a.recs[wlo + lane] : 0ull;
+                u64 p1 = wlo + lane < whi ? a.recs[a.stride + wlo + lane] : 0ull;
+                for (u64 base = wlo; base < whi; base += 64) {
+                    if (__hip_atomic_load(&misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                    const bool in = base + lane < whi;
+                    const u64 r0 = p0, r1 = p1;
+                    const u64 i = base + 64 + lane;
+                    p0 = i < whi ? a.recs[i] : 0ull;
+                    p1 = i < whi ? a.recs[a.stride + i] : 0ull;
+                    const u64 k0 = (r0 & kLow48) | kMark;
+                    const bool act = in && (rec_hash(k0, r1) & (m - 1u)) == sub;
+                    ov |= !insert(k0, r1, act, &cl);
+                    if (__ballot(ov) && lane == 0) atomicOr(&misc[0], 1u);
+                }
+                __syncthreads();
+                again = misc[0] != 0u;
+                // (a pass that overflowed is cleared and the split doubles)
+                written += write_back(b, lst + written, cl, !again);
+            }
+            if (!again) break;
+            m *= 2;
+            ok = m <= kRecMaxSplit;
+        }
+        if (tid == 0) {
+            a.dlen[b] = ok ? (kOverList | written) : kRawList;
+            if (ok) a.dpos[b] = lst;
+        }
+        if (big) {
+            // (a skipped first attempt counts as an overflow only when the
+            // bucket's distinct records would not have fit the table)
+            big_seen++;
+            big_over += (!skip_first || !ok || written > nent - nent / 8) ? 1u : 0u;
+        }
     }
 }
 
@@ -2825,7 +2920,7 @@ __global__ __launch_bounds__(kBlock) void dedup_total_k(const u32* __restrict__ 
                                                        u32 nb, u64* stats) {
     u64 v = 0;
     for (u32 b = blockIdx.x * kBlock + threadIdx.x; b < nb; b += gridDim.x * kBlock)
-        v += dlen[b] == kRawList ? starts[b + 1] - starts[b] : (u64)dlen[b];
+        v += dlen[b] == kRawList ? starts[b + 1] - starts[b] : (u64)(dlen[b] & ~kOverList);
     wave_add(&stats[ST_DEDUP], v);
 }
 
@@ -2836,9 +2931,13 @@ hipError_t launch_dedup_total(const uint32_t* dlen, const uint64_t* starts, uint
 }
 
 hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
-                            uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s) {
+                            uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s, uint64_t* over_cursor,
+                            uint64_t over_limit, uint64_t* dpos) {
     if (b1 <= b0) return hipSuccess;
     RecDedupArgs a;
+    a.over_cursor = test_hook("KC_P5A_NO_SPLIT") ? nullptr : over_cursor;
+    a.over_limit = over_limit;
+    a.dpos = dpos;
     a.recs = recs;
     a.stride = stride;
     a.starts = starts;

@@ -1,6 +1,7 @@
-"""GPU parity of the fused FASTQ index + encode pass (fq_encode_k, one text
-read for K1 emit + E) against the two-pass path (fq_emit_k + fq_validate_k +
-encode_reads_k, forced with KC_NO_FQ_ENCODE=1) and the CPU oracle: identical
+"""GPU parity of the FASTQ index + encode passes against each other and the
+CPU oracle: the fused index after fq_count_k (fq_encode_k, one text read for
+K1 emit + E; the default) and the two-pass path (fq_emit_k + fq_validate_k +
+encode_reads_k, KC_NO_FQ_ENCODE=1): identical
 SortedKMerFile bytes on well-formed blocks whose records straddle the kernel's
 8 KiB halves and 16 KiB chunks (headers of 1..400 bytes, reads of 18..3000
 bases: past the staged KiB the groups come from global memory), and the same
@@ -23,10 +24,16 @@ def _block(n, L, seed, n_rate=0.01, hdr_max=60):
     return out
 
 
-def _count(kca, fq, k, L, fused, monkeypatch, engine="auto"):
-    if fused:
-        monkeypatch.delenv("KC_NO_FQ_ENCODE", raising=False)
-    else:
+MODES = ("fused", "twopass")
+
+
+def _count(kca, fq, k, L, mode, monkeypatch, engine="auto"):
+    if mode is True:
+        mode = "fused"
+    elif mode is False:
+        mode = "twopass"
+    monkeypatch.delenv("KC_NO_FQ_ENCODE", raising=False)
+    if mode == "twopass":
         monkeypatch.setenv("KC_NO_FQ_ENCODE", "1")
     with kca.Context(kmer_length=k, line_length=L, engine=engine) as ctx:
         n = ctx.count_fastq(fq)
@@ -38,11 +45,19 @@ def _count(kca, fq, k, L, fused, monkeypatch, engine="auto"):
 def test_fused_matches_two_pass_and_oracle(kca, orc, monkeypatch, k, L, hdr):
     n = max(50, 600_000 // (2 * L + hdr))
     fq = "".join(_block(n, L, seed=k * 7 + L, hdr_max=hdr)).encode()
-    n1, got = _count(kca, fq, k, L, True, monkeypatch)
-    n2, ref = _count(kca, fq, k, L, False, monkeypatch)
-    assert n1 == n2 == n
-    assert got == ref
-    assert got == orc.count_fastq(fq, k)
+    want = orc.count_fastq(fq, k)
+    for mode in MODES:
+        assert _count(kca, fq, k, L, mode, monkeypatch) == (n, want), mode
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 51, 52, 53, 3000, 61000])
+def test_fused_index_block_sizes(kca, orc, monkeypatch, n):
+    """Blocks from one record (one chunk, one half) to ~1,200 chunks: a block
+    ending inside a chunk's first half or right at a chunk edge."""
+    fq = kca.synth_fastq(n, 150, seed=40 + n, genome_length=200_000, n_rate=0.001)
+    want = orc.count_fastq(fq, 31)
+    for mode in MODES:
+        assert _count(kca, fq, 31, 150, mode, monkeypatch) == (n, want), mode
 
 
 @pytest.mark.parametrize("engine", ["skm", "partition"])
@@ -102,21 +117,20 @@ def test_fused_rejects_like_two_pass(kca, monkeypatch, name, at):
     _mutations()[name](recs, i)
     fq = "".join(recs).encode()
     verdict = []
-    for fused in (True, False):
+    for mode in MODES:
         try:
-            _count(kca, fq, k, L, fused, monkeypatch)
+            _count(kca, fq, k, L, mode, monkeypatch)
             verdict.append("ok")
         except kca.KcError as e:
             verdict.append(e.status)
-    assert verdict[0] == verdict[1]
-    assert verdict[0] == kca.KC_ERR_FORMAT
+    assert verdict == [kca.KC_ERR_FORMAT] * len(MODES)
 
 
 def test_fused_no_final_newline_and_empty_tail(kca, monkeypatch):
     recs = _block(500, 150, seed=4)
     fq = "".join(recs).encode()
-    for fused in (True, False):
+    for mode in MODES:
         with pytest.raises(kca.KcError):
-            _count(kca, fq[:-1], 31, 150, fused, monkeypatch)
+            _count(kca, fq[:-1], 31, 150, mode, monkeypatch)
     n, got = _count(kca, fq, 31, 150, True, monkeypatch)
     assert n == 500

@@ -305,13 +305,22 @@ def test_skm_front3_lengths_multiple_of_16(kca, orc, L):
     assert got == orc.count_fastq(fq, k)
 
 
-@pytest.mark.parametrize("groups", [None, "64", "3"])
+@pytest.mark.parametrize("groups", [None, "64", "3", "64:nosplit", "8:room"])
 def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
-    """P5a: genome reads at ~20x, where most records repeat; with a small
-    record table (KC_P5A_GROUPS) buckets overflow it and P5 walks their own
-    records (kRawList); KC_NO_DEDUP walks every bucket's own records."""
+    """P5a: genome reads at ~20x, where most records repeat. With a small
+    record table (KC_P5A_GROUPS) buckets overflow it: they are deduplicated
+    again in 2..16 hash-split passes into overflow lists in the pool's free
+    tail (dpos / kOverList), or, when the split still overflows (3 groups),
+    with no splitting (KC_P5A_NO_SPLIT) or once the tail is full
+    (KC_P5A_OVER_ROOM), P5 walks their own records (kRawList); KC_NO_DEDUP
+    walks every bucket's own records."""
     if groups:
-        monkeypatch.setenv("KC_P5A_GROUPS", groups)
+        g, _, mode = groups.partition(":")
+        monkeypatch.setenv("KC_P5A_GROUPS", g)
+        if mode == "nosplit":
+            monkeypatch.setenv("KC_P5A_NO_SPLIT", "1")
+        if mode == "room":
+            monkeypatch.setenv("KC_P5A_OVER_ROOM", "20000")
     fq = kca.synth_fastq(60000, 150, seed=33, genome_length=400_000, n_rate=0.0005)
     with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
         ctx.count_fastq(fq)
@@ -321,6 +330,9 @@ def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
     with kca.Context(kmer_length=31, line_length=150, engine="skm") as ctx:
         ctx.count_fastq(fq)
         raw = ctx.records()
+        st_raw = ctx.stats()
+    if groups in ("64", "8:room"):
+        assert st["dedup_records"] < st_raw["keys"]  # overflow lists deduplicated records
     assert got == raw
     assert got == orc.count_fastq(fq, 31)
     assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
