@@ -788,8 +788,10 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         const uint64_t* p2_base = (const uint64_t*)(from_u ? c->part_base2.p : c->part_base.p);
         uint64_t n = from_u ? kp_u_n : 0;
         if (!from_u) {
+            // (the second pass's keys are read by the regional scatter only:
+            // builds whose P3 tile differs from its tile take p3_scatter_k)
             const bool dual = kpass && kp_direct && kpi + 2 < kp.size() && !test_hook("KC_NO_DUAL_PASS") &&
-                              !test_hook("KC_P3_SCATTER");
+                              !test_hook("KC_P3_SCATTER") && p3_tile(W) == rp_tile(W, false);
             if (dual && (s = ensure(c, c->part_base2, hn * 8))) return s;
             HIPCHK(c, hipEventRecord(c->ev0, c->stream));
             if (pre0 < 0)

@@ -2631,6 +2631,7 @@ constexpr int kRecPd = KC_P5A_PD;  // P5a: record batches in flight per wave
 #endif
 constexpr int kRecBlock = KC_P5A_BLOCK;
 constexpr int kRecWaves = kRecBlock / 64;
+static_assert(KC_P5A_LDS <= 160 * 1024 && (160 * 1024) / KC_P5A_LDS >= 1, "P5a LDS per workgroup: at most a CU's");
 constexpr u32 kRecMaxSplit = 16;  // P5a: most hash-split passes of an overflowing bucket
 
 struct RecDedupArgs {

@@ -597,6 +597,29 @@ def test_presplit_buckets_high_cardinality(kca, orc, monkeypatch, k):
     assert outs[0] == outs[1] == outs[2] == outs[3] == orc.count_fastq(fq, k)
 
 
+@pytest.mark.parametrize("knob", ["KC_P2_SOA", "KC_P3_SOA", "KC_P3B_SOA", "KC_P2_NO_DIGS", "KC_P3_SCATTER",
+                                  "KC_NO_DUAL_PASS"])
+@pytest.mark.parametrize("k", [31, 55])
+def test_layout_knobs_same_counts(kca, orc, monkeypatch, knob, k):
+    """The key-prefix engine's layout and path knobs (word arrays instead of
+    AoS keys from P2 / P3 / P3b, P3b's histogram from word 0 instead of P3's
+    digit bytes, the older P3 scatter, no dual key-range walk) are documented
+    as giving the same counts: each alone, on high-cardinality reads counted
+    in batches with P3b, and through key-range passes, against the oracle."""
+    monkeypatch.setenv("KC_P3B_MIN", "1")
+    monkeypatch.setenv(knob, "1")
+    fq = kca.synth_fastq(30000, 150, seed=k + 5, n_rate=0.0005)
+    want = orc.count_fastq(fq, k)
+    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=24 << 20, engine="partition") as ctx:
+        ctx.count_fastq(fq)
+        assert ctx.records() == want
+        assert ctx.stats()["presplit_batches"] >= 1 or knob == "KC_NO_P3B"
+    monkeypatch.setenv("KC_KEY_PASSES_MIN", "2")
+    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=24 << 20, engine="partition") as ctx:
+        ctx.count_fastq(fq)
+        assert ctx.records() == want
+
+
 @pytest.mark.parametrize("k", [31, 55])
 def test_direct_runs_with_equal_keys(kca, orc, monkeypatch, capfd, k):
     """P5s direct mode on batches whose runs hold equal keys (a fifth of the
