@@ -92,6 +92,8 @@ struct kc_ctx {
     // P5 segment descriptors (see finish_part_sorted) and their sort scratch
     DevBuf desc_key, desc_start, desc_len, desc_k2, desc_v, desc_v2, desc_lens, desc_offs, desc_fb;
     uint64_t* rec_keys = nullptr;  // W x rec_cap
+    uint8_t* rec_dig = nullptr;    // rec_cap: word 0 bits 48..55 of each record the skm P5 wrote (the
+                                   // finish's first grouping digit, read as 1 B instead of word 0)
     uint32_t* rec_cnts = nullptr;
     uint64_t rec_cap = 0;
     uint64_t* rec_cursor = nullptr;  // device u64
@@ -499,19 +501,24 @@ static kc_status grow_records(kc_ctx* c, uint64_t need) {
     const int W = c->W;
     uint64_t* nk = nullptr;
     uint32_t* nc = nullptr;
+    uint8_t* nd = nullptr;
     HIPCHK(c, hipMalloc((void**)&nk, (size_t)W * ncap * 8));
     HIPCHK(c, hipMalloc((void**)&nc, (size_t)ncap * 4));
+    HIPCHK(c, hipMalloc((void**)&nd, (size_t)ncap + 16));
     if (c->rec_n) {
         for (int j = 0; j < W; j++)
             HIPCHK(c, hipMemcpyAsync(nk + (size_t)j * ncap, c->rec_keys + (size_t)j * c->rec_cap, c->rec_n * 8,
                                      hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(nc, c->rec_cnts, c->rec_n * 4, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(nd, c->rec_dig, c->rec_n, hipMemcpyDeviceToDevice, c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->rec_keys) HIPCHK(c, hipFree(c->rec_keys));
     if (c->rec_cnts) HIPCHK(c, hipFree(c->rec_cnts));
+    if (c->rec_dig) HIPCHK(c, hipFree(c->rec_dig));
     c->rec_keys = nk;
     c->rec_cnts = nc;
+    c->rec_dig = nd;
     c->rec_cap = ncap;
     return KC_OK;
 }
@@ -1413,7 +1420,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                                                b0, b1, count_keys, c->rec_keys, c->rec_cnts, c->rec_cap,
                                                c->rec_cursor, c->table, c->cap, c->keys_b, c->key_cap, c->stats,
                                                l.probe_limit, c->cfg.lds_slots, c->n_cu, c->stream,
-                                               dedup ? &dd : nullptr));
+                                               dedup ? &dd : nullptr, c->rec_dig));
                     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                     HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
                     if ((s2 = sync_stats(c))) return s2;
@@ -1534,34 +1541,28 @@ static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t p
     int rb = 8;
     while (rb < 24 && (aligned >> rb) > (1ull << 18)) rb++;
     const uint64_t cap = (aligned >> rb) * 2 + 4096;  // twice the expected samples
-    if ((s = ensure(c, c->fin_keys[0], cap * 8 + 64)) || (s = ensure(c, c->fin_keys[1], cap * 8 + 64)) ||
+    // the distinct samples are counted in a set of at least 2 x cap slots
+    int set_bits = 1;
+    while ((1ull << set_bits) < 2 * cap) set_bits++;
+    const size_t set_bytes = ((size_t)8 << set_bits);
+    if ((s = ensure(c, c->fin_keys[0], cap * 8 + 64)) || (s = ensure(c, c->fin_keys[1], set_bytes)) ||
         (s = ensure(c, c->fin_misc, 64)))
         return s;
     uint64_t* fp = (uint64_t*)c->fin_keys[0].p;
-    uint64_t* counter = (uint64_t*)c->fin_misc.p;
-    HIPCHK(c, hipMemsetAsync(counter, 0, 8, c->stream));
+    uint64_t* counter = (uint64_t*)c->fin_misc.p;  // [0] samples, [1] distinct samples
+    HIPCHK(c, hipMemsetAsync(counter, 0, 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->fin_keys[1].p, 0, set_bytes, c->stream));
     HIPCHK(c, launch_sketch((const uint32_t*)c->part_codes.p + (uint64_t)pre0 * G,
                             (const uint16_t*)c->part_inval.p + (uint64_t)pre0 * G, n_reads, (int)L, (int)c->k, rb, fp,
                             cap, counter, c->stream));
-    uint64_t m = 0;
-    HIPCHK(c, hipMemcpyAsync(&m, counter, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, launch_sketch_distinct(fp, counter, cap, (uint64_t*)c->fin_keys[1].p, set_bits, counter + 1, c->stream));
+    uint64_t md[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(md, counter, 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t m = md[0];
     if (m > cap) m = cap;
     if (m < 4096) return KC_OK;  // too few samples to tell: the skm engine's own sample decides
-    int which = 0;
-    if ((s = sort_records(c, fp, (uint64_t*)c->fin_keys[1].p, nullptr, nullptr, cap, m, &which, 1))) return s;
-    const uint64_t* sorted = (const uint64_t*)c->fin_keys[which].p;
-    if ((s = ensure(c, c->rle_flags, m * 4)) || (s = ensure(c, c->rle_pos, m * 4)) ||
-        (s = ensure(c, c->rle_tmp, scan_tmp_elems(m) * 4)))
-        return s;
-    HIPCHK(c, launch_rle_heads(1, sorted, cap, m, (uint32_t*)c->rle_flags.p, c->stream));
-    HIPCHK(c, launch_scan_u32((uint32_t*)c->rle_flags.p, (uint32_t*)c->rle_pos.p, m, (uint32_t*)c->rle_tmp.p,
-                              c->stream));
-    uint32_t last[2];
-    HIPCHK(c, hipMemcpyAsync(&last[0], (uint32_t*)c->rle_pos.p + (m - 1), 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&last[1], (uint32_t*)c->rle_flags.p + (m - 1), 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    const uint64_t distinct = (uint64_t)last[0] + last[1];
+    const uint64_t distinct = md[1];
     if (getenv("KC_DEBUG"))
         fprintf(stderr, "kc: sketch %llu distinct / %llu sampled k-mers\n", (unsigned long long)distinct,
                 (unsigned long long)m);
@@ -1802,7 +1803,7 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
                               uint64_t* n_rec_out, bool two_pass = false) {
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
-    if ((s = ensure(c, c->fq_counts, nch * 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
+    if ((s = ensure(c, c->fq_counts, nch * 8 + 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
         (s = ensure(c, c->fq_tmp, scan_tmp_elems(nch) * 8)))
         return s;
     if ((s = sync_stats(c))) return s;
@@ -1821,11 +1822,12 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     HIPCHK(c, launch_fq_count(base, n, (uint64_t*)c->fq_counts.p, c->stream));
     HIPCHK(c, launch_scan_u64((uint64_t*)c->fq_counts.p, (uint64_t*)c->fq_base.p, nch, (uint64_t*)c->fq_tmp.p,
                               c->stream));
-    uint64_t tail[2];
-    HIPCHK(c, hipMemcpyAsync(&tail[0], (uint64_t*)c->fq_base.p + nch - 1, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&tail[1], (uint64_t*)c->fq_counts.p + nch - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    // the line count (last chunk's base + count, summed on the device: one readback)
+    uint64_t* total = (uint64_t*)c->fq_counts.p + nch;
+    HIPCHK(c, launch_sum_last((const uint64_t*)c->fq_base.p, (const uint64_t*)c->fq_counts.p, nch, total, c->stream));
+    uint64_t lines = 0;
+    HIPCHK(c, hipMemcpyAsync(&lines, total, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const uint64_t lines = tail[0] + tail[1];
     if (lines % 4 != 0)
         return fail(c, KC_ERR_FORMAT, "FASTQ block has %llu lines, not a multiple of 4", (unsigned long long)lines);
     const uint64_t n_rec = lines / 4;
@@ -2047,6 +2049,7 @@ void kc_destroy(kc_ctx* c) {
     if (c->keys_b) (void)hipFree(c->keys_b);
     if (c->digs) (void)hipFree(c->digs);
     if (c->rec_keys) (void)hipFree(c->rec_keys);
+    if (c->rec_dig) (void)hipFree(c->rec_dig);
     if (c->rec_cnts) (void)hipFree(c->rec_cnts);
     if (c->rec_cursor) (void)hipFree(c->rec_cursor);
     if (c->pool_cursor) (void)hipFree(c->pool_cursor);
@@ -2668,8 +2671,9 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
     const uint64_t nrec = c->rec_n;
     const uint64_t claimed = c->stats_h[ST_CLAIMED];
     if ((s = grow_records(c, nrec + claimed + 1))) return s;
-    if ((s = ensure(c, c->fin_misc, (2 * W + 1 + compact_tmp_elems()) * 8))) return s;
+    if ((s = ensure(c, c->fin_misc, (2 * W + 2 + compact_tmp_elems()) * 8))) return s;
     uint64_t* cursor = (uint64_t*)c->fin_misc.p + 2 * W;
+    uint64_t* longest = cursor + 1 + compact_tmp_elems();
     uint64_t t = 0;
     if (claimed) {
         HIPCHK(c, launch_compact(W, c->table, c->cap, c->rec_keys + nrec, c->rec_cnts + nrec, c->rec_cap, cursor,
@@ -2677,7 +2681,7 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
         HIPCHK(c, hipMemcpyAsync(&t, cursor, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    uint64_t cur = nrec + t;
+    const uint64_t cur = nrec + t;  // (kept alive until the stream is synchronised below)
     HIPCHK(c, hipMemcpyAsync(cursor, &cur, 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, launch_append_key0(W, c->rec_keys, c->rec_cnts, c->rec_cap, cursor, c->stats, c->stream));
     uint64_t n = 0;
@@ -2693,31 +2697,34 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
     uint32_t* c0 = (uint32_t*)c->fin_cnts[0].p;
     const uint32_t nb = 1u << kBucketBits;
     bool grouped = n >= nb && n <= c->key_cap && !test_hook("KC_NO_SEGSORT");
-    std::vector<uint64_t> st;
     if (grouped) {
+        // only the skm engine wrote records since the reset: P5 wrote their
+        // first grouping digit (rec_dig), the table's and key 0's (appended
+        // above) are added here, and the first pass reads 1 B per record
+        const bool dig1 = c->engines_used == 1 && c->rec_dig && !test_hook("KC_NO_REC_DIG");
+        if (dig1 && n > nrec)
+            HIPCHK(c, launch_key_digits(c->rec_keys, nrec, n, 48, c->rec_dig, c->stream));
         double gm[2] = {0, 0};
         if ((s = group16(c, W, true, c->rec_keys, c->rec_cap, c->rec_cnts, (uint64_t*)c->fin_keys[1].p, out_cap,
-                         (uint32_t*)c->fin_cnts[1].p, c->digs, n, gm)))
+                         (uint32_t*)c->fin_cnts[1].p, c->digs, n, gm, dig1 ? c->rec_dig : nullptr)))
             return s;
-        if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8))) return s;
+        if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8)) || (s = ensure(c, c->desc_v, (size_t)nb * 4)) ||
+            (s = ensure(c, c->desc_len, (size_t)nb * 4)) || (s = ensure(c, c->desc_fb, (size_t)nb * 4 + 16)))
+            return s;
         HIPCHK(c, launch_bucket_bounds(W, c->rec_keys, c->rec_cap, n, kBucketBits, (uint64_t*)c->part_starts.p,
                                        c->stream));
-        st.resize((size_t)nb + 1);
-        HIPCHK(c, hipMemcpyAsync(st.data(), c->part_starts.p, st.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        // the groups' descriptors (digit: word0 bits 36..47, the 12 bits below
+        // the 16-bit group prefix) built on the device; only the longest
+        // group's length comes back
+        HIPCHK(c, hipMemsetAsync(longest, 0, 8, c->stream));
+        HIPCHK(c, launch_group_desc((const uint64_t*)c->part_starts.p, nb, 36u, (uint32_t*)c->desc_v.p,
+                                    (uint32_t*)c->desc_len.p, longest, c->stream));
         uint64_t mx = 0;
-        for (uint32_t b = 0; b < nb; b++) mx = std::max(mx, st[b + 1] - st[b]);
+        HIPCHK(c, hipMemcpyAsync(&mx, longest, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
         if (mx > (uint64_t)seg_sort_cap(W)) grouped = false;
     }
     if (grouped) {
-        if ((s = ensure(c, c->desc_v, (size_t)nb * 4)) || (s = ensure(c, c->desc_len, (size_t)nb * 4)) ||
-            (s = ensure(c, c->desc_fb, (size_t)nb * 4 + 16)))
-            return s;
-        std::vector<uint32_t> lens(nb);
-        // digit: word0 bits 36..47 (the 12 bits below the 16-bit group prefix)
-        for (uint32_t b = 0; b < nb; b++) lens[b] = (uint32_t)(st[b + 1] - st[b]) | (36u << 24);
-        HIPCHK(c, hipMemcpyAsync(c->desc_len.p, lens.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, launch_iota_u32((uint32_t*)c->desc_v.p, nb, c->stream));
         uint64_t* fb_n = (uint64_t*)((char*)c->desc_fb.p + (size_t)nb * 4);
         // one batch, no table records: keys are distinct, so the groups are
         // sorted straight into the packed output

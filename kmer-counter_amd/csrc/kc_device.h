@@ -196,6 +196,15 @@ hipError_t launch_desc_prep(const uint32_t* order, const uint32_t* len, uint64_t
                             hipStream_t s);
 size_t seg_sort_lds(int W);
 hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s);
+// out[i] = (keys[i] >> shift) & 255 for i in [lo, hi) (word 0 of SoA records)
+hipError_t launch_key_digits(const uint64_t* keys, uint64_t lo, uint64_t hi, int shift, uint8_t* out, hipStream_t s);
+// *out = base[n - 1] + counts[n - 1] (an exclusive scan's total), n >= 1
+hipError_t launch_sum_last(const uint64_t* base, const uint64_t* counts, uint64_t n, uint64_t* out, hipStream_t s);
+// seg_sort descriptors of ng groups from their bounds starts[0..ng]: order =
+// identity, len = length | tag << 24; *longest (zeroed by the caller) = the
+// longest group
+hipError_t launch_group_desc(const uint64_t* starts, uint64_t ng, uint32_t tag, uint32_t* order, uint32_t* len,
+                             uint64_t* longest, hipStream_t s);
 // fb: ndesc u32 + fb_n: 1 u64 of scratch (the LSD fallback list). With
 // `packed`, records go straight to SortedKMerFile layout there (okeys/ocnts
 // unused).
@@ -354,7 +363,7 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
                             uint32_t b0, uint32_t b1, bool count_keys, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
                             uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s,
-                            const SkmDedup* dd = nullptr);
+                            const SkmDedup* dd = nullptr, uint8_t* rec_dig = nullptr);
 
 // Synthetic FASTQ generator (bench/test input).
 struct SynthArgs {
@@ -369,6 +378,11 @@ struct SynthArgs {
 // (cap), count in *counter
 hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t n_reads, int L, int k, int rate_bits,
                          uint64_t* out, uint64_t cap, uint64_t* counter, hipStream_t s);
+// Distinct fingerprints among the first min(*counter, cap) of fp, counted by
+// inserting them into `set` (2^set_bits zeroed u64 slots, cap <= half of them);
+// the count is added to *distinct
+hipError_t launch_sketch_distinct(const uint64_t* fp, const uint64_t* counter, uint64_t cap, uint64_t* set,
+                                  int set_bits, uint64_t* distinct, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, char* out, hipStream_t s);
 void synth_host(const SynthArgs& a, char* out);
 uint64_t synth_bytes(uint64_t first, uint64_t n, int64_t L, int layout);

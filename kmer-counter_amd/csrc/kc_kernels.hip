@@ -1222,7 +1222,13 @@ hipError_t launch_hist_group_totals(const uint64_t* h, uint64_t nseg, uint32_t g
 template <typename T>
 static hipError_t scan_impl(const T* in, T* out, u64 n, T* tmp, hipStream_t s);
 
-__global__ void sum_last(const u64* base, const u64* counts, int n, u64* out) { *out = base[n - 1] + counts[n - 1]; }
+__global__ void sum_last(const u64* base, const u64* counts, u64 n, u64* out) { *out = base[n - 1] + counts[n - 1]; }
+
+hipError_t launch_sum_last(const uint64_t* base, const uint64_t* counts, uint64_t n, uint64_t* out, hipStream_t s) {
+    if (n == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sum_last, dim3(1), dim3(1), 0, s, base, counts, (u64)n, out);
+    return hipGetLastError();
+}
 
 constexpr int kCompactGrid = 4096;
 
@@ -1330,7 +1336,7 @@ hipError_t launch_compact(int W, const uint64_t* table, uint64_t cap, uint64_t* 
 #undef KC_CC
 #undef KC_CE
     // cursor = total occupied = base[grid-1] + counts[grid-1]
-    hipLaunchKernelGGL(sum_last, dim3(1), dim3(1), 0, s, base, counts, grid, cursor);
+    hipLaunchKernelGGL(sum_last, dim3(1), dim3(1), 0, s, base, counts, (u64)grid, cursor);
     return hipGetLastError();
 }
 
@@ -3321,9 +3327,49 @@ __global__ __launch_bounds__(kBlock) void iota_k(u32* out, u64 n) {
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) out[i] = (u32)i;
 }
 
+__global__ __launch_bounds__(kBlock) void key_digits_k(const u64* __restrict__ keys, u64 lo, u64 hi, int shift,
+                                                       unsigned char* __restrict__ out) {
+    for (u64 i = lo + (u64)blockIdx.x * kBlock + threadIdx.x; i < hi; i += (u64)gridDim.x * kBlock)
+        out[i] = (unsigned char)(keys[i] >> shift);
+}
+
+hipError_t launch_key_digits(const uint64_t* keys, uint64_t lo, uint64_t hi, int shift, uint8_t* out, hipStream_t s) {
+    if (hi <= lo) return hipSuccess;
+    if (shift < 0 || shift > 56) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(key_digits_k, dim3(grid_for(hi - lo)), dim3(kBlock), 0, s, keys, lo, hi, shift, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(iota_k, dim3(grid_for(n)), dim3(kBlock), 0, s, out, n);
+    return hipGetLastError();
+}
+
+// The finish's group descriptors from the group bounds: order[g] = g,
+// len[g] = (starts[g + 1] - starts[g]) | tag << 24 (lengths clamped to 24 bits:
+// a longer group is past seg_sort's capacity, which *longest tells the host),
+// *longest = the longest group (zeroed by the caller)
+__global__ __launch_bounds__(kBlock) void group_desc_k(const u64* __restrict__ starts, u64 ng, u32 tag,
+                                                       u32* __restrict__ order, u32* __restrict__ len,
+                                                       u64* __restrict__ longest) {
+    for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < ng; i0 += (u64)gridDim.x * kBlock) {
+        const u64 g = i0 + threadIdx.x;
+        u64 l = 0;
+        if (g < ng) {
+            l = starts[g + 1] - starts[g];
+            order[g] = (u32)g;
+            len[g] = (u32)min(l, (u64)0xffffffu) | (tag << 24);
+        }
+        for (int o = 32; o >= 1; o >>= 1) l = max(l, (u64)__shfl_xor((long long)l, o));
+        if (lane_id() == 0 && l) atomicMax((unsigned long long*)longest, (unsigned long long)l);
+    }
+}
+
+hipError_t launch_group_desc(const uint64_t* starts, uint64_t ng, uint32_t tag, uint32_t* order, uint32_t* len,
+                             uint64_t* longest, hipStream_t s) {
+    if (ng == 0 || tag > 255) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(group_desc_k, dim3(grid_for(ng)), dim3(kBlock), 0, s, starts, ng, tag, order, len, longest);
     return hipGetLastError();
 }
 
@@ -4908,6 +4954,46 @@ hipError_t launch_sketch(const uint32_t* codes, const uint16_t* inval, uint64_t 
     default: KC_SKETCH(0); break;
     }
 #undef KC_SKETCH
+    return hipGetLastError();
+}
+
+// The sketch's distinct fingerprints: each of the min(*counter, cap) samples
+// inserted into an open-addressing set of 2^set_bits slots (fingerprint + 1,
+// 0 = empty; linear probing; cap <= half the slots, so every probe ends), the
+// insertions that found an empty slot counted with one atomic per wave. Same
+// count as sorting the samples and counting the run heads, with no host round
+// trip between the sketch and the count: *counter is read on the device.
+__global__ __launch_bounds__(kBlock) void sketch_distinct_k(const u64* __restrict__ fp, const u64* __restrict__ counter,
+                                                            u64 cap, u64* __restrict__ set, int set_bits,
+                                                            u64* __restrict__ distinct) {
+    const u64 m = min(*counter, cap);
+    const u64 mask = (1ull << set_bits) - 1;
+    for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < m; i0 += (u64)gridDim.x * kBlock) {
+        const u64 i = i0 + threadIdx.x;
+        bool fresh = false;
+        if (i < m) {
+            const u64 v = fp[i] + 1;  // fingerprints are < 2^56
+            u64 slot = mix64(v) & mask;
+            for (;;) {
+                const u64 old = atomicCAS((unsigned long long*)&set[slot], 0ull, (unsigned long long)v);
+                if (old == 0ull) {
+                    fresh = true;
+                    break;
+                }
+                if (old == v) break;
+                slot = (slot + 1) & mask;
+            }
+        }
+        const u64 b = __ballot(fresh);
+        if (lane_id() == 0 && b) atomicAdd((unsigned long long*)distinct, (unsigned long long)__popcll(b));
+    }
+}
+
+hipError_t launch_sketch_distinct(const uint64_t* fp, const uint64_t* counter, uint64_t cap, uint64_t* set,
+                                  int set_bits, uint64_t* distinct, hipStream_t s) {
+    if (set_bits < 1 || set_bits > 40 || cap > (1ull << set_bits) / 2) return hipErrorInvalidValue;
+    const int grid = grid_for(cap, 1024);
+    hipLaunchKernelGGL(sketch_distinct_k, dim3(grid), dim3(kBlock), 0, s, fp, counter, cap, set, set_bits, distinct);
     return hipGetLastError();
 }
 

@@ -1932,6 +1932,7 @@ struct SkmBucketArgs {
     u64 last_mask;
     u64* rec_keys;
     u32* rec_cnts;
+    unsigned char* rec_dig;  // may be null: each record's word 0 bits 48..55 (the finish's first digit)
     u64 rec_cap;
     u64* rec_cursor;
     u64* table;
@@ -2539,6 +2540,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                             for (int j = 0; j < W; j++)
                                 a.rec_keys[(u64)j * a.rec_cap + qq] = lkeys[(size_t)j * a.lcap + i];
                             a.rec_cnts[qq] = lcnt[i];
+                            if (a.rec_dig) a.rec_dig[qq] = (unsigned char)(lkeys[i] >> 48);
                         }
 #pragma unroll
                         for (int j = 0; j < W; j++) lkeys[(size_t)j * a.lcap + i] = 0ull;
@@ -2565,8 +2567,9 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
                             uint32_t b0, uint32_t b1, bool count_keys, uint64_t* rec_keys, uint32_t* rec_cnts, uint64_t rec_cap,
                             uint64_t* rec_cursor, uint64_t* table, uint64_t cap, uint64_t* spill, uint64_t spill_cap,
                             uint64_t* stats, uint32_t probe_limit, uint32_t lcap, int grid, hipStream_t s,
-                            const SkmDedup* dd) {
+                            const SkmDedup* dd, uint8_t* rec_dig) {
     SkmBucketArgs a;
+    a.rec_dig = rec_dig;
     a.dcnt = dd ? dd->cnt : nullptr;
     a.dlen = dd ? dd->len : nullptr;
     a.dpos = dd ? dd->pos : nullptr;
