@@ -111,6 +111,7 @@ struct kc_ctx {
     // scratch (grown on demand)
     DevBuf in_stage;        // host-pointer inputs
     DevBuf fq_counts, fq_base, fq_tmp, seq_off, seq_end;
+    DevBuf fq_phase;  // one-pass index: each chunk's guessed line phase
     DevBuf spill_keys2, rle_flags, rle_pos, rle_head, rle_tmp, run_keys, run_cnts, run_packed;
     DevBuf fin_keys[2], fin_cnts[2], fin_hist, fin_packed, fin_misc;
     DevBuf merge_tmp;  // packed run merge: the other ping-pong buffer
@@ -143,6 +144,12 @@ struct kc_ctx {
     int64_t pend_L = 0;
     bool pend_var = false;
     uint64_t pend_reads = 0;
+    // the pending rows hold one-pass-indexed blocks (rows per chunk, empty rows
+    // of length 0): every pending row has its length in part_rlen, the skm
+    // front end reads them, and key 0's presence is recomputed at the flush
+    // from ST_VHOLE as for variable-length reads
+    bool pend_sparse = false;
+    uint64_t flush_present0 = 0;  // key 0's presence before the flush of padded / one-pass rows
     uint64_t flushes = 0;
     uint64_t dev_total = 0;  // device memory (bytes)
     // kc_checkpoint / kc_rollback: the pending state and the counters a
@@ -171,6 +178,7 @@ struct kc_ctx {
 };
 
 static kc_status cut_run(kc_ctx* c);
+static kc_status recompute_presence(kc_ctx* c);
 static kc_status keep_finished_run(kc_ctx* c, uint64_t n);
 static kc_status cut_run_if_full(kc_ctx* c);
 static kc_status merge_runs_list(kc_ctx* c, const std::vector<std::pair<const void*, uint64_t>>& runs);
@@ -554,7 +562,8 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, uint64_t kstride, c
     const size_t rs = (size_t)c->rs;
     uint8_t* bf = rf + ((size_t)nb << 8);
     uint32_t* nflag = (uint32_t*)(bf + nb);
-    if ((s = sync_stats(c))) return s;
+    // (inside a flush of padded / one-pass rows: key 0's presence from the reads)
+    if ((s = c->var_rlen ? recompute_presence(c) : sync_stats(c))) return s;
     const bool key0 = c->stats_h[ST_KEY0_PRESENT] != 0;
     const uint64_t off0 = key0 ? 1 : 0;
     if (pk_at == 0 && (s = ensure_pooled(c, c->fin_packed, (off0 + (total > n ? total : n)) * rs + 16))) return s;
@@ -617,7 +626,7 @@ static kc_status p5s_direct(kc_ctx* c, const uint64_t* keys, uint64_t kstride, c
 // becomes a finished sorted run
 static kc_status direct_keep(kc_ctx* c, uint64_t nrec) {
     kc_status s;
-    if ((s = sync_stats(c))) return s;
+    if ((s = c->var_rlen ? recompute_presence(c) : sync_stats(c))) return s;
     const bool key0 = c->stats_h[ST_KEY0_PRESENT] != 0;
     std::vector<uint32_t> r0((size_t)c->rs / 4, 0u);
     if (key0) {
@@ -1656,6 +1665,53 @@ extern "C" {
 static kc_status chunk_acc_flush(kc_ctx* c);  // defined with the chunk entry points (C linkage block)
 }
 
+// Key 0's presence for reads whose slots hold positions that are no bases
+// (variable-length padding, one-pass empty rows): the engines read those as
+// not-ACGT, so it is recomputed as (presence before the flush) | ST_VHOLE (a
+// read of >= k bases holds a not-ACGT base, set by the encoders) | a key-0
+// window counted. Also applied before a run is cut inside such a flush.
+static kc_status recompute_presence(kc_ctx* c) {
+    kc_status s;
+    if ((s = sync_stats(c))) return s;
+    const uint64_t present =
+        (c->flush_present0 | c->stats_h[ST_VHOLE] | (c->stats_h[ST_KEY0] != 0 ? 1u : 0u)) ? 1u : 0u;
+    c->stats_h[ST_KEY0_PRESENT] = present;
+    HIPCHK(c, hipMemcpyAsync(c->stats + ST_KEY0_PRESENT, &c->stats_h[ST_KEY0_PRESENT], 8, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KC_OK;
+}
+
+// Fixed-length pending reads [0, n): more than one engine batch is counted
+// whole when it is a high-cardinality batch on an empty record state
+// (key-range passes, count_reads_part), anything else batch by batch with a
+// run cut between batches when the records outgrow half the working set
+static kc_status pend_count_fixed(kc_ctx* c, uint64_t n) {
+    kc_status s;
+    const int64_t L = c->pend_L;
+    const uint64_t b = batch_reads(c, L);
+    if (n > b) {
+        if ((s = sketch_gate(c, n, L, 0))) return s;
+        const bool passes = c->hc_hint && c->part && (!c->skm || c->skm_hc) && c->rec_n == 0 && c->batches == 0 &&
+                            !c->skm_used && c->runs.empty() && !test_hook("KC_NO_KEY_PASSES");
+        if (!passes) {
+            // the skm engine may take a large batch (count_reads_skm)
+            uint64_t bs = b;
+            if (c->skm && !c->skm_hc && skm_geometry((int)L, (int)c->k).ok) {
+                const uint64_t nw = (uint64_t)(L - c->k + 1);
+                bs = std::max(b, skm_big_reads(c, nw, (uint64_t)c->W * c->key_cap / (c->W + 1)));
+            }
+            for (uint64_t r0 = 0; r0 < n; r0 += bs) {
+                if ((s = count_reads(c, nullptr, nullptr, n - r0 < bs ? n - r0 : bs, L, (int64_t)r0))) return s;
+                if ((s = cut_run_if_full(c))) return s;
+            }
+            return KC_OK;
+        }
+    }
+    if ((s = count_reads(c, nullptr, nullptr, n, L, 0))) return s;
+    return cut_run_if_full(c);
+}
+
 static kc_status pend_flush(kc_ctx* c) {
     if (c->acc_n) {
         kc_status s0 = chunk_acc_flush(c);
@@ -1666,58 +1722,27 @@ static kc_status pend_flush(kc_ctx* c) {
     const uint64_t n = c->pend_reads;
     c->pend_reads = 0;  // a failed count is not counted again
     c->flushes++;
+    const bool sparse = c->pend_sparse;
+    c->pend_sparse = false;
+    if (!c->pend_var && !sparse) return pend_count_fixed(c, n);
+    // variable-length reads (slot padding) or one-pass rows (empty rows): the
+    // skm front end reads each row's length; key 0's presence is recomputed
     kc_status s;
-    if (!c->pend_var) {
-        const int64_t L = c->pend_L;
-        const uint64_t b = batch_reads(c, L);
-        if (n > b) {
-            // more than one engine batch: a high-cardinality batch on an empty
-            // record state is counted whole (key-range passes, count_reads_part),
-            // anything else batch by batch with a run cut between batches when
-            // the records outgrow half the working set
-            if ((s = sketch_gate(c, n, L, 0))) return s;
-            const bool passes = c->hc_hint && c->part && (!c->skm || c->skm_hc) && c->rec_n == 0 &&
-                                c->batches == 0 && !c->skm_used && c->runs.empty() && !test_hook("KC_NO_KEY_PASSES");
-            if (!passes) {
-                // the skm engine may take a large batch (count_reads_skm)
-                uint64_t bs = b;
-                if (c->skm && !c->skm_hc && skm_geometry((int)L, (int)c->k).ok) {
-                    const uint64_t nw = (uint64_t)(L - c->k + 1);
-                    bs = std::max(b, skm_big_reads(c, nw, (uint64_t)c->W * c->key_cap / (c->W + 1)));
-                }
-                for (uint64_t r0 = 0; r0 < n; r0 += bs) {
-                    if ((s = count_reads(c, nullptr, nullptr, n - r0 < bs ? n - r0 : bs, L, (int64_t)r0))) return s;
-                    if ((s = cut_run_if_full(c))) return s;
-                }
-                return KC_OK;
-            }
-        }
-        if ((s = count_reads(c, nullptr, nullptr, n, L, 0))) return s;
-        return cut_run_if_full(c);
-    }
-    // variable-length reads: the slot padding's invalid windows are no holes;
-    // key 0^W is present iff a read of >= k bases holds a not-ACGT base
-    // (ST_VHOLE, written by the encoders) or a key-0 window was counted
     if ((s = sync_stats(c))) return s;
-    const uint64_t present0 = c->stats_h[ST_KEY0_PRESENT];
+    c->flush_present0 = c->stats_h[ST_KEY0_PRESENT];
     c->var_rlen = (const uint16_t*)c->part_rlen.p;
-    s = count_reads(c, nullptr, nullptr, n, c->pend_L, 0);
+    s = c->pend_var ? count_reads(c, nullptr, nullptr, n, c->pend_L, 0) : pend_count_fixed(c, n);
     c->var_rlen = nullptr;
     if (s) return s;
-    if ((s = sync_stats(c))) return s;
-    const uint64_t present = (present0 | c->stats_h[ST_VHOLE] | (c->stats_h[ST_KEY0] != 0 ? 1u : 0u)) ? 1u : 0u;
-    c->stats_h[ST_KEY0_PRESENT] = present;
-    HIPCHK(c, hipMemcpyAsync(c->stats + ST_KEY0_PRESENT, &c->stats_h[ST_KEY0_PRESENT], 8, hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return cut_run_if_full(c);
+    if ((s = recompute_presence(c))) return s;
+    return c->pend_var ? cut_run_if_full(c) : KC_OK;
 }
 
 // Room for n_new more pending reads of length L (fixed or variable): the
 // pending batch is counted first when it is of another kind or n_new would
 // not fit; the buffers grow keeping the pending reads. *off receives the
 // read index where the new reads go.
-static kc_status pend_reserve(kc_ctx* c, int64_t L, bool var, uint64_t n_new, uint64_t* off) {
+static kc_status pend_reserve(kc_ctx* c, int64_t L, bool var, uint64_t n_new, uint64_t* off, bool sparse = false) {
     kc_status s;
     if (c->pend_reads && (c->pend_L != L || c->pend_var != var || c->pend_reads + n_new > pend_room(c, L, var)))
         if ((s = pend_flush(c))) return s;
@@ -1726,7 +1751,12 @@ static kc_status pend_reserve(kc_ctx* c, int64_t L, bool var, uint64_t n_new, ui
     if ((s = grow_keep(c, c->part_codes, need * 4 + 16, keep * 4)) ||
         (s = grow_keep(c, c->part_inval, need * 2 + 16, keep * 2)))
         return s;
-    if (var && (s = grow_keep(c, c->part_rlen, (c->pend_reads + n_new) * 2 + 16, c->pend_reads * 2))) return s;
+    if ((var || sparse || c->pend_sparse) &&
+        (s = grow_keep(c, c->part_rlen, (c->pend_reads + n_new) * 2 + 16, c->pend_reads * 2)))
+        return s;
+    // a one-pass block joins reads of full length L: their lengths first
+    if (sparse && !c->pend_sparse && c->pend_reads)
+        HIPCHK(c, hipMemsetD16Async((hipDeviceptr_t)c->part_rlen.p, (unsigned short)L, c->pend_reads, c->stream));
     c->pend_L = L;
     c->pend_var = var;
     *off = c->pend_reads;
@@ -1762,7 +1792,10 @@ static kc_status pend_add_reads(kc_ctx* c, const uint8_t* base, const uint64_t* 
             l.n_reads = m;
             l.L = (int)L;
             l.k = (int)c->k;
-            HIPCHK(c, launch_encode_reads(l, codes, inval, c->stream));
+            HIPCHK(c, launch_encode_reads(l, codes, inval, c->stream, c->stats));
+            if (c->pend_sparse)  // rows of a one-pass batch carry their length
+                HIPCHK(c, hipMemsetD16Async((hipDeviceptr_t)((uint16_t*)c->part_rlen.p + off), (unsigned short)L, m,
+                                            c->stream));
         }
         c->pend_reads += m;
         done += m;
@@ -1800,7 +1833,7 @@ static std::string fq_errors(uint64_t e, bool var) {
 }
 
 static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_t L, bool var, bool count,
-                              uint64_t* n_rec_out, bool two_pass = false) {
+                              uint64_t* n_rec_out, bool two_pass = false, bool no_spec = false) {
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
     if ((s = ensure(c, c->fq_counts, nch * 8 + 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
@@ -1817,6 +1850,52 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
         memcpy(c->stats_h, snap, sizeof(snap));
         return KC_OK;
     };
+    // One-pass index (fixed L, codes engines): the text is read once; every
+    // chunk guesses its line phase and writes its records to rows of its own,
+    // then the guesses are checked against the scanned newline counts. A miss
+    // or any error: the block is indexed again by the path below, which also
+    // gives format errors their verdict.
+    const bool spec = count && !var && !two_pass && !no_spec && engine_reads_codes(c, L) && fq_spec_ok((int)L) &&
+                      !test_hook("KC_NO_FQ_ENCODE") && !test_hook("KC_NO_FQ_SPEC");
+    const uint64_t spec_rows = spec ? nch * fq_spec_rows_per_chunk((int)L) : 0;
+    if (spec && spec_rows <= pend_room(c, L)) {
+        uint64_t off = 0;
+        if ((s = pend_reserve(c, L, false, spec_rows, &off, true)) || (s = ensure(c, c->fq_phase, nch + 16)))
+            return s;
+        const uint64_t G = (uint64_t)groups_per_read((int)L);
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
+        HIPCHK(c, launch_fq_encode_spec(base, n, (int)L, (uint32_t*)c->part_codes.p + off * G,
+                                        (uint16_t*)c->part_inval.p + off * G, (uint16_t*)c->part_rlen.p + off,
+                                        (uint64_t*)c->fq_counts.p, (uint8_t*)c->fq_phase.p, c->stats, c->stream));
+        HIPCHK(c, launch_scan_u64((uint64_t*)c->fq_counts.p, (uint64_t*)c->fq_base.p, nch, (uint64_t*)c->fq_tmp.p,
+                                  c->stream));
+        HIPCHK(c, launch_fq_spec_verify((const uint64_t*)c->fq_base.p, (const uint8_t*)c->fq_phase.p, nch, c->stats,
+                                        c->stream));
+        uint64_t* total = (uint64_t*)c->fq_counts.p + nch;
+        HIPCHK(c, launch_sum_last((const uint64_t*)c->fq_base.p, (const uint64_t*)c->fq_counts.p, nch, total, c->stream));
+        uint64_t lines = 0;
+        HIPCHK(c, hipMemcpyAsync(&lines, total, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        if ((s = sync_stats(c))) return s;
+        float t = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+        c->st.decode_ms += t;
+        if (c->stats_h[ST_ERR] == 0 && lines % 4 == 0 && lines > 0) {
+            const uint64_t n_rec = lines / 4;
+            if (n_rec_out) *n_rec_out = n_rec;
+            c->pend_reads += spec_rows;
+            c->pend_sparse = true;
+            c->st.reads += n_rec;
+            c->st.windows += n_rec * (uint64_t)(L - c->k + 1);
+            return KC_OK;
+        }
+        if (getenv("KC_DEBUG"))
+            fprintf(stderr, "kc: one-pass FASTQ index missed (errors %#llx, %llu lines): two-kernel index\n",
+                    (unsigned long long)c->stats_h[ST_ERR], (unsigned long long)lines);
+        if ((s = restore())) return s;
+        return ingest_fastq(c, base, n, L, var, count, n_rec_out, false, true);
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipMemsetAsync(c->stats + ST_ERR, 0, 8, c->stream));
     HIPCHK(c, launch_fq_count(base, n, (uint64_t*)c->fq_counts.p, c->stream));
@@ -1876,7 +1955,7 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     if (fused_var && (e & ERR_FQ_LIST)) {
         // a half held more records than the fused list: the two-pass index
         if ((s = restore())) return s;
-        return ingest_fastq(c, base, n, L, var, count, n_rec_out, true);
+        return ingest_fastq(c, base, n, L, var, count, n_rec_out, true, no_spec);
     }
     if (e) {
         const std::string why = fq_errors(e, var);
@@ -1889,6 +1968,9 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     const uint64_t vwin0 = snap[ST_VWIN];
     c->st.reads += n_rec;
     if (fused || whole_var) {
+        if (fused && c->pend_sparse)  // rows of a one-pass batch carry their length
+            HIPCHK(c, hipMemsetD16Async((hipDeviceptr_t)((uint16_t*)c->part_rlen.p + off), (unsigned short)L, n_rec,
+                                        c->stream));
         c->pend_reads += n_rec;
     } else if (codes) {
         if ((s = pend_add_reads(c, base, (const uint64_t*)c->seq_off.p, (const uint64_t*)c->seq_end.p, n_rec, L, var)))
@@ -2120,6 +2202,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->pend_reads = 0;
     c->pend_L = 0;
     c->pend_var = false;
+    c->pend_sparse = false;
     c->acc_n = 0;  // (a DMA still reading a buffer is waited for before it is refilled)
     c->ckpt = false;
     c->finished = false;
@@ -2569,6 +2652,7 @@ kc_status kc_rollback(kc_ctx* c) {
         return fail(c, KC_ERR_STATE, "reads were counted since the checkpoint: it cannot be rolled back");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     c->pend_reads = c->ckpt_reads;
+    if (c->pend_reads == 0) c->pend_sparse = false;  // (rows kept keep their lengths)
     c->acc_n = 0;  // chunks accumulated since (kc_checkpoint flushed the accumulator) are forgotten too
     c->st.reads = c->ckpt_st_reads;
     c->st.windows = c->ckpt_st_windows;
@@ -3398,6 +3482,8 @@ static kc_status merge_runs_packed(kc_ctx* c, const std::vector<std::pair<const 
 // record state starts empty. kc_finish merges the runs on the device.
 static kc_status cut_run(kc_ctx* c) {
     kc_status s;
+    // inside a flush of padded / one-pass rows: key 0's presence from the reads
+    if (c->var_rlen && (s = recompute_presence(c))) return s;
     if ((s = sync_stats(c))) return s;
     uint64_t n = 0;
     const double t0 = kc::trace_on() ? kc::now_s() : 0;

@@ -63,8 +63,10 @@ enum ErrBits : uint64_t {
     ERR_FQ_NO_FINAL_NL = 32, // block does not end with '\n'
     ERR_REC_OVERFLOW = 64,   // partition engine: record buffer too small
     ERR_SEG_TOO_LONG = 128,  // seg_sort: a segment longer than its LDS capacity
-    ERR_FQ_LIST = 256        // fused variable-length index: a half held more records than its list (not a
+    ERR_FQ_LIST = 256,       // fused variable-length index: a half held more records than its list (not a
                              // format error: the block is indexed again by the two-pass path)
+    ERR_FQ_SPEC = 512        // one-pass index: a chunk's guessed line phase was wrong or not found (not a
+                             // format error: the block is indexed again by the two-kernel path)
 };
 
 // Slot stride (uint64 words) of the open-addressed table for W key words:
@@ -95,7 +97,9 @@ struct CountLaunch {
 // base highest) and not-ACGT masks (u16 per 16 bases); read r of the launch at
 // r * groups_per_read(L). P1 and P2 read these instead of the FASTQ text.
 int groups_per_read(int L);
-hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s);
+// stats (may be null): stats[ST_VHOLE] set when a read holds a not-ACGT base
+hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s,
+                               uint64_t* stats = nullptr);
 // Variable-length reads (KC_FLAG_VARLEN): read r = text [seq_off[r], seq_end[r])
 // of at most L bases, encoded as a read of L bases whose positions past its
 // own end are not-ACGT with code 0 (no window reaches them; a key's bases past
@@ -295,6 +299,17 @@ hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* lin
 // index the block with the two-pass path).
 // The fused variable-length index + encode handles reads up to ~4060 bases (else two-pass)
 bool fq_encode_var_ok(int L);
+// One-pass FASTQ index + encode (fixed L, fq_spec_ok(L)): chunk c's records at
+// rows [c R, c R + R), R = fq_spec_rows_per_chunk(L), rows past them empty
+// (rlen 0, every base not-ACGT); cnt[c] = the chunk's newlines, phase[c] = its
+// guessed line phase | 4 when not found. Then scan cnt into line bases and run
+// launch_fq_spec_verify, which sets ERR_FQ_SPEC in stats[ST_ERR] on a miss.
+bool fq_spec_ok(int L);
+uint64_t fq_spec_rows_per_chunk(int L);
+hipError_t launch_fq_encode_spec(const uint8_t* base, uint64_t n, int L, uint32_t* codes, uint16_t* inval,
+                                 uint16_t* rlen, uint64_t* cnt, uint8_t* phase, uint64_t* stats, hipStream_t s);
+hipError_t launch_fq_spec_verify(const uint64_t* line_base, const uint8_t* phase, uint64_t nch, uint64_t* stats,
+                                 hipStream_t s);
 hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t* line_base, uint64_t max_rec, int L,
                                 int k, uint32_t* codes, uint16_t* inval, uint16_t* rlen, uint64_t* stats,
                                 hipStream_t s);

@@ -893,8 +893,9 @@ int groups_per_read(int L) { return (L + 15) / 16; }
 __global__ __launch_bounds__(kBlock) void encode_reads_k(const uint8_t* __restrict__ base,
                                                          const u64* __restrict__ seq_off, u64 read0, u64 n_reads,
                                                          int L, int G, u32* __restrict__ codes,
-                                                         unsigned short* __restrict__ inval) {
+                                                         unsigned short* __restrict__ inval, u64* __restrict__ stats) {
     const u64 total = n_reads * (u64)G;
+    bool hole = false;  // a not-ACGT base (stats[ST_VHOLE], when stats is given)
     for (u64 it = (u64)blockIdx.x * kBlock + threadIdx.x; it < total; it += (u64)gridDim.x * kBlock) {
         const u64 r = it / (u64)G;
         const int g = (int)(it - r * (u64)G);
@@ -932,17 +933,20 @@ __global__ __launch_bounds__(kBlock) void encode_reads_k(const uint8_t* __restri
         const u32 c2 = bytes_to_codes(x2, nb - 8, &b2);
         const u32 c3 = bytes_to_codes(x3, nb - 12, &b3);
         codes[it] = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
-        inval[it] = (unsigned short)((b0 << 12) | (b1 << 8) | (b2 << 4) | b3);
+        const u32 bad = (b0 << 12) | (b1 << 8) | (b2 << 4) | b3;
+        inval[it] = (unsigned short)bad;
+        hole = hole || bad != 0u;
     }
+    if (stats && __ballot(hole) && lane_id() == 0) atomicOr((unsigned long long*)&stats[ST_VHOLE], 1ull);
 }
 
-hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s) {
+hipError_t launch_encode_reads(const CountLaunch& l, uint32_t* codes, uint16_t* inval, hipStream_t s, uint64_t* stats) {
     if (l.n_reads == 0) return hipSuccess;
     const int G = groups_per_read(l.L);
     const u64 total = l.n_reads * (u64)G;
     const int grid = (int)hmin((total + kBlock - 1) / kBlock, 65536);
     hipLaunchKernelGGL(encode_reads_k, dim3(grid), dim3(kBlock), 0, s, l.base, l.seq_off, l.read0, l.n_reads, l.L, G,
-                       codes, (unsigned short*)inval);
+                       codes, (unsigned short*)inval, (u64*)stats);
     return hipGetLastError();
 }
 
@@ -4487,12 +4491,25 @@ __device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb
 // read's own bytes and marks the rest of the L-base slot not-ACGT (as
 // encode_reads_var_k). The list holds lcap records per half (records of >= 32
 // bytes); a denser half sets ERR_FQ_LIST.
-template <bool VAR>
+// SP (one-pass index, fixed L): no line_base. Each chunk guesses its line
+// phase (the line index of its first byte mod 4) from the first newlines of
+// its text: the line after newline i is taken for a header when a line of L
+// bases, a '+' line and a line of L bytes follow (a quality line starting with
+// '@' is followed by a header and a sequence line, which does not start with
+// '+'). The chunk's records go to its own rows [c cap, c cap + cap) (cap =
+// max_rec), the rows past them are empty (rlen 0, codes 0, every base
+// not-ACGT), and sp_cnt[c] / sp_phase[c] = its newlines / phase | 4 (not
+// found). fq_spec_verify_k checks the phases against the scanned counts; any
+// miss or error sends the block to the two-kernel index. rlen[row] = L for the
+// records; stats[ST_VHOLE] is set when a read holds a not-ACGT base.
+template <bool VAR, bool SP = false>
 __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_FQ_WPE))) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
                                                       const u64* __restrict__ line_base, u64 max_rec, int L, int G,
                                                       int lcap, u32* __restrict__ codes,
                                                       unsigned short* __restrict__ inval, u64* stats,
-                                                      unsigned short* __restrict__ rlen, int k) {
+                                                      unsigned short* __restrict__ rlen, int k,
+                                                      u64* __restrict__ sp_cnt,
+                                                      unsigned char* __restrict__ sp_phase) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uintptr_t A = (uintptr_t)base & ~(uintptr_t)15;
     const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -4548,12 +4565,19 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
     u64 c = (u64)blockIdx.x * kFqEncWaves + wave;
     int h = 0;
     u64 run = 0;
+    // SP: the chunk's phase, whether it was found, its first record's local
+    // index ((phase + 3) >> 2) and the row of local record 0 (row = rowoff + local)
+    u32 sp_phi = 0;
+    bool sp_fail = false;
+    u64 rbase = 0, rowoff = 0;
     if (c < nchunks) issue(c, 0);
     while (c < nchunks) {
         {
             const uintptr_t hb = A + c * kFqChunk + (u64)h * kFqHalf;
             const long long hrel = (long long)(hb - (uintptr_t)base);
-            if (h == 0) run = line_base[c];
+            if constexpr (!SP) {
+                if (h == 0) run = line_base[c];
+            }
             // the next half: (c, 1) unless it starts past the block
             u64 cn = c;
             int hn = 1;
@@ -4603,6 +4627,49 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
             }
             if (cn < nchunks) issue(cn, hn);
             sync();
+            if constexpr (SP) {
+                if (h == 0) {
+                    // the phase from the first newlines of the chunk's first 4 KiB
+                    // (the block's first chunk starts with a header: phase 0)
+                    sp_phi = 0;
+                    sp_fail = false;
+                    if (c != 0) {
+                        u64 m0 = trim(mk[0], hrel + lane * 64);
+                        const u32 c0 = (u32)__popcll(m0);
+                        u32 inc = c0;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const u32 y = __shfl_up(inc, o);
+                            if (lane >= o) inc += y;
+                        }
+                        u32 kx = inc - c0;
+                        const u32 tot0 = (u32)__shfl((int)inc, 63);
+                        unsigned short* nl8 = lst;  // scratch: the walk below rewrites the list
+                        while (m0 && kx < 8u) {
+                            nl8[kx++] = (unsigned short)(lane * 64 + __ffsll((long long)m0) - 1);
+                            m0 &= m0 - 1;
+                        }
+                        sync();
+                        sp_fail = true;
+                        int nl[8];
+#pragma unroll
+                        for (int i = 0; i < 8; i++) nl[i] = (u32)i < tot0 ? (int)nl8[i] : 0;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            if (sp_fail && (u32)(i + 4) < tot0 && txt[nl[i] + 1] == (unsigned char)'@' &&
+                                nl[i + 2] - nl[i + 1] - 1 == L && txt[nl[i + 2] + 1] == (unsigned char)'+' &&
+                                nl[i + 4] - nl[i + 3] - 1 == L) {
+                                sp_phi = (u32)(3 - i) & 3u;
+                                sp_fail = false;
+                            }
+                        }
+                        sync();
+                    }
+                    run = sp_phi;
+                    rbase = (sp_phi + 3u) >> 2;
+                    rowoff = c * max_rec - rbase;
+                }
+            }
             const u64 rec0 = (run + 3) >> 2;  // first record whose header may end in this half
 #pragma unroll
             for (int rd = 0; rd < kFqRounds; rd++) {
@@ -4639,7 +4706,7 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
                     const u32 jc = (u32)j & 3u;
                     if (jc == 0u) {
                         const u64 li = (j >> 2) - rec0;
-                        if ((j >> 2) >= max_rec) err |= ERR_FQ_TOO_MANY;
+                        if ((j >> 2) - rbase >= max_rec) err |= ERR_FQ_TOO_MANY;
                         else if (li < (u64)lcap) lst[li] = (unsigned short)(o + 1);
                         else err |= VAR ? ERR_FQ_LIST : ERR_FQ_SEQ_LEN;  // more records than the list holds
                     } else if (jc != 2u) {
@@ -4658,7 +4725,7 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
             sync();
             // records [rec0, rec1) have their header newline in this half
             u64 rec1 = (run + 3) >> 2;
-            if (rec1 > max_rec) rec1 = max_rec;
+            if (rec1 - rbase > max_rec) rec1 = rbase + max_rec;
             const u32 nrec = rec1 > rec0 ? (u32)min(rec1 - rec0, (u64)lcap) : 0u;
             if constexpr (VAR) {
                 // each listed record's sequence length: the walk saw its
@@ -4741,13 +4808,31 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
                         wrong = wrong || nxt != (u32)'\n' || hrel + s0 + nb >= (long long)n;
                     }
                     if (wrong) err |= ERR_FQ_SEQ_LEN;
+                    if (bad != 0u) vhole = true;  // (ST_VHOLE: key 0's presence for padded / one-pass rows)
                 } else {
                     if (bad != 0u && lr >= k) vhole = true;
                     bad |= ((1u << (16 - nb)) - 1u) & ~((1u << (16 - nb0)) - 1u);  // the slot past the read
                 }
-                const u64 at = (rec0 + r) * (u64)G + (u64)g;
+                const u64 at = (rowoff + rec0 + r) * (u64)G + (u64)g;
                 codes[at] = cw;
                 inval[at] = (unsigned short)bad;
+                if (SP && g == 0) rlen[rowoff + rec0 + r] = (unsigned short)L;
+            }
+            if constexpr (SP) {
+                if (hn == 0) {
+                    // the chunk is done: its empty rows, newline count and phase
+                    const u64 nrec_c = min(((run + 3) >> 2) - rbase, max_rec);
+                    const u64 row0 = c * max_rec;
+                    for (u64 q = nrec_c * (u64)G + (u64)lane; q < max_rec * (u64)G; q += 64) {
+                        codes[row0 * (u64)G + q] = 0u;
+                        inval[row0 * (u64)G + q] = (unsigned short)0xffffu;
+                    }
+                    for (u64 q = nrec_c + (u64)lane; q < max_rec; q += 64) rlen[row0 + q] = 0;
+                    if (lane == 0) {
+                        sp_cnt[c] = run - sp_phi;
+                        sp_phase[c] = (unsigned char)(sp_phi | (sp_fail ? 4u : 0u));
+                    }
+                }
             }
             sync();
             c = cn;
@@ -4755,8 +4840,8 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
         }
     }
     if (err) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)err);
+    if (__ballot(vhole) && lane == 0) atomicOr((unsigned long long*)&stats[ST_VHOLE], 1ull);
     if constexpr (VAR) {
-        if (__ballot(vhole) && lane == 0) atomicOr((unsigned long long*)&stats[ST_VHOLE], 1ull);
         for (int o = 32; o >= 1; o >>= 1) vwin += __shfl_xor(vwin, o);
         if (lane == 0 && vwin) atomicAdd((unsigned long long*)&stats[ST_VWIN], (unsigned long long)vwin);
     }
@@ -4772,7 +4857,49 @@ hipError_t launch_fq_encode(const uint8_t* base, uint64_t n, const uint64_t* lin
     const size_t lds = (size_t)kFqEncWaves * fq_encode_wave_lds(L);
     int g = (int)hmin((nch + kFqEncWaves - 1) / kFqEncWaves, 16384);
     hipLaunchKernelGGL(fq_encode_k<false>, dim3(g ? g : 1), dim3(kFqEncBlock), lds, s, base, n, nch, line_base, max_rec,
-                       L, G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)nullptr, 0);
+                       L, G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)nullptr, 0, (u64*)nullptr,
+                       (unsigned char*)nullptr);
+    return hipGetLastError();
+}
+
+// One-pass index (fq_encode_k<false, true>): rows per chunk, the largest number
+// of records whose header ends in one 16 KiB chunk (records of >= 2L + 6 bytes,
+// so consecutive header ends are >= 2L + 6 bytes apart)
+uint64_t fq_spec_rows_per_chunk(int L) { return 1 + (kFqChunk - 1) / (2 * (u64)L + 6); }
+// the phase guess reads the first 8 newlines of a chunk's first 4 KiB
+bool fq_spec_ok(int L) { return L >= 1 && 4 * (2 * L + 8) <= 4096 - 2 * L; }
+
+hipError_t launch_fq_encode_spec(const uint8_t* base, uint64_t n, int L, uint32_t* codes, uint16_t* inval,
+                                 uint16_t* rlen, uint64_t* cnt, uint8_t* phase, uint64_t* stats, hipStream_t s) {
+    if (!fq_spec_ok(L)) return hipErrorInvalidValue;
+    u64 nch = fq_chunks(base, n);
+    const int G = groups_per_read(L);
+    const int lcap = fq_encode_list_cap(L);
+    if ((u64)lcap * (u64)G >= 65536 || lcap < 8) return hipErrorInvalidValue;
+    const size_t lds = (size_t)kFqEncWaves * fq_encode_wave_lds(L);
+    int g = (int)hmin((nch + kFqEncWaves - 1) / kFqEncWaves, 16384);
+    hipLaunchKernelGGL((fq_encode_k<false, true>), dim3(g ? g : 1), dim3(kFqEncBlock), lds, s, base, n, nch,
+                       (const u64*)nullptr, (u64)fq_spec_rows_per_chunk(L), L, G, lcap, codes, (unsigned short*)inval,
+                       stats, (unsigned short*)rlen, 0, cnt, phase);
+    return hipGetLastError();
+}
+
+// The guessed phases against the scanned newline counts (line_base = their
+// exclusive scan): a chunk whose phase was not found or differs sets ERR_FQ_SPEC
+__global__ __launch_bounds__(kBlock) void fq_spec_verify_k(const u64* __restrict__ line_base,
+                                                           const unsigned char* __restrict__ phase, u64 nch,
+                                                           u64* __restrict__ stats) {
+    bool bad = false;
+    for (u64 c = (u64)blockIdx.x * kBlock + threadIdx.x; c < nch; c += (u64)gridDim.x * kBlock)
+        bad = bad || (phase[c] & 4u) != 0u || (u32)(line_base[c] & 3u) != (u32)(phase[c] & 3u);
+    if (__ballot(bad) && lane_id() == 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_FQ_SPEC);
+}
+
+hipError_t launch_fq_spec_verify(const uint64_t* line_base, const uint8_t* phase, uint64_t nch, uint64_t* stats,
+                                 hipStream_t s) {
+    if (nch == 0) return hipSuccess;
+    hipLaunchKernelGGL(fq_spec_verify_k, dim3(grid_for(nch)), dim3(kBlock), 0, s, line_base,
+                       (const unsigned char*)phase, nch, stats);
     return hipGetLastError();
 }
 
@@ -4795,7 +4922,8 @@ hipError_t launch_fq_encode_var(const uint8_t* base, uint64_t n, const uint64_t*
     const size_t lds = (size_t)kFqEncWaves * wl;
     int g = (int)hmin((nch + kFqEncWaves - 1) / kFqEncWaves, 16384);
     hipLaunchKernelGGL(fq_encode_k<true>, dim3(g ? g : 1), dim3(kFqEncBlock), lds, s, base, n, nch, line_base, max_rec, L,
-                       G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)rlen, k);
+                       G, lcap, codes, (unsigned short*)inval, stats, (unsigned short*)rlen, k, (u64*)nullptr,
+                       (unsigned char*)nullptr);
     return hipGetLastError();
 }
 

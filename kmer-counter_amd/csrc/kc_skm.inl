@@ -1117,10 +1117,15 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
     for (u64 tile = wid; tile < a.ntiles; tile += nwaves) {
         const u64 r0 = tile * 64;
         const int nr = (int)min((u64)64, a.n_reads - r0);
-        const u64 livem = nr >= 64 ? ~0ull : ((1ull << nr) - 1ull);
+        // the lane's read length (variable-length reads, one-pass rows), loaded
+        // before the wait below: a global load issued after the next tile's
+        // prefetch would wait for the whole prefetch (in-order vmcnt)
+        const int my_rl = (a.rlen && lane < nr) ? (int)a.rlen[r0 + (u64)lane] : L;
         // 1. the tile's staged code words into the rows; read flags (not-ACGT
         // bases, aligned all-A halves inside the read)
         rflag[lane] = 0;
+        int* rls = (int*)ring;  // the lengths by row (the ring is empty between tiles)
+        rls[lane] = my_rl;
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the staging DMA has landed
         wave_sync();
         {
@@ -1135,7 +1140,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                 if (a.rlen) {
                     // a variable-length read: the padding past its end is no
                     // bad base (its windows end with the read, below)
-                    lr = (int)a.rlen[r0 + (u64)r];
+                    lr = rls[r];
                     const int o = lr - 16 * g;
                     ivr = o >= 16 ? iv : (o <= 0 ? 0u : iv & ~((1u << (16 - o)) - 1u));
                 }
@@ -1158,13 +1163,18 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
 #pragma unroll
         for (int i = 0; i < (D > 0 ? D : 1); i++) St[i] = ~0u;
         const bool fast = !slow && !(a.skip & 2);
-        const bool live = lane < nr;
         // windows of the lane's read (variable-length reads: its own; windows
         // from nwr on are not windows, their bucket is kNoKey); vt: a read of
-        // the tile is shorter than the slot (wave-uniform)
+        // the tile is shorter than the slot (wave-uniform). A row of length 0
+        // (one-pass index: a chunk's rows past its records) is no read: it
+        // pushes nothing (live) and does not make the interior blocks take
+        // the per-window length test (vtf)
         int nwr = nw;
-        if (a.rlen && live) nwr = max(0, (int)a.rlen[r0 + (u64)lane] - K + 1);
-        const bool vt = a.rlen != nullptr && __builtin_amdgcn_ballot_w64(live && nwr < nw) != 0ull;
+        if (a.rlen && lane < nr) nwr = max(0, my_rl - K + 1);
+        const bool live = lane < nr && my_rl != 0;
+        const u64 livem = __builtin_amdgcn_ballot_w64(live);
+        const bool vt = a.rlen != nullptr && __builtin_amdgcn_ballot_w64(lane < nr && nwr < nw) != 0ull;
+        const bool vtf = a.rlen != nullptr && __builtin_amdgcn_ballot_w64(live && nwr < nw) != 0ull;
         const int g_lo = (E + 1 + 15) / 16;                  // first block whose windows are all >= 1
         const int g_hi = np >= 16 ? (np - 16) / 16 + 1 : 0;  // blocks ending before np
         u32 c0 = crow[0];
@@ -1254,10 +1264,10 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                         } else if (!(a.skip & 2)) {
                             if (!slow) {
                                 const bool bnd = u != prev;
-                                push(bnd && lane < nr, __builtin_amdgcn_ballot_w64(bnd) & livem, w - 1, s, prev);
+                                push(bnd && live, __builtin_amdgcn_ballot_w64(bnd) & livem, w - 1, s, prev);
                                 if (bnd) s = (u32)w;
                             } else {
-                                const bool ended = u != prev && lane < nr && prev != kNoKey;
+                                const bool ended = u != prev && live && prev != kNoKey;
                                 const u64 pm = __builtin_amdgcn_ballot_w64(ended);
                                 push(ended, pm, w - 1, s, prev);
                                 if (u != prev) s = (u32)w;
@@ -1275,7 +1285,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                 for (int i = B - 2; i >= 0; i--) Sp[i] = min(h[i], Sp[i + 1]);
             };
             if (fast && g >= g_lo && g < g_hi) {
-                if (vt) {
+                if (vtf) {
                     fast_block(F3Tag<0>{}, std::true_type{});
                     if constexpr (B == 8) fast_block(F3Tag<8>{}, std::true_type{});
                 } else {
@@ -1290,7 +1300,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
         }
         // the open runs end at the last window
         {
-            const bool ended = prev != kNoKey && lane < nr && !(a.skip & 2);
+            const bool ended = prev != kNoKey && live && !(a.skip & 2);
             push(ended, __builtin_amdgcn_ballot_w64(ended), nw - 1, s, prev);
         }
         while (qn) drain(min(64u, qn));

@@ -1,7 +1,9 @@
 """GPU parity of the FASTQ index + encode passes against each other and the
-CPU oracle: the fused index after fq_count_k (fq_encode_k, one text read for
-K1 emit + E; the default) and the two-pass path (fq_emit_k + fq_validate_k +
-encode_reads_k, KC_NO_FQ_ENCODE=1): identical
+CPU oracle: the one-pass index (fq_encode_k<false, true>: each chunk guesses
+its line phase, rows per chunk, checked against the scanned newline counts;
+the default), the fused index after fq_count_k (fq_encode_k, KC_NO_FQ_SPEC=1)
+and the two-pass path (fq_emit_k + fq_validate_k + encode_reads_k,
+KC_NO_FQ_ENCODE=1): identical
 SortedKMerFile bytes on well-formed blocks whose records straddle the kernel's
 8 KiB halves and 16 KiB chunks (headers of 1..400 bytes, reads of 18..3000
 bases: past the staged KiB the groups come from global memory), and the same
@@ -24,17 +26,24 @@ def _block(n, L, seed, n_rate=0.01, hdr_max=60):
     return out
 
 
-MODES = ("fused", "twopass")
+MODES = ("onepass", "fused", "twopass")
+
+
+def _set_mode(monkeypatch, mode):
+    monkeypatch.delenv("KC_NO_FQ_ENCODE", raising=False)
+    monkeypatch.delenv("KC_NO_FQ_SPEC", raising=False)
+    if mode == "twopass":
+        monkeypatch.setenv("KC_NO_FQ_ENCODE", "1")
+    elif mode == "fused":
+        monkeypatch.setenv("KC_NO_FQ_SPEC", "1")
 
 
 def _count(kca, fq, k, L, mode, monkeypatch, engine="auto"):
     if mode is True:
-        mode = "fused"
+        mode = "onepass"
     elif mode is False:
         mode = "twopass"
-    monkeypatch.delenv("KC_NO_FQ_ENCODE", raising=False)
-    if mode == "twopass":
-        monkeypatch.setenv("KC_NO_FQ_ENCODE", "1")
+    _set_mode(monkeypatch, mode)
     with kca.Context(kmer_length=k, line_length=L, engine=engine) as ctx:
         n = ctx.count_fastq(fq)
         return n, ctx.records()
@@ -60,12 +69,86 @@ def test_fused_index_block_sizes(kca, orc, monkeypatch, n):
         assert _count(kca, fq, 31, 150, mode, monkeypatch) == (n, want), mode
 
 
+@pytest.mark.parametrize("mode", ["onepass", "fused"])
 @pytest.mark.parametrize("engine", ["skm", "partition"])
-def test_fused_engines(kca, orc, monkeypatch, engine):
+def test_fused_engines(kca, orc, monkeypatch, engine, mode):
     fq = kca.synth_fastq(30000, 150, seed=13, genome_length=500_000, n_rate=0.001)
-    n, got = _count(kca, fq, 31, 150, True, monkeypatch, engine=engine)
+    n, got = _count(kca, fq, 31, 150, mode, monkeypatch, engine=engine)
     assert n == 30000
     assert got == orc.count_fastq(fq, 31)
+
+
+def _onepass_missed(capfd):
+    return "one-pass FASTQ index missed" in capfd.readouterr().err
+
+
+@pytest.mark.parametrize("k", [21, 31, 33])
+def test_onepass_guess_miss_falls_back(kca, orc, monkeypatch, capfd, k):
+    """Headers of ~5 KiB leave chunks whose first 4 KiB hold fewer than the
+    newlines the phase guess needs: the guess misses, the verify kernel flags
+    the block and the two-kernel index counts it (same records as the oracle).
+    With short headers the one-pass index takes the block."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L = 150
+    rng = random.Random(k)
+    recs = [f"@{'h' * rng.randrange(4800, 5400)}{i}\n" + "".join(rng.choice("ACGT") for _ in range(L)) +
+            "\n+\n" + "I" * L + "\n" for i in range(300)]
+    fq = "".join(recs).encode()
+    capfd.readouterr()
+    assert _count(kca, fq, k, L, "onepass", monkeypatch) == (300, orc.count_fastq(fq, k))
+    assert _onepass_missed(capfd)
+    fq2 = "".join(_block(4000, L, seed=k, hdr_max=40)).encode()
+    assert _count(kca, fq2, k, L, "onepass", monkeypatch) == (4000, orc.count_fastq(fq2, k))
+    assert not _onepass_missed(capfd)
+
+
+@pytest.mark.parametrize("engine", ["auto", "skm", "partition"])
+@pytest.mark.parametrize("kind", ["clean", "n_base", "all_a"])
+def test_onepass_key0_presence(kca, orc, monkeypatch, engine, kind):
+    """Key 0 (all-A) in the output iff a read holds a not-ACGT base (count 0
+    unless all-A windows were counted) or an all-A window exists: the one-pass
+    rows past each chunk's records are no reads, whatever the engine makes of
+    them (the skm front end skips them, the key-prefix engine reads them as
+    bases that are not ACGT and key 0's presence is recomputed at the flush)."""
+    L, k = 150, 31
+    rng = random.Random(hash(kind) & 0xffff)
+    seqs = ["".join(rng.choice("CGT") for _ in range(L)) for _ in range(3000)]
+    if kind == "n_base":
+        seqs[1234] = seqs[1234][:70] + "N" + seqs[1234][71:]
+    elif kind == "all_a":
+        seqs[77] = "A" * 40 + seqs[77][40:]
+    fq = "".join(f"@r{i}\n{s}\n+\n{'I' * L}\n" for i, s in enumerate(seqs)).encode()
+    want = orc.count_fastq(fq, k)
+    got = {}
+    for mode in MODES:
+        got[mode] = _count(kca, fq, k, L, mode, monkeypatch, engine=engine)
+        assert got[mode] == (3000, want), mode
+
+
+def test_onepass_mixed_pending_batch(kca, orc, monkeypatch, capfd):
+    """One pending batch of one-pass rows and rows of other producers (a block
+    whose phase guess misses, reference chunks, a second one-pass block),
+    counted together at kc_finish: the same records as the oracle over the
+    concatenated input."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    _set_mode(monkeypatch, "onepass")
+    L, k = 150, 31
+    rng = random.Random(5)
+    a = "".join(_block(3000, L, seed=21, n_rate=0.002)).encode()
+    long_hdr = "".join(f"@{'h' * 5000}{i}\n" + "".join(rng.choice("ACGT") for _ in range(L)) + "\n+\n" + "I" * L +
+                       "\n" for i in range(200)).encode()
+    c = "".join(_block(2500, L, seed=22, n_rate=0.0)).encode()
+    chunk_reads = [("".join(rng.choice("ACGN") for _ in range(L))) for _ in range(500)]
+    chunk = "".join(chunk_reads).encode()
+    with kca.Context(kmer_length=k, line_length=L) as ctx:
+        ctx.count_fastq(a)
+        ctx.count_fastq(long_hdr)
+        ctx.count_chunk(chunk, L)
+        ctx.count_fastq(c)
+        got = ctx.records()
+    assert _onepass_missed(capfd)
+    fq_chunk = "".join(f"@c{i}\n{s}\n+\n{'I' * L}\n" for i, s in enumerate(chunk_reads)).encode()
+    assert got == orc.count_fastq(a + long_hdr + fq_chunk + c, k)
 
 
 def _mutations():
