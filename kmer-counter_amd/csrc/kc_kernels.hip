@@ -4456,12 +4456,12 @@ __device__ __forceinline__ u32 swar_codes(u32 x, int nv, u32* bad4) {
 
 // 16 bytes (x0 first, lowest byte first; nb of them valid) -> the group's code
 // word (base 0 in bits 31-30) and not-ACGT mask (base 0 in bit 15), as
-// swar_codes per dword, with the four code bytes packed by one 24-bit multiply
-// each (c0, c1, c2 at bits 0, 8, 16 times 2^22 + 2^12 + 2^2 land at bits 22,
-// 20, 18 with no carries) and the 16 byte flags transposed as in nl_mask16w
+// swar_codes per dword; each dword's four 2-bit codes and four bad-byte flags
+// are packed by one v_dot4_u32_u8 each (bytes times 64 16 4 1 and 8 4 2 1:
+// the first byte lands highest)
 __device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb, u32* bad16) {
     const u32 xs[4] = {x0, x1, x2, x3};
-    u32 bf[4], code = 0;
+    u32 code = 0, bm = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int nv = nb - 4 * k;
@@ -4469,19 +4469,12 @@ __device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb
         u32 t = ((xs[k] >> 1) ^ (xs[k] >> 2)) & 0x03030303u;
         const u32 y = __builtin_amdgcn_perm(0u, 0x54474341u, t) ^ xs[k];
         const u32 bad = (((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u & vm;
-        t = (t & vm) | (bad >> 7) | (bad >> 6);
-        bf[k] = bad;
-        const u32 c4 = ((__umul24(t, 0x401004u) >> 16) & 0xfcu) | (t >> 24);
-        code |= c4 << (24 - 8 * k);
+        const u32 b1 = bad >> 7;  // 1 in each bad byte
+        t = (t & vm) | b1 | (bad >> 6);  // bad bytes code 3, bytes past nb code 0
+        code = __builtin_amdgcn_udot4(t, 0x01041040u, code << 8, false);
+        bm = __builtin_amdgcn_udot4(b1, 0x01020408u, bm << 4, false);
     }
-    const u32 yb = (bf[0] >> 7) | (bf[1] >> 6) | (bf[2] >> 5) | (bf[3] >> 4);
-    const u32 v1 = (yb | (yb >> 4)) & 0x00ff00ffu;
-    u32 p = (v1 & 0xffu) | ((v1 >> 8) & 0xff00u);
-    u32 tt = (p ^ (p >> 3)) & 0x0a0au;
-    p ^= tt ^ (tt << 3);
-    tt = (p ^ (p >> 6)) & 0x00ccu;
-    p ^= tt ^ (tt << 6);
-    *bad16 = __builtin_bitreverse32(p) >> 16;
+    *bad16 = bm;
     return code;
 }
 
