@@ -739,6 +739,8 @@ static kc_status count_reads_part(kc_ctx* c, const uint8_t* base, const uint64_t
         const uint64_t g0 = pre0 < 0 ? 0 : ((uint64_t)pre0 + read0) * G;
         l.codes = (const uint32_t*)c->part_codes.p + g0;
         l.inval = (const uint16_t*)c->part_inval.p + g0;
+        // rows of length 0 (one-pass empty rows) are skipped by P1 / P2
+        l.rlen = (pre0 >= 0 && c->var_rlen) ? c->var_rlen + (uint64_t)pre0 + read0 : nullptr;
         return l;
     };
     // Key-range passes (plan_key_passes): high cardinality, all reads encoded,

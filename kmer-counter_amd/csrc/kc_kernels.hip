@@ -166,6 +166,7 @@ struct CountArgs {
     u64 spill_cap;
     u64* stats;
     u32 probe_limit;
+    const unsigned short* rlen;  // CODES: a row of length 0 (one-pass empty row) is no read
 };
 
 // Reads per tile that keep the kRoll-window chunks of a tile close to a whole
@@ -425,9 +426,11 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
     // current tile is processed (software pipelining across tiles and units)
     u32 pf_code[kPrefetch];
     u32 pf_inv[kPrefetch];
+    u32 pf_len = 1;  // (row lengths: this thread's row of the next tile, with its codes)
     auto prefetch = [&](u64 tile) {
         const u64 r0 = tile * (u64)a.R;
         const int nr = (tile < ntiles) ? (int)min((u64)a.R, a.n_reads - r0) : 0;
+        if (a.rlen) pf_len = tid < nr ? (u32)a.rlen[r0 + (u64)tid] : 1u;
 #pragma unroll
         for (int j = 0; j < kPrefetch; j++) {
             const int it = tid + j * NT;
@@ -482,8 +485,20 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                     codes[it] = cw;
                     inval[it] = iv;
                 }
-                if (tid < nr) rflag[tid] = 0;
+                // flag 2: a row of length 0 (no read: its windows are skipped)
+                if (tid < nr) rflag[tid] = (a.rlen && pf_len == 0u) ? 2u : 0u;
                 __syncthreads();
+                if (a.rlen && tid < 64) {
+                    // the tile's rows of length > 0, in order (lead is free in
+                    // CODES mode): the window walk below takes only these
+                    u32 cnt = 0;
+                    for (int b = 0; b < nr; b += 64) {
+                        const bool lv = b + tid < nr && !(rflag[b + tid] & 2u);
+                        const u64 m = __ballot(lv);
+                        if (lv) lead[cnt + (u32)__popcll(m & lanemask_lt())] = (u32)(b + tid);
+                        cnt += (u32)__popcll(m);
+                    }
+                }
                 // issue the next tile's loads now; they land during this tile
                 prefetch(tile + 1 < t_end ? tile + 1 : (unit + gridDim.x) * per_unit);
                 for (int it = tid; it < nr * NG; it += NT)
@@ -544,7 +559,16 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             //    shifts one base in (the base 32W past the window comes from a
             //    tail word; past the read end it is 0, as in the reference).
             const int nchr = (nw + kRoll - 1) / kRoll;
-            const int total = nr * nchr;
+            // CODES with row lengths: the walk covers the rows of length > 0
+            // (listed in lead), so a one-pass chunk's empty rows take no lanes
+            const bool rmap = CODES && a.rlen != nullptr;
+            int nlive = nr;
+            if (rmap) {
+                nlive = 0;
+                for (int b = 0; b < nr; b += 64)
+                    nlive += (int)__popcll(__ballot(b + (int)lane_id() < nr && !(rflag[b + (int)lane_id()] & 2u)));
+            }
+            const int total = nlive * nchr;
             if constexpr (SINK == SINK_SCATTER) {
                 const bool filt = pa.fhi - pa.flo < 256u || pa.out2 != nullptr;
                 const u32 fmid = pa.out2 ? pa.fmid : 256u;  // first slot of the second pass: word0 >> 56 >= fmid
@@ -556,16 +580,15 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                 // consecutive lanes write consecutive slots. B: roll again and
                 // stage. No LDS round trip inside a step.
                 for (int c = tid; c - (tid & 63) < total; c += NT) {
+                    int r = c < total ? (rmap ? (int)lead[c / nchr] : c / nchr) : 0, p0 = 0;
                     const bool cact = c < total;
-                    int r = 0, p0 = 0;
                     u64 raw[W];
                     u64 tail = 0;
                     bool clean = true;
 #pragma unroll
                     for (int j = 0; j < W; j++) raw[j] = 0;
                     if (cact) {
-                        r = c / nchr;
-                        p0 = (c - r * nchr) * kRoll;
+                        p0 = (c - (c / nchr) * nchr) * kRoll;
                         const u32* cr = codes + r * NG;
 #pragma unroll
                         for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
@@ -675,16 +698,15 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             } else {
                 for (int c = tid; c - (tid & 63) < total; c += NT) {
                     // the loop bound is wave-uniform so every lane reaches the ballots
+                    int r = c < total ? (rmap ? (int)lead[c / nchr] : c / nchr) : 0, p0 = 0;
                     const bool cact = c < total;
-                    int r = 0, p0 = 0;
                     u64 raw[W];
                     u64 tail = 0;
                     bool clean = true;
     #pragma unroll
                     for (int j = 0; j < W; j++) raw[j] = 0;
                     if (cact) {
-                        r = c / nchr;
-                        p0 = (c - r * nchr) * kRoll;
+                        p0 = (c - (c / nchr) * nchr) * kRoll;
                         const u32* cr = codes + r * NG;
     #pragma unroll
                         for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
@@ -860,6 +882,7 @@ static CountArgs make_args(const CountLaunch& l, const CountGeom& g) {
     a.spill_cap = l.spill_cap;
     a.stats = l.stats;
     a.probe_limit = l.probe_limit;
+    a.rlen = l.rlen;
     return a;
 }
 
