@@ -488,17 +488,6 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                 // flag 2: a row of length 0 (no read: its windows are skipped)
                 if (tid < nr) rflag[tid] = (a.rlen && pf_len == 0u) ? 2u : 0u;
                 __syncthreads();
-                if (a.rlen && tid < 64) {
-                    // the tile's rows of length > 0, in order (lead is free in
-                    // CODES mode): the window walk below takes only these
-                    u32 cnt = 0;
-                    for (int b = 0; b < nr; b += 64) {
-                        const bool lv = b + tid < nr && !(rflag[b + tid] & 2u);
-                        const u64 m = __ballot(lv);
-                        if (lv) lead[cnt + (u32)__popcll(m & lanemask_lt())] = (u32)(b + tid);
-                        cnt += (u32)__popcll(m);
-                    }
-                }
                 // issue the next tile's loads now; they land during this tile
                 prefetch(tile + 1 < t_end ? tile + 1 : (unit + gridDim.x) * per_unit);
                 for (int it = tid; it < nr * NG; it += NT)
@@ -559,16 +548,7 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             //    shifts one base in (the base 32W past the window comes from a
             //    tail word; past the read end it is 0, as in the reference).
             const int nchr = (nw + kRoll - 1) / kRoll;
-            // CODES with row lengths: the walk covers the rows of length > 0
-            // (listed in lead), so a one-pass chunk's empty rows take no lanes
-            const bool rmap = CODES && a.rlen != nullptr;
-            int nlive = nr;
-            if (rmap) {
-                nlive = 0;
-                for (int b = 0; b < nr; b += 64)
-                    nlive += (int)__popcll(__ballot(b + (int)lane_id() < nr && !(rflag[b + (int)lane_id()] & 2u)));
-            }
-            const int total = nlive * nchr;
+            const int total = nr * nchr;
             if constexpr (SINK == SINK_SCATTER) {
                 const bool filt = pa.fhi - pa.flo < 256u || pa.out2 != nullptr;
                 const u32 fmid = pa.out2 ? pa.fmid : 256u;  // first slot of the second pass: word0 >> 56 >= fmid
@@ -580,15 +560,15 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
                 // consecutive lanes write consecutive slots. B: roll again and
                 // stage. No LDS round trip inside a step.
                 for (int c = tid; c - (tid & 63) < total; c += NT) {
-                    int r = c < total ? (rmap ? (int)lead[c / nchr] : c / nchr) : 0, p0 = 0;
-                    const bool cact = c < total;
+                    int r = c < total ? c / nchr : 0, p0 = 0;
+                    const bool cact = c < total && !(rflag[r] & 2u);  // (a row of length 0: no windows)
                     u64 raw[W];
                     u64 tail = 0;
                     bool clean = true;
 #pragma unroll
                     for (int j = 0; j < W; j++) raw[j] = 0;
                     if (cact) {
-                        p0 = (c - (c / nchr) * nchr) * kRoll;
+                        p0 = (c - r * nchr) * kRoll;
                         const u32* cr = codes + r * NG;
 #pragma unroll
                         for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);
@@ -698,15 +678,15 @@ __global__ __launch_bounds__(NT) void count_front(CountArgs a, PartArgs pa) {
             } else {
                 for (int c = tid; c - (tid & 63) < total; c += NT) {
                     // the loop bound is wave-uniform so every lane reaches the ballots
-                    int r = c < total ? (rmap ? (int)lead[c / nchr] : c / nchr) : 0, p0 = 0;
-                    const bool cact = c < total;
+                    int r = c < total ? c / nchr : 0, p0 = 0;
+                    const bool cact = c < total && !(rflag[r] & 2u);  // (a row of length 0: no windows)
                     u64 raw[W];
                     u64 tail = 0;
                     bool clean = true;
     #pragma unroll
                     for (int j = 0; j < W; j++) raw[j] = 0;
                     if (cact) {
-                        p0 = (c - (c / nchr) * nchr) * kRoll;
+                        p0 = (c - r * nchr) * kRoll;
                         const u32* cr = codes + r * NG;
     #pragma unroll
                         for (int j = 0; j < W; j++) raw[j] = code_word(cr, p0 + 32 * j);

@@ -82,7 +82,7 @@ def _onepass_missed(capfd):
     return "one-pass FASTQ index missed" in capfd.readouterr().err
 
 
-@pytest.mark.parametrize("k", [21, 31, 33])
+@pytest.mark.parametrize("k", [21, 31])
 def test_onepass_guess_miss_falls_back(kca, orc, monkeypatch, capfd, k):
     """Headers of ~5 KiB leave chunks whose first 4 KiB hold fewer than the
     newlines the phase guess needs: the guess misses, the verify kernel flags
@@ -123,6 +123,37 @@ def test_onepass_key0_presence(kca, orc, monkeypatch, engine, kind):
     for mode in MODES:
         got[mode] = _count(kca, fq, k, L, mode, monkeypatch, engine=engine)
         assert got[mode] == (3000, want), mode
+
+
+@pytest.mark.parametrize("k,used", [(31, True), (19, True), (18, False), (33, False), (55, False)])
+def test_onepass_only_for_the_f3_front_end(kca, orc, monkeypatch, capfd, k, used):
+    """The one-pass index runs where the skm engine's F3 front end reads the
+    rows (k in [19, 32]); other k take the two-kernel index (a guess miss shows
+    which one ran: it is reported only by the one-pass index)."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L = 150
+    rng = random.Random(k)
+    recs = [f"@{'h' * 5000}{i}\n" + "".join(rng.choice("ACGT") for _ in range(L)) + "\n+\n" + "I" * L + "\n"
+            for i in range(100)]
+    fq = "".join(recs).encode()
+    capfd.readouterr()
+    assert _count(kca, fq, k, L, "onepass", monkeypatch) == (100, orc.count_fastq(fq, k))
+    assert _onepass_missed(capfd) == used
+
+
+def test_onepass_rows_through_the_key_prefix_engine(kca, orc, monkeypatch):
+    """iid reads at k = 31 (no coverage): the one-pass rows are indexed for
+    F3, then the coverage sketch hands the batch to the key-prefix engine,
+    whose front end skips the empty rows; key 0 follows the reads."""
+    _set_mode(monkeypatch, "onepass")
+    L, k, n = 150, 31, 150_000  # >= 2^24 windows: the sketch runs
+    fq = kca.synth_fastq(n, L, seed=91, genome_length=0, n_rate=0.0005)
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=8 << 30) as ctx:
+        assert ctx.count_fastq(fq) == n
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["engines_used"] == 2, st["engines_used"]
+    assert got == orc.count_fastq(fq, k)
 
 
 def test_onepass_mixed_pending_batch(kca, orc, monkeypatch, capfd):
