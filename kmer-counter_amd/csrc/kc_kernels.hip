@@ -4761,6 +4761,10 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
                 }
                 sync();
             }
+            // the half's rows start at row rowoff + rec0: item (r, g) is word
+            // r G + g = item past that row's first word (no per-item 64-bit math)
+            u32* const hcodes = codes + (rowoff + rec0) * (u64)G;
+            unsigned short* const hinval = inval + (rowoff + rec0) * (u64)G;
 #pragma unroll 1
             for (u32 item = (u32)lane; item < nrec * (u32)G; item += 64) {
                 const u32 r = divg.div(item);
@@ -4809,9 +4813,8 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
                     if (bad != 0u && lr >= k) vhole = true;
                     bad |= ((1u << (16 - nb)) - 1u) & ~((1u << (16 - nb0)) - 1u);  // the slot past the read
                 }
-                const u64 at = (rowoff + rec0 + r) * (u64)G + (u64)g;
-                codes[at] = cw;
-                inval[at] = (unsigned short)bad;
+                hcodes[item] = cw;
+                hinval[item] = (unsigned short)bad;
                 if (SP && g == 0) rlen[rowoff + rec0 + r] = (unsigned short)L;
             }
             if constexpr (SP) {
