@@ -50,6 +50,7 @@ struct kc_ctx {
     int64_t k = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev2 = nullptr;  // a third mark: two phases timed by one synchronisation
     uint64_t id = 0;
 
     // table + spill (the gpu_memory_limit working set)
@@ -1204,22 +1205,22 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
     h[2] = 0;
     h[3] = nt1;
     HIPCHK(c, hipMemcpyAsync(rt, h.data(), 4 * 8, hipMemcpyHostToDevice, c->stream));
+    // (histogram and scatter timed by three marks and the one synchronisation
+    // each pass needs anyway: no wait between a histogram and its scatter)
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     // first pass digit: the producer's byte per item when it wrote one, else word 0 bits 48..55
     HIPCHK(c, launch_rp_hist(dig1, dig1 ? nullptr : a, 48, rt, rt + 2, 1, nt1, (uint32_t)tile, pos, tmp, grid,
                              c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    HIPCHK(c, hipEventSynchronize(c->ev1));
-    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-    ms[0] += t;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_rp_scatter(NW, pay, a, sa, b, sb, pa, pb, rt, rt + 2, 1, nt1, pos, 48, digs, 56, grid,
                                 c->stream));
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     std::vector<uint64_t> dbase(256);
     HIPCHK(c, hipMemcpyAsync(dbase.data(), rp_digit_base(tmp, nt1), 256 * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    ms[0] += t;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev1, c->ev2));
     ms[1] += t;
     uint64_t* rs = h.data() + 4;
     uint64_t* tp = rs + 257;
@@ -1233,15 +1234,13 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
     HIPCHK(c, launch_rp_hist(digs, nullptr, 0, rt + 4, rt + 4 + 257, 256, nt2, (uint32_t)tile, pos, tmp, grid,
                              c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    HIPCHK(c, hipEventSynchronize(c->ev1));
-    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-    ms[0] += t;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_rp_scatter(NW, pay, b, sb, a, sa, pb, pa, rt + 4, rt + 4 + 257, 256, nt2, pos, 56, nullptr, 0,
                                 grid, c->stream));
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev2));
     HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+    ms[0] += t;
+    HIPCHK(c, hipEventElapsedTime(&t, c->ev1, c->ev2));
     ms[1] += t;
     return KC_OK;
 }
@@ -1412,30 +1411,35 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 const uint64_t rec0 = c->rec_n;
                 const uint64_t claimed0 = c->stats_h[ST_CLAIMED];
                 kc_status s2;
+                // P5a and P5 back to back, timed by three marks after P5's
+                // synchronisation (P5a's time: ev0 -> ev1, P5's: ev1 -> ev2)
+                bool p5a_pending = false;
                 if (dedup) {
                     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                     HIPCHK(c, launch_count_rec(c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, b0, b1,
                                                (uint32_t*)c->digs, (uint32_t*)c->part_dedup.p, c->n_cu, c->stream,
                                                over0 < over_limit ? c->pool_cursor : nullptr, over_limit,
                                                (uint64_t*)dd.pos));
-                    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-                    HIPCHK(c, hipEventSynchronize(c->ev1));
-                    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-                    c->dedup_ms += t;
+                    p5a_pending = true;
                 }
                 for (;;) {
                     if ((s2 = grow_records(c, rec0 + bound))) return s2;
                     // keys_b is free after S2: it takes P5's spills (W x key_cap words)
-                    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+                    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
                     HIPCHK(c, launch_count_skm(W, (int)c->k, c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p,
                                                b0, b1, count_keys, c->rec_keys, c->rec_cnts, c->rec_cap,
                                                c->rec_cursor, c->table, c->cap, c->keys_b, c->key_cap, c->stats,
                                                l.probe_limit, c->cfg.lds_slots, c->n_cu, c->stream,
                                                dedup ? &dd : nullptr, c->rec_dig));
-                    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+                    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
                     HIPCHK(c, hipMemcpyAsync(&c->rec_n, c->rec_cursor, 8, hipMemcpyDeviceToHost, c->stream));
                     if ((s2 = sync_stats(c))) return s2;
-                    HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                    if (p5a_pending) {
+                        HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+                        c->dedup_ms += t;
+                        p5a_pending = false;
+                    }
+                    HIPCHK(c, hipEventElapsedTime(&t, c->ev1, c->ev2));
                     c->part_ms[4] += t;
                     c->p5_launches++;
                     if (getenv("KC_DEBUG"))
@@ -2050,7 +2054,9 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     };
     if (hipSetDevice(cfg->device) != hipSuccess) return bail(KC_ERR_NODEVICE);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(KC_ERR_HIP);
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) return bail(KC_ERR_HIP);
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev2) != hipSuccess)
+        return bail(KC_ERR_HIP);
     uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
     if (M < (1u << 20)) M = 1u << 20;
     if ((cfg->flags & KC_FLAG_VARLEN) && (cfg->flags & KC_FLAG_ENGINE_TABLE)) {
@@ -2162,6 +2168,7 @@ void kc_destroy(kc_ctx* c) {
     if (c->stats_h) (void)hipHostFree(c->stats_h);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
