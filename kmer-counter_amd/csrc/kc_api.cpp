@@ -1842,7 +1842,7 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
                               uint64_t* n_rec_out, bool two_pass = false, bool no_spec = false) {
     kc_status s;
     uint64_t nch = fq_chunks(base, n);
-    if ((s = ensure(c, c->fq_counts, nch * 8 + 8)) || (s = ensure(c, c->fq_base, nch * 8)) ||
+    if ((s = ensure(c, c->fq_counts, nch * 8 + 16)) || (s = ensure(c, c->fq_base, nch * 8)) ||
         (s = ensure(c, c->fq_tmp, scan_tmp_elems(nch) * 8)))
         return s;
     if ((s = sync_stats(c))) return s;
@@ -1883,19 +1883,22 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
                                   c->stream));
         HIPCHK(c, launch_fq_spec_verify((const uint64_t*)c->fq_base.p, (const uint8_t*)c->fq_phase.p, nch, c->stats,
                                         c->stream));
+        // [nch]: the line total; [nch + 1]: the rows per chunk the kernel used
         uint64_t* total = (uint64_t*)c->fq_counts.p + nch;
         HIPCHK(c, launch_sum_last((const uint64_t*)c->fq_base.p, (const uint64_t*)c->fq_counts.p, nch, total, c->stream));
-        uint64_t lines = 0;
-        HIPCHK(c, hipMemcpyAsync(&lines, total, 8, hipMemcpyDeviceToHost, c->stream));
+        uint64_t lr[2] = {0, 0};
+        HIPCHK(c, hipMemcpyAsync(lr, total, 16, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev1, c->stream));
         if ((s = sync_stats(c))) return s;
         float t = 0.f;
         HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
         c->st.decode_ms += t;
-        if (c->stats_h[ST_ERR] == 0 && lines % 4 == 0 && lines > 0) {
+        const uint64_t lines = lr[0];
+        if (c->stats_h[ST_ERR] == 0 && lines % 4 == 0 && lines > 0 && lr[1] >= 1 &&
+            lr[1] <= fq_spec_rows_per_chunk((int)L)) {
             const uint64_t n_rec = lines / 4;
             if (n_rec_out) *n_rec_out = n_rec;
-            c->pend_reads += spec_rows;
+            c->pend_reads += nch * lr[1];  // rows the kernel used (<= the reserved spec_rows)
             c->pend_sparse = true;
             c->st.reads += n_rec;
             c->st.windows += n_rec * (uint64_t)(L - c->k + 1);

@@ -4500,7 +4500,7 @@ __device__ __forceinline__ u32 swar_group(u32 x0, u32 x1, u32 x2, u32 x3, int nb
 // records; stats[ST_VHOLE] is set when a read holds a not-ACGT base.
 template <bool VAR, bool SP = false>
 __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_FQ_WPE))) void fq_encode_k(const uint8_t* __restrict__ base, u64 n, u64 nchunks,
-                                                      const u64* __restrict__ line_base, u64 max_rec, int L, int G,
+                                                      const u64* __restrict__ line_base, u64 max_rec_in, int L, int G,
                                                       int lcap, u32* __restrict__ codes,
                                                       unsigned short* __restrict__ inval, u64* stats,
                                                       unsigned short* __restrict__ rlen, int k,
@@ -4566,6 +4566,31 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
     u32 sp_phi = 0;
     bool sp_fail = false;
     u64 rbase = 0, rowoff = 0;
+    u64 max_rec = max_rec_in;
+    if constexpr (SP) {
+        // rows per chunk for this block: records are at least 2L + 5 + h
+        // bytes with h the header line's length; h from the block's first
+        // header less a margin (header lengths differ by the read number's
+        // digits). A chunk denser than that reports ERR_FQ_TOO_MANY and the
+        // block takes the two-kernel index. max_rec_in assumes h = 1.
+        u32 h0 = 1;
+        bool found = false;
+        for (u32 b0 = 0; b0 < 1024u && !found; b0 += 256u) {
+            const u64 o = (u64)b0 + 4u * (u32)lane;
+            int pos = -1;
+#pragma unroll
+            for (int b = 3; b >= 0; b--)
+                if (o + (u64)b < n && base[o + (u64)b] == (uint8_t)'\n') pos = (int)(o + (u64)b);
+            const u64 bm = __ballot(pos >= 0);
+            if (bm) {
+                h0 = (u32)__builtin_amdgcn_readlane(pos, __ffsll((long long)bm) - 1);
+                found = true;
+            }
+        }
+        const u64 hmin = h0 > 17u ? (u64)h0 - 16u : 1u;
+        max_rec = min(max_rec_in, 1 + (kFqChunk - 1) / (2 * (u64)L + 5 + hmin));
+        if (blockIdx.x == 0 && threadIdx.x == 0) sp_cnt[nchunks + 1] = max_rec;
+    }
     if (c < nchunks) issue(c, 0);
     while (c < nchunks) {
         {

@@ -141,6 +141,27 @@ def test_onepass_only_for_the_f3_front_end(kca, orc, monkeypatch, capfd, k, used
     assert _onepass_missed(capfd) == used
 
 
+@pytest.mark.parametrize("first,rest,missed", [(60, (58, 62), False), (8, (1, 12), False), (300, (1, 3), True)])
+def test_onepass_rows_per_chunk_from_first_header(kca, orc, monkeypatch, capfd, first, rest, missed):
+    """Rows per chunk are sized from the block's first header (less a
+    16-character margin): uniform long headers take the one-pass index with
+    fewer empty rows; a block whose later headers are much shorter than its
+    first overfills a chunk's rows and is re-indexed by the two-kernel path.
+    Either way the same records as the oracle."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    L, k = 150, 31
+    rng = random.Random(first)
+    recs = []
+    for i in range(6000):
+        hl = first if i == 0 else rng.randrange(rest[0], rest[1] + 1)
+        h = ("r" + str(i) + "x" * hl)[:hl] if hl > 0 else ""
+        recs.append(f"@{h}\n" + "".join(rng.choice("ACGT") for _ in range(L)) + "\n+\n" + "I" * L + "\n")
+    fq = "".join(recs).encode()
+    capfd.readouterr()
+    assert _count(kca, fq, k, L, "onepass", monkeypatch) == (6000, orc.count_fastq(fq, k))
+    assert _onepass_missed(capfd) == missed
+
+
 def test_onepass_rows_through_the_key_prefix_engine(kca, orc, monkeypatch):
     """iid reads at k = 31 (no coverage): the one-pass rows are indexed for
     F3, then the coverage sketch hands the batch to the key-prefix engine,
