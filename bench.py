@@ -39,9 +39,12 @@ counts reads [r R, (r+1) R) of the one read stream (weak scaling).
     file); the parts in rank order are the node's SortedKMerFile.
   --exchange files (default of --config 3; cfg3 as BASELINE.json states it:
     read-shard, no RCCL, host KMerFileMerger k-way merge): every rank writes
-    its sorted run as a SortedKMerFile and rank 0 merges the N files on the
-    host (kc_merge_files: one k-way level, key ranges merged by all usable
-    CPUs); the step includes the run files and the merge.
+    its sorted run as a SortedKMerFile, then every rank merges one key range
+    of all N files on the host (kc_merge_part_create: one k-way level, the
+    range cut into sub-ranges merged by the rank's share of the CPUs) and
+    writes it at its offset of the one output file (--files-merge rank0:
+    rank 0 merges everything, kc_merge_files); the step includes the run
+    files and the merge.
   --exchange none (read-shard variant over RCCL): the runs are gathered to
     rank 0's GPU (RCCL) and merged there (device merge path), rank 0 writes
     the file.
@@ -233,26 +236,60 @@ def gather_runs_to_rank0(kca, ctx, D):
     return 0
 
 
-def host_merge_runs(kca, ctx, D, run_dir, out_path, k, fan_in=0, threads=0):
+def merge_threads(D):
+    """Host threads one rank may use: the usable CPUs shared by the node's local ranks."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(D.world)))
+    return max(1, usable_cpus() // max(1, local))
+
+
+def host_merge_runs(kca, ctx, D, run_dir, out_path, k, threads=0, where="ranks", timing=None):
     """cfg3 as BASELINE.json states it (read-shard, no RCCL, host
-    KMerFileMerger k-way merge; KMerFileMergeHandler.cpp:49-100,
+    KMerFileMerger k-way merge; KMerFileMergeHandler.cpp:41-123,
     KMerFileMerger.cpp:49-96): every rank writes its sorted run as a
-    SortedKMerFile into run_dir (kc_write_output), and rank 0 merges the N
-    files into out_path with kc_merge_files (fan-in noOfMergersAtOnce, default
-    N: one k-way level; noOfMergeThreads threads, default the usable CPUs:
-    the last level merges key ranges in parallel). The barriers only order the
-    ranks (no data moves through a collective). The files are overwritten in
-    place each step. Returns rank 0's merged record count (0 on other ranks)."""
+    SortedKMerFile into run_dir (kc_write_output), then the N run files are
+    merged into out_path.
+      where="ranks" (default): the merge is shared by the ranks, as the
+        reference runs its merge groups concurrently: rank r merges the r-th key
+        range of all N files (kc_merge_part_create; the ranges' boundary keys
+        come from the files by one deterministic rule, so no rank sends another
+        any records), the ranks all-gather their merged sizes (one integer each
+        over the process group: control, not data) and each writes its range at
+        its offset of the one output file (kc_merge_part_write).
+      where="rank0": rank 0 merges all N files alone (kc_merge_files).
+    `threads` per rank (default: the usable CPUs shared by the node's ranks).
+    The barriers only order the ranks. The files are overwritten in place each
+    step. `timing` (a dict, optional) accumulates this rank's seconds in
+    run_file / merge / write. Returns (records in the node's output, output
+    bytes this rank wrote)."""
+    tm = timing if timing is not None else {}
+    t0 = time.perf_counter()
     run = os.path.join(run_dir, f"kc_cfg3.run{D.rank}")
     ctx.write_output(run)
     D.barrier_sync()
-    n = 0
-    if D.rank == 0:
-        runs = [os.path.join(run_dir, f"kc_cfg3.run{r}") for r in range(D.world)]
-        kca.merge_files(runs, out_path, k, fan_in or D.world, threads or usable_cpus())
-        n = os.path.getsize(out_path) // ctx.rs
+    t1 = time.perf_counter()
+    tm["run_file"] = tm.get("run_file", 0.0) + (t1 - t0)
+    runs = [os.path.join(run_dir, f"kc_cfg3.run{r}") for r in range(D.world)]
+    thr = threads or merge_threads(D)
+    if where == "rank0":
+        n, mine = 0, 0
+        if D.rank == 0:
+            kca.merge_files(runs, out_path, k, D.world, threads or usable_cpus())
+            mine = os.path.getsize(out_path)
+            n = mine // ctx.rs
+        D.barrier_sync()
+        tm["merge"] = tm.get("merge", 0.0) + (time.perf_counter() - t1)
+        return n, mine
+    with kca.MergePart(runs, k, D.rank, D.world, thr) as part:
+        sizes = D.all_gather_int(part.nbytes)
+        t2 = time.perf_counter()
+        total = sum(sizes)
+        part.write(out_path, sum(sizes[:D.rank]), total)
+        mine = part.nbytes
     D.barrier_sync()
-    return n
+    t3 = time.perf_counter()
+    tm["merge"] = tm.get("merge", 0.0) + (t2 - t1)
+    tm["write"] = tm.get("write", 0.0) + (t3 - t2)
+    return total // ctx.rs, mine
 
 
 def write_node_output(kca, ctx, D, path, exchange):
@@ -274,8 +311,9 @@ def write_node_output(kca, ctx, D, path, exchange):
         ctx.write_output(f"{path}.part{D.rank}")
         return n * ctx.rs
     if exchange == "files":
-        n = host_merge_runs(kca, ctx, D, os.path.dirname(path) or ".", path, ctx.k)
-        return n * ctx.rs
+        _, mine = host_merge_runs(kca, ctx, D, os.path.dirname(path) or ".", path, ctx.k,
+                                  where=getattr(D, "files_merge", "ranks"))
+        return mine
     n = gather_runs_to_rank0(kca, ctx, D)
     if D.rank == 0:
         ctx.write_output(path)
@@ -327,7 +365,9 @@ def main(args, D, state):
     ptr, nbytes = ctx.synth_device(args.reads, L, args.seed, args.genome, 0.0, first, lmin)
     state["ptr"] = ptr
     exchange = args.exchange if D.world > 1 else "none"
+    D.files_merge = args.files_merge
     run_dir = None
+    files_tm = {}
     if exchange == "files":
         # the ranks' run files and rank 0's merged file (SortedKMerFile each)
         local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", str(D.world)))
@@ -360,7 +400,8 @@ def main(args, D, state):
             xch_ms[0] += (time.perf_counter() - t) * 1e3
         elif exchange == "files":
             t = time.perf_counter()
-            n = host_merge_runs(kca, ctx, D, run_dir, os.path.join(run_dir, "kc_cfg3.out"), k)
+            n, _ = host_merge_runs(kca, ctx, D, run_dir, os.path.join(run_dir, "kc_cfg3.out"), k,
+                                   where=args.files_merge, timing=files_tm)
             xch_ms[0] += (time.perf_counter() - t) * 1e3
         return n
 
@@ -368,6 +409,7 @@ def main(args, D, state):
         dev_step()
     D.barrier_sync()
     xch_ms[0] = 0.0
+    files_tm.clear()
     acc = {"insert_ms": 0.0, "finish_ms": 0.0, "decode_ms": 0.0, "dedup_ms": 0.0, "presplit_ms": 0.0, "launches": 0,
            "part_ms": [0.0] * 5}
     t0 = time.perf_counter()
@@ -396,6 +438,10 @@ def main(args, D, state):
                                   "finish": acc["finish_ms"] / args.steps,
                                   "exchange_rank0": xch_ms[0] / args.steps,
                                   "exchange": exchange,
+                                  **({"files_merge": args.files_merge, "merge_threads_per_rank": merge_threads(D),
+                                      "files_ms_rank0": {key: round(v / args.steps * 1e3, 2)
+                                                         for key, v in files_tm.items()}}
+                                     if exchange == "files" else {}),
                                   "partition_passes": [round(x / args.steps, 3) for x in acc["part_ms"]],
                                   "p5a_dedup": round(acc["dedup_ms"] / args.steps, 3),
                                   "p3b_presplit (in partition_passes[2])": round(acc["presplit_ms"] / args.steps, 3)},
@@ -447,10 +493,15 @@ def main(args, D, state):
                     f"(rank-order concatenation = the SortedKMerFile)")
         parallelism = f"read-shard count + key-space all-to-all x{D.world}"
     elif exchange == "files":
-        workload = (f"cfg3 at {D.world} GPUs as BASELINE.json states it: {base}; read-shard, no RCCL: each rank's "
-                    f"sorted run written as a SortedKMerFile, rank 0's host k-way merge (kc_merge_files, "
-                    f"KMerFileMerger semantics) into the node's SortedKMerFile; step = count + run files + merge")
-        parallelism = f"read-shard x{D.world} + host k-way merge on rank 0"
+        by = ("shared by the ranks: rank r merges the r-th key range of every run file (kc_merge_part_create) "
+              "and writes it at its offset of the one output file" if args.files_merge == "ranks"
+              else "on rank 0 alone (kc_merge_files)")
+        workload = (f"cfg3 at {D.world} GPUs as BASELINE.json states it: {base}; read-shard, no RCCL on the data "
+                    f"path: each rank's sorted run written as a SortedKMerFile, then the host k-way merge "
+                    f"(KMerFileMerger semantics) into the node's SortedKMerFile, {by}; step = count + run files + "
+                    f"merge")
+        parallelism = (f"read-shard x{D.world} + host k-way merge "
+                       f"{'by key range on every rank' if args.files_merge == 'ranks' else 'on rank 0'}")
     else:
         workload = (f"cfg3 pattern at {D.world} GPUs: {base}; {path_desc}; runs gathered to rank 0's GPU "
                     f"(RCCL) and merged there by merge path")
@@ -510,6 +561,8 @@ def e2e_leg(kca, ctx, D, args, state, ptr, nbytes, exchange, windows_of_step):
     # the same directory: room for all of them (at N = 8, cfg2: ~160 GB)
     local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", str(D.world)))
     need = local_ranks * (nbytes + 2 * out_est) + (1 << 30)
+    if exchange == "files":
+        need += local_ranks * out_est  # each rank's run file (kc_cfg3.run<r>) next to the output
     workdir, free, tried = pick_workdir(args.workdir, need)
     if workdir is None:
         return {"skipped": f"no directory with {need / 1e9:.1f} GB free for the input file and one output file",
@@ -518,6 +571,9 @@ def e2e_leg(kca, ctx, D, args, state, ptr, nbytes, exchange, windows_of_step):
     in_path = os.path.join(workdir, f"kc_bench_in.{tag}.fq")
     out_path = os.path.join(workdir, f"kc_bench_out.{os.getpid() if D.world == 1 else 'node'}.bin")
     state.setdefault("files", []).append(in_path)
+    run_file = os.path.join(workdir, f"kc_cfg3.run{D.rank}")  # written by host_merge_runs (exchange files)
+    if exchange == "files":
+        state["files"].append(run_file)
     write_input_file(ctx, ptr, nbytes, in_path)
     state["in_path"] = in_path
     varlen = 0 < args.min_read_length < args.L
@@ -561,6 +617,9 @@ def e2e_leg(kca, ctx, D, args, state, ptr, nbytes, exchange, windows_of_step):
     ph = {key: v / args.steps * 1e3 for key, v in phase.items()}
     _unlink(in_path)
     state["files"].remove(in_path)
+    if exchange == "files":
+        _unlink(run_file)
+        state["files"].remove(run_file)
     state.pop("in_path", None)
     return {"value": win / step_s, "ms_per_step": step_s * 1e3,
             "path": ("FASTQ file (page cache) -> pinned blocks -> PCIe -> GPU decode + count -> sorted records -> "
@@ -608,6 +667,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-variants", action="store_true", help="skip the host_memory / reference_chunks lines")
     ap.add_argument("--workdir", default=None, help="input/output files (default: $TMPDIR, /tmp, /dev/shm, ... "
                                                     "whichever has the space)")
+    ap.add_argument("--files-merge", default="ranks", choices=["ranks", "rank0"],
+                    help="--exchange files: the run files' k-way merge shared by the ranks (each merges one key "
+                         "range of every file and writes it at its offset of the one output file; default) or "
+                         "done by rank 0 alone")
     ap.add_argument("--min-read-length", type=int, default=0,
                     help="variable-length reads of M..L bases (KC_FLAG_VARLEN); 0 = every read has L bases")
     ap.add_argument("--exchange", default=None, choices=["alltoall", "none", "files"],

@@ -332,6 +332,23 @@ kc_status kc_copy_device(kc_ctx* ctx, void* d_dst, const void* d_src, uint64_t n
 kc_status kc_merge_files(const char* const* inputs, uint32_t n_inputs, const char* output,
                          int64_t kmer_length, uint32_t merge_fan_in, uint32_t merge_threads);
 
+/* The same merge shared by `parts` processes (the ranks of a read-shard job,
+ * SURVEY §8e cfg3; the reference runs its merge groups concurrently,
+ * KMerFileMergeHandler.cpp:41-123). Every process opens the same input files;
+ * the key space is cut into `parts` ranges at keys chosen from the files by a
+ * deterministic rule (no data exchange), and kc_merge_part_create merges range
+ * `part` (by up to merge_threads threads) into host memory, reporting its
+ * merged size. The caller gathers the sizes (an all-gather of one u64 per
+ * process); part p is written at the sum of the sizes of parts 0..p-1 by
+ * kc_merge_part_write, which also cuts the file to file_bytes (the sum of all
+ * sizes; 0 = no cut). The parts written side by side are the bytes
+ * kc_merge_files writes. kc_merge_part_destroy frees a part. */
+typedef struct kc_merge_part kc_merge_part;
+kc_status kc_merge_part_create(const char* const* inputs, uint32_t n_inputs, int64_t kmer_length, uint32_t part,
+                               uint32_t parts, uint32_t merge_threads, kc_merge_part** out, uint64_t* n_bytes);
+kc_status kc_merge_part_write(kc_merge_part* p, const char* output, uint64_t offset, uint64_t file_bytes);
+void kc_merge_part_destroy(kc_merge_part* p);
+
 /* ---- synthetic input (bench/test data; not on the counting path) ---------- */
 uint64_t kc_synth_fastq_bytes(const kc_synth_spec* spec);
 /* Writes the FASTQ text of spec into host memory (dst_bytes >= kc_synth_fastq_bytes). */

@@ -166,6 +166,9 @@ def lib() -> ctypes.CDLL:
         "kc_count_file": ([P(vp), u32, ctypes.c_char_p, i64, u32, P(u64)], ctypes.c_int),
         "kc_write_output_at": ([vp, ctypes.c_char_p, u64], ctypes.c_int),
         "kc_gather_contexts": ([P(vp), u32], ctypes.c_int),
+        "kc_merge_part_create": ([P(ctypes.c_char_p), u32, i64, u32, u32, u32, P(vp), P(u64)], ctypes.c_int),
+        "kc_merge_part_write": ([vp, ctypes.c_char_p, u64, u64], ctypes.c_int),
+        "kc_merge_part_destroy": ([vp], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -199,6 +202,48 @@ def merge_files(inputs: List[str], output: str, kmer_length: int, fan_in: int = 
     st = L.kc_merge_files(arr, len(inputs), output.encode(), kmer_length, fan_in, threads)
     if st:
         raise KcError(st, L.kc_strerror(st).decode())
+
+
+class MergePart:
+    """One part of a host k-way merge shared by `parts` processes over the same
+    run files (kc_merge_part_create): cfg3's ranks each merge one key range of
+    every rank's run file, then write it at its offset of the one output file
+    (the offsets are the prefix sums of the parts' sizes, gathered by the
+    caller). Use as a context manager or call close()."""
+
+    def __init__(self, inputs: List[str], kmer_length: int, part: int, parts: int, threads: int = 1):
+        self._L = lib()
+        arr = (ctypes.c_char_p * max(1, len(inputs)))(*[p.encode() for p in inputs])
+        h = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        st = self._L.kc_merge_part_create(arr, len(inputs), kmer_length, part, parts, threads, ctypes.byref(h),
+                                          ctypes.byref(n))
+        if st:
+            raise KcError(st, self._L.kc_strerror(st).decode())
+        self._h = h
+        self.nbytes = int(n.value)
+
+    def write(self, output: str, offset: int, file_bytes: int = 0) -> None:
+        st = self._L.kc_merge_part_write(self._h, output.encode(), offset, file_bytes)
+        if st:
+            raise KcError(st, self._L.kc_strerror(st).decode())
+
+    def close(self) -> None:
+        if self._h:
+            self._L.kc_merge_part_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:

@@ -15,6 +15,8 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <memory>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -3251,6 +3253,44 @@ kc_status kc_merge_files(const char* const* inputs, uint32_t n_inputs, const cha
     if (!merge_tree(src, output, W, fan_in, threads, std::string(output) + ".kctmp", &err)) return KC_ERR_IO;
     return KC_OK;
 }
+
+struct kc_merge_part {
+    kc::MergedPart part;
+};
+
+kc_status kc_merge_part_create(const char* const* inputs, uint32_t n_inputs, int64_t kmer_length, uint32_t part,
+                               uint32_t parts, uint32_t threads, kc_merge_part** out, uint64_t* n_bytes) {
+    if (!out || kmer_length < 1 || kmer_length > KC_MAX_K || (n_inputs && !inputs) || parts < 1 || part >= parts)
+        return KC_ERR_ARG;
+    *out = nullptr;
+    const int W = (int)((kmer_length + 31) / 32);
+    std::vector<RunSource> src;
+    for (uint32_t i = 0; i < n_inputs; i++) {
+        if (!inputs[i]) return KC_ERR_ARG;
+        RunSource r;
+        r.path = inputs[i];
+        src.push_back(r);
+    }
+    std::unique_ptr<kc_merge_part> p(new (std::nothrow) kc_merge_part());
+    if (!p) return KC_ERR_NOMEM;
+    int e = 0;
+    try {
+        if (!kc::merge_runs_part(src, W, part, parts, threads ? threads : 1, &p->part, &e)) return KC_ERR_IO;
+    } catch (const std::bad_alloc&) {
+        return KC_ERR_NOMEM;
+    }
+    if (n_bytes) *n_bytes = p->part.bytes;
+    *out = p.release();
+    return KC_OK;
+}
+
+kc_status kc_merge_part_write(kc_merge_part* p, const char* output, uint64_t offset, uint64_t file_bytes) {
+    if (!p || !output) return KC_ERR_ARG;
+    if (file_bytes && offset + p->part.bytes > file_bytes) return KC_ERR_ARG;
+    return kc::write_part_at(p->part, output, offset, file_bytes) ? KC_OK : KC_ERR_IO;
+}
+
+void kc_merge_part_destroy(kc_merge_part* p) { delete p; }
 
 uint64_t kc_synth_fastq_bytes(const kc_synth_spec* sp) {
     if (!sp) return 0;

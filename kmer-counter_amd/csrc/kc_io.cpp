@@ -326,87 +326,187 @@ static uint64_t merge_slices_w(const std::vector<const uint8_t*>& beg, const std
     return (uint64_t)(o - dst);
 }
 
+// One-word keys (every k <= 32, cfg2/cfg3), at most M runs: a merge by
+// output key rather than by input record. Each step takes the smallest head
+// key of the live runs and consumes that key from every run whose head holds
+// it, summing the counts; all M lanes do the same work each step (selects, no
+// data-dependent branches), so the compiler keeps the heads in registers and
+// nothing mispredicts. A read-shard job's runs cover one genome, so most keys
+// are in most runs and a step emits one output record for ~M input records
+// (the per-record min scan did ~M unpredictable compares per input record).
+// An exhausted lane reads its last record again (a valid address) and stays
+// dead; a key repeated inside one run (not written by the library, but valid
+// SortedKMerFile input) is folded into the previous output record.
+template <int M>
+static uint64_t merge_keys_w1(const std::vector<const uint8_t*>& beg, const std::vector<const uint8_t*>& end,
+                              uint8_t* dst) {
+    static const uint8_t dead_rec[12] = {0};
+    const uint8_t* cur[M];
+    const uint8_t* lim[M];
+    const uint8_t* tail[M];
+    uint64_t hk[M];
+    uint32_t hc[M];
+    uint32_t al[M];
+    int j = 0;
+    for (size_t i = 0; i < beg.size(); i++)
+        if (beg[i] < end[i]) {
+            cur[j] = beg[i], lim[j] = end[i], tail[j] = end[i] - 12, al[j] = 1;
+            j++;
+        }
+    for (; j < M; j++) cur[j] = lim[j] = tail[j] = dead_rec, al[j] = 0;
+    uint32_t any = 0;
+    for (int i = 0; i < M; i++) {
+        const uint8_t* src = al[i] ? cur[i] : tail[i];
+        hk[i] = ld64(src);
+        memcpy(&hc[i], src + 8, 4);
+        any |= al[i];
+    }
+    uint8_t* o = dst;
+    uint64_t lastk = 0;
+    while (any) {
+        uint64_t mn = ~0ull;
+        for (int i = 0; i < M; i++) {
+            const uint64_t kk = al[i] ? hk[i] : ~0ull;
+            mn = kk < mn ? kk : mn;
+        }
+        uint32_t sum = 0;
+        any = 0;
+        for (int i = 0; i < M; i++) {
+            const bool e = al[i] && hk[i] == mn;
+            sum += e ? hc[i] : 0u;
+            const uint8_t* nx = cur[i] + (e ? 12 : 0);
+            const uint32_t a = nx < lim[i] ? al[i] : 0u;
+            const uint8_t* src = a ? nx : tail[i];
+            cur[i] = nx;
+            hk[i] = ld64(src);
+            memcpy(&hc[i], src + 8, 4);
+            al[i] = a;
+            any |= a;
+        }
+        const bool fold = o != dst && mn == lastk;
+        uint8_t* t = fold ? o - 12 : o;
+        uint32_t prev;
+        memcpy(&prev, fold ? o - 4 : dead_rec, 4);
+        sum += fold ? prev : 0u;
+        memcpy(t, &mn, 8);
+        memcpy(t + 8, &sum, 4);
+        o = t + 12;
+        lastk = mn;
+    }
+    return (uint64_t)(o - dst);
+}
+
+static uint64_t merge_slices_w1(const std::vector<const uint8_t*>& beg, const std::vector<const uint8_t*>& end,
+                                uint8_t* dst) {
+    size_t m = 0;
+    for (size_t i = 0; i < beg.size(); i++) m += beg[i] < end[i];
+    if (m <= 4) return merge_keys_w1<4>(beg, end, dst);
+    if (m <= 8) return merge_keys_w1<8>(beg, end, dst);
+    if (m <= 16) return merge_keys_w1<16>(beg, end, dst);
+    return merge_slices_w<1>(beg, end, dst);
+}
+
 static uint64_t merge_slices(const std::vector<const uint8_t*>& beg, const std::vector<const uint8_t*>& end, int W,
                              uint8_t* dst) {
     switch (W) {
-    case 1: return merge_slices_w<1>(beg, end, dst);
+    case 1: return merge_slices_w1(beg, end, dst);
     case 2: return merge_slices_w<2>(beg, end, dst);
     case 3: return merge_slices_w<3>(beg, end, dst);
     default: return merge_slices_w<4>(beg, end, dst);
     }
 }
 
-}  // namespace
-
-bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t threads,
-                         int* err_no) {
-    const int rs = 8 * W + 4;
-    if (threads < 1) threads = 1;
-    std::vector<RunAccess> acc(runs.size());
-    uint64_t total = 0;
-    for (size_t i = 0; i < runs.size(); i++) {
-        if (!acc[i].open_src(runs[i], rs)) {
-            if (err_no) *err_no = errno ? errno : EIO;
-            return false;
-        }
-        total += acc[i].n;
-    }
+// Cuts run slices [lo, hi) into ranges of about range_recs() input records
+// (bounds[r][i] = run i's first record of range r; the last entry is hi). A
+// range is split at the middle key of the run holding most of its records;
+// when that key is also the range's first key in every run (a long repeat),
+// the cut moves past the repeat (upper bound), so no worker is handed the
+// whole remainder. A range of one repeated key stays whole.
+static bool plan_ranges(const std::vector<RunAccess>& acc, int W, const std::vector<uint64_t>& lo0,
+                        const std::vector<uint64_t>& hi0, std::vector<std::vector<uint64_t>>* bounds, int* err_no) {
     const int m = (int)acc.size();
-    // ranges: bounds[r][i] = run i's first record of range r. Split the
-    // key space at keys of the run holding the most records of a range until
-    // every range holds about kRangeRecs records (a range of one repeated key
-    // cannot be split and stays whole).
-    std::vector<std::vector<uint64_t>> bounds;
     const uint64_t rr = range_recs();
-    {
-        std::vector<uint64_t> lo(m, 0), hi(m);
-        for (int i = 0; i < m; i++) hi[i] = acc[i].n;
-        std::vector<std::pair<std::vector<uint64_t>, std::vector<uint64_t>>> todo;
-        todo.push_back({lo, hi});
-        std::vector<std::pair<std::vector<uint64_t>, std::vector<uint64_t>>> done;
-        uint8_t key[8 * 4 + 4];
-        while (!todo.empty()) {
-            auto rg = todo.back();
-            todo.pop_back();
-            uint64_t n = 0, best = 0;
-            int bi = 0;
-            for (int i = 0; i < m; i++) {
-                const uint64_t c = rg.second[i] - rg.first[i];
-                n += c;
-                if (c > best) best = c, bi = i;
-            }
-            bool split = false;
-            if (n > 2 * rr && best > 1) {
-                const uint64_t mid = rg.first[bi] + best / 2;
-                if (!acc[bi].read(mid, 1, key)) {
-                    if (err_no) *err_no = errno ? errno : EIO;
-                    return false;
-                }
-                std::vector<uint64_t> cut(m);
-                for (int i = 0; i < m; i++)
-                    if (!acc[i].lower_bound(key, W, rg.first[i], rg.second[i], &cut[i])) {
-                        if (err_no) *err_no = errno ? errno : EIO;
-                        return false;
-                    }
-                uint64_t left = 0, right = 0;
-                for (int i = 0; i < m; i++) left += cut[i] - rg.first[i], right += rg.second[i] - cut[i];
-                if (left > 0 && right > 0) {
-                    todo.push_back({cut, rg.second});  // right half later: ranges come out in key order
-                    todo.push_back({rg.first, cut});
-                    split = true;
-                }
-            }
-            if (!split) done.push_back(rg);
-        }
-        for (auto& d : done) bounds.push_back(d.first);
-        bounds.push_back(std::vector<uint64_t>(hi));
-    }
-    const size_t nr = bounds.size() - 1;
-    int fd = ::open(out.c_str(), O_WRONLY | O_CREAT, 0644);
-    if (fd < 0) {
-        if (err_no) *err_no = errno;
+    using Rg = std::pair<std::vector<uint64_t>, std::vector<uint64_t>>;
+    std::vector<Rg> todo{{lo0, hi0}}, done;
+    uint8_t key[8 * 4 + 4], rec[8 * 4 + 4];
+    auto io_fail = [&]() {
+        if (err_no) *err_no = errno ? errno : EIO;
         return false;
+    };
+    while (!todo.empty()) {
+        Rg rg = todo.back();
+        todo.pop_back();
+        uint64_t n = 0, best = 0;
+        int bi = 0;
+        for (int i = 0; i < m; i++) {
+            const uint64_t c = rg.second[i] - rg.first[i];
+            n += c;
+            if (c > best) best = c, bi = i;
+        }
+        bool split = false;
+        if (n > 2 * rr && best > 1) {
+            if (!acc[bi].read(rg.first[bi] + best / 2, 1, key)) return io_fail();
+            std::vector<uint64_t> cut(m);
+            for (int i = 0; i < m; i++)
+                if (!acc[i].lower_bound(key, W, rg.first[i], rg.second[i], &cut[i])) return io_fail();
+            uint64_t left = 0, right = 0;
+            for (int i = 0; i < m; i++) left += cut[i] - rg.first[i], right += rg.second[i] - cut[i];
+            if (left == 0) {
+                // the middle key is the smallest key of the range: cut after
+                // every copy of it instead (first record with a larger key)
+                for (int i = 0; i < m; i++) {
+                    uint64_t a = rg.first[i], b = rg.second[i];
+                    while (a < b) {
+                        const uint64_t mid = a + (b - a) / 2;
+                        if (!acc[i].read(mid, 1, rec)) return io_fail();
+                        if (key_compare(rec, key, W) <= 0)
+                            a = mid + 1;
+                        else
+                            b = mid;
+                    }
+                    cut[i] = a;
+                }
+                left = right = 0;
+                for (int i = 0; i < m; i++) left += cut[i] - rg.first[i], right += rg.second[i] - cut[i];
+            }
+            if (left > 0 && right > 0) {
+                todo.push_back({cut, rg.second});  // right half later: ranges come out in key order
+                todo.push_back({rg.first, cut});
+                split = true;
+            }
+        }
+        if (!split) done.push_back(rg);
     }
+    bounds->clear();
+    for (auto& d : done) bounds->push_back(d.first);
+    bounds->push_back(hi0);
+    return true;
+}
+
+// Workers merging one range at a time need an input and a result buffer of up
+// to ~2 range_recs() records each; the pool is capped so that those buffers
+// stay within kMergeMemBudget however many CPUs the host has.
+static const uint64_t kMergeMemBudget = 4ull << 30;
+
+static uint32_t merge_workers(uint32_t threads, size_t ranges, int rs) {
+    const uint64_t per = 2 * (2 * range_recs() * (uint64_t)rs);
+    const uint64_t cap = std::max<uint64_t>(1, kMergeMemBudget / std::max<uint64_t>(1, per));
+    uint64_t t = std::max<uint32_t>(1, threads);
+    t = std::min<uint64_t>(t, cap);
+    t = std::min<uint64_t>(t, std::max<size_t>(1, ranges));
+    return (uint32_t)t;
+}
+
+// Merges every range of `bounds` by `threads` workers, in key order of
+// completion commitment: `sink(r, data, bytes, offset)` receives range r's
+// merged bytes and their offset from the first range (prefix sum of the
+// merged sizes; called once per range, in any order, from the workers).
+template <class Sink>
+static bool merge_ranges(const std::vector<RunAccess>& acc, int W, const std::vector<std::vector<uint64_t>>& bounds,
+                         uint32_t threads, uint64_t* total_bytes, int* err_no, Sink sink) {
+    const int rs = 8 * W + 4;
+    const int m = (int)acc.size();
+    const size_t nr = bounds.size() - 1;
     std::mutex mu;
     std::condition_variable cv;
     size_t committed = 0;  // ranges whose output offset is known
@@ -445,27 +545,183 @@ bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& 
                 committed = r + 1;
             }
             cv.notify_all();
-            size_t put = 0;
-            while (ok && put < nbytes) {
-                ssize_t w = pwrite(fd, res.data() + put, (size_t)(nbytes - put), (off_t)(off + put));
-                if (w <= 0) {
-                    if (w < 0 && errno == EINTR) continue;
-                    bad = errno ? errno : EIO;
-                    ok = false;
-                }
-                put += w > 0 ? (size_t)w : 0;
-            }
+            if (ok && !sink(r, res.data(), nbytes, off)) bad = errno ? errno : EIO;
         }
     };
     std::vector<std::thread> pool;
-    for (uint32_t t = 0; t < threads && t < nr; t++) pool.emplace_back(work);
+    const uint32_t nt = merge_workers(threads, nr, rs);
+    for (uint32_t t = 0; t < nt; t++) pool.emplace_back(work);
     for (auto& t : pool) t.join();
+    *total_bytes = next_off;
+    if (bad.load()) {
+        if (err_no) *err_no = bad.load();
+        return false;
+    }
+    return true;
+}
+
+static bool pwrite_all(int fd, const uint8_t* p, uint64_t n, uint64_t off) {
+    uint64_t put = 0;
+    while (put < n) {
+        ssize_t w = pwrite(fd, p + put, (size_t)(n - put), (off_t)(off + put));
+        if (w <= 0) {
+            if (w < 0 && errno == EINTR) continue;
+            if (w == 0) errno = EIO;
+            return false;
+        }
+        put += (uint64_t)w;
+    }
+    return true;
+}
+
+static bool open_runs(const std::vector<RunSource>& runs, int rs, std::vector<RunAccess>* acc, int* err_no) {
+    *acc = std::vector<RunAccess>(runs.size());
+    for (size_t i = 0; i < runs.size(); i++)
+        if (!(*acc)[i].open_src(runs[i], rs)) {
+            if (err_no) *err_no = errno ? errno : EIO;
+            return false;
+        }
+    return true;
+}
+
+}  // namespace
+
+bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t threads,
+                         int* err_no) {
+    const int rs = 8 * W + 4;
+    std::vector<RunAccess> acc;
+    if (!open_runs(runs, rs, &acc, err_no)) return false;
+    const int m = (int)acc.size();
+    std::vector<uint64_t> lo(m, 0), hi(m);
+    for (int i = 0; i < m; i++) hi[i] = acc[i].n;
+    std::vector<std::vector<uint64_t>> bounds;
+    if (!plan_ranges(acc, W, lo, hi, &bounds, err_no)) return false;
+    int fd = ::open(out.c_str(), O_WRONLY | O_CREAT, 0644);
+    if (fd < 0) {
+        if (err_no) *err_no = errno;
+        return false;
+    }
+    uint64_t total = 0;
+    bool ok = merge_ranges(acc, W, bounds, threads, &total, err_no,
+                           [&](size_t, const uint8_t* p, uint64_t n, uint64_t off) { return pwrite_all(fd, p, n, off); });
     // written in place, cut to size (no truncation of an old file first)
-    bool ok = !bad.load();
-    if (ok && ftruncate(fd, (off_t)next_off) != 0) bad = errno, ok = false;
-    if (::close(fd) != 0 && ok) bad = errno, ok = false;
-    if (!ok && err_no) *err_no = bad.load();
-    (void)total;
+    if (ok && ftruncate(fd, (off_t)total) != 0) {
+        if (err_no) *err_no = errno;
+        ok = false;
+    }
+    if (::close(fd) != 0 && ok) {
+        if (err_no) *err_no = errno;
+        ok = false;
+    }
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// One part of a merge shared by several processes (the ranks of a read-shard
+// job, cfg3). Part boundaries are keys chosen from the runs themselves by a
+// deterministic rule, so every process computes the same cuts from the same
+// files without exchanging anything: boundary j (of parts - 1) aims at
+// j / parts of all input records; its candidates are the record at that
+// fraction of each run, and the candidate whose rank (records below it, summed
+// over the runs by binary search) is closest to the target wins; boundaries
+// are made non-decreasing. A key's copies in every run fall on one side of
+// each boundary, so the parts' merges concatenate to the whole merge.
+// ---------------------------------------------------------------------------
+
+bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, uint32_t parts, uint32_t threads,
+                     MergedPart* out, int* err_no) {
+    const int rs = 8 * W + 4;
+    out->ranges.clear();
+    out->bytes = 0;
+    if (parts < 1 || part >= parts) {
+        if (err_no) *err_no = EINVAL;
+        return false;
+    }
+    std::vector<RunAccess> acc;
+    if (!open_runs(runs, rs, &acc, err_no)) return false;
+    const int m = (int)acc.size();
+    uint64_t total = 0;
+    for (int i = 0; i < m; i++) total += acc[i].n;
+    // cut[j][i]: run i's first record of part j (cut[0] = 0, cut[parts] = n)
+    std::vector<std::vector<uint64_t>> cut(parts + 1, std::vector<uint64_t>(m, 0));
+    for (int i = 0; i < m; i++) cut[parts][i] = acc[i].n;
+    std::vector<uint8_t> prev_key;
+    uint8_t key[8 * 4 + 4];
+    for (uint32_t j = 1; j < parts; j++) {
+        const long double target = (long double)total * j / parts;
+        bool have = false;
+        long double best_d = 0;
+        std::vector<uint8_t> best_key(rs);
+        std::vector<uint64_t> best_pos(m);
+        for (int c = 0; c < m; c++) {
+            if (acc[c].n == 0) continue;
+            const uint64_t at = std::min<uint64_t>(acc[c].n - 1, (uint64_t)((long double)acc[c].n * j / parts));
+            if (!acc[c].read(at, 1, key)) {
+                if (err_no) *err_no = errno ? errno : EIO;
+                return false;
+            }
+            std::vector<uint64_t> pos(m);
+            uint64_t below = 0;
+            for (int i = 0; i < m; i++) {
+                if (!acc[i].lower_bound(key, W, 0, acc[i].n, &pos[i])) {
+                    if (err_no) *err_no = errno ? errno : EIO;
+                    return false;
+                }
+                below += pos[i];
+            }
+            const long double d = below > target ? below - target : target - below;
+            if (!have || d < best_d || (d == best_d && key_compare(key, best_key.data(), W) < 0)) {
+                have = true;
+                best_d = d;
+                memcpy(best_key.data(), key, rs);
+                best_pos = pos;
+            }
+        }
+        if (!have) continue;  // every run empty: all cuts stay 0
+        if (!prev_key.empty() && key_compare(best_key.data(), prev_key.data(), W) < 0) {
+            best_key = prev_key;  // non-decreasing boundaries
+            best_pos = cut[j - 1];
+        }
+        cut[j] = best_pos;
+        prev_key = best_key;
+    }
+    std::vector<std::vector<uint64_t>> bounds;
+    if (!plan_ranges(acc, W, cut[part], cut[part + 1], &bounds, err_no)) return false;
+    out->ranges.assign(bounds.size() - 1, std::vector<uint8_t>());
+    uint64_t merged = 0;
+    bool ok = merge_ranges(acc, W, bounds, threads, &merged, err_no,
+                           [&](size_t r, const uint8_t* p, uint64_t n, uint64_t) {
+                               out->ranges[r].assign(p, p + n);
+                               return true;
+                           });
+    out->bytes = merged;
+    for (int i = 0; i < m; i++) out->in_records += cut[part + 1][i] - cut[part][i];
+    return ok;
+}
+
+bool write_part_at(const MergedPart& p, const std::string& path, uint64_t offset, uint64_t file_bytes, int* err_no) {
+    int fd = ::open(path.c_str(), O_WRONLY | O_CREAT, 0644);
+    if (fd < 0) {
+        if (err_no) *err_no = errno;
+        return false;
+    }
+    bool ok = true;
+    uint64_t off = offset;
+    for (const auto& r : p.ranges) {
+        if (!pwrite_all(fd, r.data(), r.size(), off)) {
+            ok = false;
+            break;
+        }
+        off += r.size();
+    }
+    // every part cuts the file to the node's total: idempotent, and no part
+    // writes past it, so the order of the parts' truncations does not matter
+    if (ok && file_bytes && ftruncate(fd, (off_t)file_bytes) != 0) ok = false;
+    if (!ok && err_no) *err_no = errno ? errno : EIO;
+    if (::close(fd) != 0 && ok) {
+        if (err_no) *err_no = errno;
+        ok = false;
+    }
     return ok;
 }
 

@@ -79,6 +79,24 @@ bool merge_runs(const std::vector<RunSource>& runs, const std::string& out, int 
 bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& out, int W, uint32_t threads,
                          int* err_no = nullptr);
 
+// One part of a merge shared by `parts` processes over the same run files
+// (cfg3's ranks): part boundaries are keys picked from the runs by a
+// deterministic rule (no exchange between the processes), each part merged by
+// up to `threads` threads into memory. The parts in order concatenate to
+// merge_runs' bytes; part p's offset in the output is the sum of the sizes of
+// parts 0..p-1 (the caller gathers them).
+struct MergedPart {
+    std::vector<std::vector<uint8_t>> ranges;  // merged bytes, range by range in key order
+    uint64_t bytes = 0;                        // sum of the ranges' sizes
+    uint64_t in_records = 0;                   // input records of the part (all runs)
+};
+bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, uint32_t parts, uint32_t threads,
+                     MergedPart* out, int* err_no = nullptr);
+// Writes a part at `offset` of `path` (created if missing, not truncated);
+// file_bytes > 0 cuts the file to that size (the node's total) afterwards.
+bool write_part_at(const MergedPart& p, const std::string& path, uint64_t offset, uint64_t file_bytes,
+                   int* err_no = nullptr);
+
 // Merge tree with the reference handler's knobs (KMerFileMergeHandler.cpp):
 // while more than fan_in runs remain, groups of fan_in runs are merged into
 // temporary files "<tmp_prefix>.m<i>" by up to `threads` threads; the rest is

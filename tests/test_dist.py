@@ -41,8 +41,15 @@ class _GlooRanks:
     def barrier_sync(self):
         self.dist.barrier()
 
+    def all_gather_int(self, v):
+        import torch
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
 
-def _worker(rank, world, port, tmpdir, per, k):
+
+def _worker(rank, world, port, tmpdir, per, k, where):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -62,12 +69,13 @@ def _worker(rank, world, port, tmpdir, per, k):
     run = oracle.count_fastq(fq, k)
     with open(os.path.join(tmpdir, f"run{rank}"), "wb") as f:
         f.write(run)
-    # bench's cfg3 step as stated (--exchange files): run files + rank 0's
-    # host k-way merge, the barriers only ordering the ranks
-    n = bench.host_merge_runs(kca, _FileRun(run, k), _GlooRanks(dist, rank, world), tmpdir,
-                              os.path.join(tmpdir, "node.bin"), k, threads=3)
+    # bench's cfg3 step as stated (--exchange files): run files + the host
+    # k-way merge, shared by the ranks (each merges one key range of every
+    # run file and writes it at its offset) or on rank 0 alone
+    n, mine = bench.host_merge_runs(kca, _FileRun(run, k), _GlooRanks(dist, rank, world), tmpdir,
+                                    os.path.join(tmpdir, "node.bin"), k, threads=2, where=where)
     with open(os.path.join(tmpdir, f"n{rank}"), "w") as f:
-        f.write(str(n))
+        f.write(f"{n} {mine}")
     t = bench.max_over_ranks(dist, float(rank + 1), torch.device("cpu"))
     with open(os.path.join(tmpdir, f"t{rank}"), "w") as f:
         f.write(repr(t))
@@ -75,17 +83,24 @@ def _worker(rank, world, port, tmpdir, per, k):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [31, 55])
-def test_read_shard_merge_equals_whole(kca, orc, tmp_path, k):
-    world, per = 2, 3000
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), per, k), nprocs=world, join=True)
+@pytest.mark.parametrize("world,k,where", [(2, 31, "ranks"), (2, 55, "ranks"), (3, 31, "ranks"), (8, 21, "ranks"),
+                                           (2, 31, "rank0"), (2, 55, "rank0")])
+def test_read_shard_merge_equals_whole(kca, orc, tmp_path, world, k, where):
+    per = 3000 if world < 8 else 600
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), per, k, where), nprocs=world, join=True)
     runs = [str(tmp_path / f"run{r}") for r in range(world)]
     out = tmp_path / "merged.bin"
     kca.merge_files(runs, str(out), k)
     whole = kca.synth_fastq(world * per, 150, 2, genome_length=400_000)
     assert out.read_bytes() == orc.count_fastq(whole, k)
     assert (tmp_path / "node.bin").read_bytes() == out.read_bytes()
-    assert int((tmp_path / "n0").read_text()) * (8 * ((k + 31) // 32) + 4) == out.stat().st_size
+    rs = 8 * ((k + 31) // 32) + 4
+    ns = [tuple(map(int, (tmp_path / f"n{r}").read_text().split())) for r in range(world)]
+    if where == "ranks":
+        assert all(n * rs == out.stat().st_size for n, _ in ns)
+        assert sum(m for _, m in ns) == out.stat().st_size
+    else:
+        assert ns[0] == (out.stat().st_size // rs, out.stat().st_size)
     for r in range(world):
         assert float((tmp_path / f"t{r}").read_text()) == float(world)
 

@@ -770,8 +770,9 @@ def _u64_sortable(lo32, hi32):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("batches", [False, True], ids=["key_passes", "read_batches"])
-def test_config5_full_size_properties(kca, orc, monkeypatch, batches):
+@pytest.mark.parametrize("batches,mem", [(False, 24 << 30), (True, 24 << 30), (False, 48 << 30)],
+                         ids=["key_passes", "read_batches", "bench_48GiB"])
+def test_config5_full_size_properties(kca, orc, monkeypatch, batches, mem):
     """BASELINE config 5 (k=55 two-word keys, 20M x 150 bp iid reads, ~1.92e9
     distinct) on the default engine with a working set below the distinct
     count: the records outgrow it, are cut into sorted runs (the reference's
@@ -781,14 +782,16 @@ def test_config5_full_size_properties(kca, orc, monkeypatch, batches):
     no lower than its multiplicity in the sample; and on the host the window
     checksums of the whole input equal the records'. Default: key-range passes
     (one run, concatenated); read_batches (KC_NO_KEY_PASSES): one sorted run
-    per read batch, merged on the device."""
+    per read batch, merged on the device. bench_48GiB: exactly bench.py
+    --config 5's working set (48 GiB), whose pass plan (two key-range passes,
+    one P2 walk, direct P5s runs) produces the cfg5 bench lines."""
     import torch
     if batches:
         monkeypatch.setenv("KC_NO_KEY_PASSES", "1")
 
     n, L, k = 20_000_000, 150, 55
     dev = torch.device("cuda", 0)
-    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=24 << 30) as ctx:
+    with kca.Context(kmer_length=k, line_length=L, gpu_memory_limit=mem) as ctx:
         ptr, nb = ctx.synth_device(n, L, 5, 0, 0.0, 0)
         checksum = (orc, _host_fastq(ctx, ptr, nb))
         assert ctx.count_fastq_device(ptr, nb) == n
@@ -798,6 +801,9 @@ def test_config5_full_size_properties(kca, orc, monkeypatch, batches):
         assert st["valid_kmers"] == n * (L - k + 1)
         if batches:
             assert st["spill_runs"] >= 2 and st["key_passes"] == 0
+        elif mem == 48 << 30:
+            assert st["key_passes"] == 2 and st["spill_runs"] == 1 and st["spilled_kmers"] == 0
+            assert st["engines_used"] == 2 and st["sorted_run_batches"] >= 1
         else:
             assert st["key_passes"] >= 2 and st["spill_runs"] == 1
         rec = torch.empty(nrec * 20, dtype=torch.uint8, device=dev)

@@ -173,6 +173,64 @@ def test_merge_key_ranges_parallel(kca, orc, tmp_path, monkeypatch, k, nruns, th
         assert orc.ref_merge(paths, str(tmp_path / "ref.bin"), k, len(paths) + 1, 1) == mine
 
 
+@pytest.mark.parametrize("k,nruns,parts,thr,rr", [(31, 8, 2, 3, 400), (31, 8, 8, 2, 100), (31, 12, 3, 4, 300),
+                                                  (31, 20, 5, 2, 200), (21, 2, 7, 1, 1 << 20), (55, 4, 3, 2, 150),
+                                                  (100, 3, 4, 2, 80), (31, 1, 3, 2, 100), (31, 5, 1, 4, 100)])
+def test_merge_parts_concatenate(kca, orc, tmp_path, monkeypatch, k, nruns, parts, thr, rr):
+    """The merge shared by `parts` processes (kc_merge_part_create /
+    kc_merge_part_write, cfg3's ranks): every part computed from the same
+    files on its own (no exchange), written at the prefix sum of the parts'
+    sizes into one file holding an older, larger file's bytes; the result
+    equals merge_files' bytes and the reference merger's. Runs with in-run
+    duplicates, a key repeated for several ranges' worth, an empty run, u32
+    count wrap; 1 to 20 runs (the one-word merge's 4/8/16-lane forms and its
+    fallback) and more parts than some runs have distinct keys."""
+    monkeypatch.setenv("KC_MERGE_RANGE_RECS", str(rr))
+    W = (k + 31) // 32
+    rng = random.Random(k * 13 + nruns * 5 + parts)
+    runs = _random_runs(rng, nruns, 2500, W, dup_frac=0.2, space=4000 if W == 1 else 40)
+    key = runs[0][len(runs[0]) // 3][0]
+    runs[0] = sorted(runs[0] + [(key, 0xFFFFFFF0)] * (3 * min(rr, 400)))
+    if nruns > 2:
+        runs[1] = []
+    paths = []
+    for i, r in enumerate(runs):
+        p = tmp_path / f"run{i}"
+        _run_file(p, r, W)
+        paths.append(str(p))
+    want = _expected(runs, W)
+    one = tmp_path / "one.bin"
+    kca.merge_files(paths, str(one), k, max(2, nruns), 1)
+    assert one.read_bytes() == want
+    out = tmp_path / "parts.bin"
+    out.write_bytes(b"y" * (len(want) + 777_777))
+    ps = [kca.MergePart(paths, k, p, parts, thr) for p in range(parts)]
+    sizes = [p.nbytes for p in ps]
+    assert sum(sizes) == len(want)
+    for i in reversed(range(parts)):  # any order
+        ps[i].write(str(out), sum(sizes[:i]), sum(sizes))
+        ps[i].close()
+    assert out.read_bytes() == want
+    if parts > 1 and nruns > 1 and rr < 1 << 20:
+        assert max(sizes) < 0.75 * len(want)  # the boundaries split the key space
+    if orc.have_ref("ref_merge"):  # (the reference merger dereferences NULL on an empty run)
+        full = [q for q, r in zip(paths, runs) if r]
+        assert orc.ref_merge(full, str(tmp_path / "ref.bin"), k, len(full) + 1, 1) == want
+
+
+def test_merge_part_bad_args(kca, tmp_path):
+    p = tmp_path / "r"
+    p.write_bytes(b"")
+    with pytest.raises(kca.KcError):
+        kca.MergePart([str(p)], 31, 2, 2)
+    with pytest.raises(kca.KcError):
+        kca.MergePart([str(tmp_path / "missing")], 31, 0, 1)
+    with kca.MergePart([str(p)], 31, 0, 1) as mp:
+        assert mp.nbytes == 0
+        with pytest.raises(kca.KcError):
+            mp.write(str(tmp_path / "o"), 5, 4)  # past the file size
+
+
 def test_merge_large_runs_cross_cache_refill(kca, orc, tmp_path):
     """Runs above the reference's 1M-record cache (SortedKMerFile.cpp:29)."""
     rng = np.random.default_rng(3)
