@@ -89,6 +89,7 @@ struct MergedPart {
     std::vector<std::vector<uint8_t>> ranges;  // merged bytes, range by range in key order
     uint64_t bytes = 0;                        // sum of the ranges' sizes
     uint64_t in_records = 0;                   // input records of the part (all runs)
+    uint32_t threads = 1;                      // writers of write_part_at
 };
 bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, uint32_t parts, uint32_t threads,
                      MergedPart* out, int* err_no = nullptr);
