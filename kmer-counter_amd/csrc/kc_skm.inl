@@ -1813,188 +1813,6 @@ __global__ __launch_bounds__(kRpBlock) void rp_scatter_k(const u64* __restrict__
     }
 }
 
-// The same scatter with the store phase of tile t and the ranking of the next
-// tile in one phase (round 6). The ranking needs only the per-wave digit
-// counters and the item registers, the stores only the staged tile and its
-// run starts, so each thread issues its rank atomics for the next tile and then
-// its global stores of the current one with no barrier between them: the
-// ranking's LDS round trips overlap the stores of the CU's other waves, and
-// one barrier per tile goes (four instead of five). Same LDS and tile as rp_scatter_k; the counters are
-// cleared during the LDS scatter, the digit starts and run starts are
-// rewritten after the stores that read them.
-template <int NW, bool PAY>
-__global__ __launch_bounds__(kRpBlock) void rp_scatter_ovl_k(const u64* __restrict__ kin, u64 istride,
-                                                             u64* __restrict__ kout, u64 ostride,
-                                                             const u32* __restrict__ pin, u32* __restrict__ pout,
-                                                             const u64* __restrict__ rstart,
-                                                             const u64* __restrict__ tpre, int nreg, u64 ntiles,
-                                                             const u64* __restrict__ pos, int dshift,
-                                                             unsigned char* __restrict__ emit, int eshift) {
-    constexpr int KPT = RpCfg<NW, PAY>::KPT;
-    constexpr int TILE = RpCfg<NW, PAY>::TILE;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    u64* skey = (u64*)smem;                                    // NW x TILE
-    u32* spay = (u32*)(skey + (size_t)NW * TILE);              // TILE (PAY)
-    u32* wc = spay + (PAY ? TILE : 0);                         // kRpWaves x 128 words: two u16 counters each
-    unsigned short* woff = (unsigned short*)(wc + kRpWaves * 128);  // kRpWaves x 256
-    u32* dst = (u32*)(woff + kRpWaves * 256);                        // 256 digit starts in the tile
-    u64* gpos = (u64*)(dst + 256);                             // 256 global run starts
-    u32* wsum = (u32*)(gpos + 256);                            // 16
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    u64 nk[KPT][NW];
-    u32 np[KPT];
-    u64 npos = 0;  // the loaded tile's 256 run starts (tid < 256), loaded with its items
-    const bool xcd_map = (gridDim.x & 7u) == 0u && ntiles >= 8;
-    const u64 step = xcd_map ? (u64)(gridDim.x >> 3) : (u64)gridDim.x;
-    const u64 tx = (ntiles + 7) >> 3;
-    const u64 t_first = xcd_map ? (u64)(blockIdx.x & 7u) * tx + (blockIdx.x >> 3) : (u64)blockIdx.x;
-    const u64 t_end = xcd_map ? min(ntiles, (u64)((blockIdx.x & 7u) + 1) * tx) : ntiles;
-    if (t_first >= t_end) return;
-    auto load = [&](u64 t) {
-        if (t >= t_end) return;
-        u64 lo = 0, hi = 0;
-        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
-        if (tid < 256) npos = pos[t * 256 + tid];
-#pragma unroll
-        for (int i = 0; i < KPT; i++) {
-            const u64 q = min(lo + (u64)i * kRpBlock + tid, hi - 1);
-            if (istride == 0) {  // AoS items (uniform branch)
-                if constexpr (NW == 2) {
-                    const v2u64 v = __builtin_nontemporal_load((const v2u64*)(kin + 2 * q));
-                    nk[i][0] = v.x;
-                    nk[i][1] = v.y;
-                } else {
-#pragma unroll
-                    for (int j = 0; j < NW; j++) nk[i][j] = __builtin_nontemporal_load(kin + q * NW + j);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < NW; j++) nk[i][j] = __builtin_nontemporal_load(kin + (u64)j * istride + q);
-            }
-            if constexpr (PAY) np[i] = __builtin_nontemporal_load(pin + q);
-        }
-    };
-    u64 key[KPT][NW];
-    u32 pv[KPT];
-    u32 rank2[(KPT + 1) / 2];  // the ranks as u16 pairs (registers are at the 128-VGPR limit)
-    // the next tile's items into key/pv (waits for its loads), its loads
-    // after that issued; returns its length
-    auto take = [&](u64 t) -> u32 {
-        u64 lo, hi;
-        rp_tile_range(rstart, tpre, nreg, t, TILE, &lo, &hi);
-#pragma unroll
-        for (int i = 0; i < KPT; i++) {
-#pragma unroll
-            for (int j = 0; j < NW; j++) key[i][j] = nk[i][j];
-            pv[i] = PAY ? np[i] : 0u;
-        }
-        return (u32)(hi - lo);
-    };
-    // digit starts of the ranked tile (wc) -> woff, dst; gpos <- run starts
-    auto scan = [&](u64 gp) {
-        if (tid < 256) {
-            u32 run = 0;
-            for (int w = 0; w < kRpWaves; w++) {
-                woff[w * 256 + tid] = (unsigned short)run;
-                run += (wc[w * 128 + (tid >> 1)] >> (16 * (tid & 1))) & 0xffffu;
-            }
-            const u32 v = run;
-            u32 inc = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const u32 y = __shfl_up(inc, o);
-                if (lane >= o) inc += y;
-            }
-            if (lane == 63) wsum[wave] = inc;
-            dst[tid] = inc - v;
-            gpos[tid] = gp;
-        }
-        __syncthreads();
-        if (tid < 256) {
-            u32 add = 0;
-            for (int w = 0; w < wave; w++) add += wsum[w];
-            dst[tid] += add;
-        }
-        __syncthreads();
-    };
-    // the ranked tile into skey (its digit order); the counters cleared for
-    // the next ranking
-    auto place = [&](u32 len) {
-#pragma unroll
-        for (int i = 0; i < KPT; i++) {
-            const u32 q = (u32)i * kRpBlock + (u32)tid;
-            if (q < len) {
-                const u32 d = (u32)(key[i][0] >> dshift) & 255u;
-                const u32 at = dst[d] + woff[wave * 256 + d] + ((rank2[i >> 1] >> (16 * (i & 1))) & 0xffffu);
-#pragma unroll
-                for (int j = 0; j < NW; j++) skey[(size_t)j * TILE + at] = key[i][j];
-                if constexpr (PAY) spay[at] = pv[i];
-            }
-        }
-        for (int i = tid; i < kRpWaves * 128; i += kRpBlock) wc[i] = 0;
-        __syncthreads();
-    };
-    // iteration: stores of the placed tile (none in the first) and ranking of
-    // tile nt | scan | LDS scatter of nt; the tile after nt loads meanwhile
-    for (int i = tid; i < kRpWaves * 128; i += kRpBlock) wc[i] = 0;
-    load(t_first);
-    u32 len = 0;
-    for (u64 nt = t_first;; nt += step) {
-        const bool more = nt < t_end;  // uniform
-        u32 nlen = 0;
-        u64 gp = 0;
-        if (more) {
-            nlen = take(nt);
-            gp = npos;
-        }
-        if (nt == t_first) __syncthreads();  // the cleared counters (later: place's barrier)
-#pragma unroll
-        for (int i = 0; i < (KPT + 1) / 2; i++) rank2[i] = 0;
-#pragma unroll
-        for (int i = 0; i < KPT; i++) {
-            const u32 q = (u32)i * kRpBlock + (u32)tid;
-            if (q < nlen) {
-                const u32 d = (u32)(key[i][0] >> dshift) & 255u;
-                const u32 sh = 16 * (d & 1);
-                rank2[i >> 1] |= ((atomicAdd(&wc[wave * 128 + (d >> 1)], 1u << sh) >> sh) & 0xffffu) << (16 * (i & 1));
-            }
-        }
-        // (a runtime loop: the unrolled form spills)
-        for (u32 q = tid; q < len; q += kRpBlock) {
-            const u64 k0 = skey[q];
-            const u32 d = (u32)(k0 >> dshift) & 255u;
-            const u64 g = gpos[d] + (q - dst[d]);
-            if (ostride == 0) {  // AoS output (uniform branch)
-                if constexpr (NW == 2) {
-                    v2u64 v;
-                    v.x = k0;
-                    v.y = skey[(size_t)TILE + q];
-                    *(v2u64*)(kout + 2 * g) = v;
-                } else {
-                    kout[g * NW] = k0;
-#pragma unroll
-                    for (int j = 1; j < NW; j++) kout[g * NW + j] = skey[(size_t)j * TILE + q];
-                }
-            } else {
-                kout[g] = k0;
-#pragma unroll
-                for (int j = 1; j < NW; j++) kout[(u64)j * ostride + g] = skey[(size_t)j * TILE + q];
-            }
-            if constexpr (PAY) pout[g] = spay[q];
-            if (emit) emit[g] = (unsigned char)(k0 >> eshift);
-        }
-        __syncthreads();
-        if (!more) break;
-        // the tile after nt: issued here, not before the stores, so its item
-        // registers are not live across them (the 128-VGPR budget of a
-        // 1024-thread workgroup); the scan and the LDS scatter hide its latency
-        load(nt + step);
-        scan(gp);
-        place(nlen);
-        len = nlen;
-    }
-}
-
 static size_t rp_scatter_lds(int NW, bool pay) {
     const size_t tile = (size_t)rp_tile(NW, pay);
     return (size_t)NW * tile * 8 + (pay ? tile * 4 : 0) + kRpWaves * 128 * 4 + kRpWaves * 256 * 2 + 256 * 4 +
@@ -2080,23 +1898,9 @@ hipError_t launch_rp_scatter(int NW, bool pay, const uint64_t* kin, uint64_t ist
     // prefetch pipeline
     const int g = (int)hmin(ntiles, (u64)(grid / 2 > 0 ? KC_RP_WPC * grid / 2 : 1));
     const size_t lds = (rp_scatter_lds(NW, pay) + 15) & ~(size_t)15;
-    // the overlapped form by default for records without a payload (S, P3,
-    // P3b); the (key, count) passes of the finish keep the phase-serial form,
-    // whose registers fit (the overlapped one spills with a payload, and
-    // with one-word keys);
-    // KC_RP_SERIAL (test hook) selects the phase-serial form everywhere
-    static const bool serial = KC_RP_ABL != 0 || test_hook("KC_RP_SERIAL") != nullptr;
 #define KC_RPS(NWV, PAYV)                                                                                          \
-    do {                                                                                                           \
-        if (serial || PAYV || NWV == 1)                                                                            \
-            hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kRpBlock), lds, s, kin, istride, kout,      \
-                               ostride, pin, pout, rstart, tpre, nreg, ntiles, pos, dshift, (unsigned char*)emit,    \
-                               eshift);                                                                            \
-        else                                                                                                       \
-            hipLaunchKernelGGL((rp_scatter_ovl_k<NWV, PAYV>), dim3(g), dim3(kRpBlock), lds, s, kin, istride, kout,  \
-                               ostride, pin, pout, rstart, tpre, nreg, ntiles, pos, dshift, (unsigned char*)emit,    \
-                               eshift);                                                                            \
-    } while (0)
+    hipLaunchKernelGGL((rp_scatter_k<NWV, PAYV>), dim3(g), dim3(kRpBlock), lds, s, kin, istride, kout, ostride, pin, \
+                       pout, rstart, tpre, nreg, ntiles, pos, dshift, (unsigned char*)emit, eshift)
     if (pay) {
         switch (NW) {
         case 1: KC_RPS(1, true); break;
