@@ -411,7 +411,7 @@ def main(args, D, state):
     xch_ms[0] = 0.0
     files_tm.clear()
     acc = {"insert_ms": 0.0, "finish_ms": 0.0, "decode_ms": 0.0, "dedup_ms": 0.0, "presplit_ms": 0.0, "launches": 0,
-           "part_ms": [0.0] * 5}
+           "part_ms": [0.0] * 5, "finish_group_ms": 0.0, "records": 0}
     t0 = time.perf_counter()
     n_rec = 0
     for _ in range(args.steps):
@@ -423,6 +423,8 @@ def main(args, D, state):
         acc["decode_ms"] += st["decode_ms"]
         acc["dedup_ms"] += st.get("dedup_ms", 0.0)
         acc["presplit_ms"] += st.get("presplit_ms", 0.0)
+        acc["finish_group_ms"] += st.get("finish_group_ms", 0.0)
+        acc["records"] += st["output_records"]
         acc["part_ms"] = [a + b for a, b in zip(acc["part_ms"], st["part_ms"])]
     D.barrier_sync()
     dev_el = D.max(time.perf_counter() - t0)
@@ -436,6 +438,7 @@ def main(args, D, state):
         "value": dev_value, "ms_per_step": dev_el / args.steps * 1e3,
         "breakdown_ms_per_step": {"fastq_index": acc["decode_ms"] / args.steps,
                                   "finish": acc["finish_ms"] / args.steps,
+                                  "finish_grouping (in finish)": round(acc["finish_group_ms"] / args.steps, 3),
                                   "exchange_rank0": xch_ms[0] / args.steps,
                                   "exchange": exchange,
                                   **({"files_merge": args.files_merge, "merge_threads_per_rank": merge_threads(D),
@@ -770,6 +773,14 @@ def device_roofline(args, st, acc, windows_step, nbytes, dev_el, varlen, k, L, W
         else:
             specs.append(("P5", f"count_skm_k<{W}>", part_ms[4], steps * st["batches"], rec_step, "records",
                           rb + (8 * W + 4) * recs_step / rec_step))
+        if acc["finish_ms"] > 0 and acc["records"] > 0:
+            # kc_finish: two grouping passes over the (key, count) records (read
+            # and write 8W + 4 B each, plus the digit byte written by one pass and
+            # read by the next's histogram) and the LDS segment sort writing the
+            # SortedKMerFile records (8W + 4 in, 8W + 4 out)
+            specs.append(("finish", f"rp_scatter_k<{W},true> x2 + seg_sort_k<{W}> (+ histograms, bounds)",
+                          acc["finish_ms"], steps, acc["records"] / steps, "distinct records",
+                          6 * (8 * W + 4) + 3))
     elif used & 2:
         keys_step = st["keys"] or windows_step
         p5_per_step = max(1, st["p5_launches"])

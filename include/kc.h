@@ -56,10 +56,11 @@
 extern "C" {
 #endif
 
-#define KC_ABI_VERSION 6 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
+#define KC_ABI_VERSION 7 /* 2: kc_stats.dedup_ms / dedup_records; 3: kc_synth_spec.min_read_length;
                             4: kc_count_file, kc_checkpoint / kc_rollback / kc_commit;
                             5: kc_stats.presplit_ms / presplit_batches / sorted_run_batches;
-                            6: kc_stats.key_passes */
+                            6: kc_stats.key_passes;
+                            7: kc_stats.finish_group_ms, kc_merge_part_* */
 #define KC_MAX_K 128 /* keys up to 4 words, the widest KMerSizes.h type (KMer128) */
 
 typedef enum kc_status {
@@ -141,7 +142,7 @@ typedef struct kc_stats {
     uint64_t insert_launches;  /* count_kmers kernel launches since the last reset */
     double insert_ms;          /* summed device time of those launches (HIP events) */
     double decode_ms;          /* FASTQ index + validate kernels */
-    double finish_ms;          /* compact + sort + pack */
+    double finish_ms;          /* kc_finish's device time: compact + group/sort + pack */
     double last_count_ms;      /* device time of the last kc_count_* call */
     double part_ms[5];         /* partition engine (summed device time): [0] encode
                                   (E) + P1 digit histogram, [1] P2 scatter,
@@ -169,6 +170,9 @@ typedef struct kc_stats {
     uint64_t key_passes;       /* key-prefix engine, high cardinality: key-range passes
                                   (a batch too big for the working set counted by
                                   disjoint key ranges whose runs concatenate) */
+    double finish_group_ms;    /* part of finish_ms: the super-k-mer finish's two
+                                  grouping passes (histograms + radix scatters of the
+                                  (key, count) records by their first 8 bases) */
 } kc_stats;
 
 /* Synthetic FASTQ. Records are "@r<i>\n<seq>\n+\n<'I' x L>\n". (ABI 4: layout) */

@@ -88,6 +88,7 @@ class Stats(ctypes.Structure):
         ("presplit_batches", ctypes.c_uint64),
         ("sorted_run_batches", ctypes.c_uint64),
         ("key_passes", ctypes.c_uint64),
+        ("finish_group_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -53,6 +53,8 @@ struct kc_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev2 = nullptr;  // a third mark: two phases timed by one synchronisation
+    hipEvent_t evf[2] = {nullptr, nullptr};  // kc_finish's own marks (the passes inside it use ev0..ev2)
+    double finish_group_ms = 0;              // the finish's grouping passes (histograms + scatters)
     uint64_t id = 0;
 
     // table + spill (the gpu_memory_limit working set)
@@ -2060,7 +2062,8 @@ kc_status kc_create(kc_ctx** out, const kc_config* cfg) {
     if (hipSetDevice(cfg->device) != hipSuccess) return bail(KC_ERR_NODEVICE);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(KC_ERR_HIP);
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev2) != hipSuccess)
+        hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->evf[0]) != hipSuccess ||
+        hipEventCreate(&c->evf[1]) != hipSuccess)
         return bail(KC_ERR_HIP);
     uint64_t M = cfg->gpu_memory_limit ? cfg->gpu_memory_limit : 100000000ull;
     if (M < (1u << 20)) M = 1u << 20;
@@ -2174,6 +2177,8 @@ void kc_destroy(kc_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
+    for (hipEvent_t e : c->evf)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2202,6 +2207,7 @@ kc_status kc_reset(kc_ctx* c) {
     c->sorted_run_batches = 0;
     c->key_passes = 0;
     c->dedup_ms = 0;
+    c->finish_group_ms = 0;
     c->dedup_records = 0;
     c->part_keys = 0;
     c->p5_launches = 0;
@@ -2811,6 +2817,7 @@ static kc_status finish_skm(kc_ctx* c, uint64_t* n_out) {
         if ((s = group16(c, W, true, c->rec_keys, c->rec_cap, c->rec_cnts, (uint64_t*)c->fin_keys[1].p, out_cap,
                          (uint32_t*)c->fin_cnts[1].p, c->digs, n, gm, dig1 ? c->rec_dig : nullptr)))
             return s;
+        c->finish_group_ms += gm[0] + gm[1];
         if ((s = ensure(c, c->part_starts, ((size_t)nb + 1) * 8)) || (s = ensure(c, c->desc_v, (size_t)nb * 4)) ||
             (s = ensure(c, c->desc_len, (size_t)nb * 4)) || (s = ensure(c, c->desc_fb, (size_t)nb * 4 + 16)))
             return s;
@@ -2996,13 +3003,14 @@ kc_status kc_finish(kc_ctx* c, uint64_t* n_records) {
     if ((s = sync_stats(c))) return s;
     if (c->stats_h[ST_SPILL_FILL] > 0 && (s = flush_spill(c))) return s;
     // the table run: the engines' records (or the global table) sorted into fin_packed
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    // (own events: the grouping passes inside record ev0..ev2 themselves)
+    HIPCHK(c, hipEventRecord(c->evf[0], c->stream));
     uint64_t n = 0;
     if ((s = c->part ? finish_part(c, &n) : finish_table(c, &n))) return s;
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(c->evf[1], c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float tf = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&tf, c->ev0, c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&tf, c->evf[0], c->evf[1]));
     c->st.finish_ms += tf;
     c->st.table_used = c->stats_h[ST_CLAIMED];
     if (c->dev_runs.size() == 1 && n == 0) {
@@ -3236,6 +3244,7 @@ kc_status kc_get_stats(const kc_ctx* c, kc_stats* out) {
     out->engines_used = c->engines_used;
     out->dedup_ms = c->dedup_ms;
     out->dedup_records = c->stats_h[ST_DEDUP];
+    out->finish_group_ms = c->finish_group_ms;
     return KC_OK;
 }
 

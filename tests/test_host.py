@@ -18,7 +18,7 @@ def test_library_exports_header_symbols(kca):
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.kc_abi_version() == 6
+    assert L.kc_abi_version() == 7
     assert L.kc_strerror(4) == b"malformed FASTQ block"
 
 
