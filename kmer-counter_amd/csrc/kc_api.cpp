@@ -1418,21 +1418,12 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                 // P5a and P5 back to back, timed by three marks after P5's
                 // synchronisation (P5a's time: ev0 -> ev1, P5's: ev1 -> ev2)
                 bool p5a_pending = false;
-                // P5a counts the buckets whose distinct records fit as well
-                // (fused; not when the tests shrink P5's LDS table to reach its
-                // overflow paths): its (key, count) records go where P5's go,
-                // so the record buffer is sized first
-                const bool fuse = dedup && c->cfg.lds_slots == 0;
-                dd.fused_raw = 0;
-                if (fuse && (s2 = grow_records(c, rec0 + bound))) return s2;
                 if (dedup) {
-                    SkmFuse fz = {(int)c->k, count_keys, c->rec_keys, c->rec_cnts, c->rec_dig, c->rec_cap,
-                                  c->rec_cursor, c->stats};
                     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
                     HIPCHK(c, launch_count_rec(c->keys_a, pool_cap, (const uint64_t*)c->part_starts.p, b0, b1,
                                                (uint32_t*)c->digs, (uint32_t*)c->part_dedup.p, c->n_cu, c->stream,
                                                over0 < over_limit ? c->pool_cursor : nullptr, over_limit,
-                                               (uint64_t*)dd.pos, fuse ? &fz : nullptr));
+                                               (uint64_t*)dd.pos));
                     p5a_pending = true;
                 }
                 for (;;) {
@@ -1475,9 +1466,6 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
                     HIPCHK(c, hipStreamSynchronize(c->stream));
                     c->stats_h[ST_ERR] = err;
                     c->rec_n = rec0;
-                    // the fused P5a's records are dropped with the rest: P5
-                    // counts its buckets again from their own (intact) records
-                    dd.fused_raw = 1;
                 }
             };
             // bucket 0xffff holds only the pool's padding records. Unless this

@@ -361,23 +361,9 @@ int seg_sort_cap(int W);  // longest segment seg_sort_k takes
 // again in hash-split passes into a list reserved from *over_cursor (records
 // of recs / cnt below over_limit, free), dpos[b] its start, dlen[b] =
 // 0x80000000 | its length; no room or no over_cursor: left raw.
-// fuse (optional): a bucket whose distinct records all fit the claim list is
-// counted right there (P5's work, P5's output buffers), dlen[b] = 0x40000000 |
-// its distinct records; P5 skips it (SkmFuse::fused_raw = 0) or counts it from
-// its records again (1: a rerun after a record overflow)
-struct SkmFuse {
-    int k;
-    bool count_keys;
-    uint64_t* rec_keys;
-    uint32_t* rec_cnts;
-    uint8_t* rec_dig;
-    uint64_t rec_cap;
-    uint64_t* rec_cursor;
-    uint64_t* stats;
-};
 hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
                             uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s, uint64_t* over_cursor = nullptr,
-                            uint64_t over_limit = 0, uint64_t* dpos = nullptr, const SkmFuse* fuse = nullptr);
+                            uint64_t over_limit = 0, uint64_t* dpos = nullptr);
 // stats[ST_DEDUP] += sum over buckets [0, nb) of dlen[b] (raw: the bucket's records)
 hipError_t launch_dedup_total(const uint32_t* dlen, const uint64_t* starts, uint32_t nb, uint64_t* stats,
                               hipStream_t s);
@@ -385,7 +371,6 @@ struct SkmDedup {
     const uint32_t* cnt;  // P5a output
     const uint32_t* len;
     const uint64_t* pos;  // overflow lists' starts (len flag 0x80000000)
-    int fused_raw;        // buckets the fused P5a counted (len flag 0x40000000): 0 skip, 1 count from their records
 };
 // buckets [b0, b1); count_keys: add the buckets' key counts to stats[ST_P5_KEYS];
 // dd (optional): P5a's lists, walked instead of the buckets' records

@@ -1960,12 +1960,10 @@ struct SkmBucketArgs {
     const u32* dcnt;
     const u32* dlen;
     const u64* dpos;  // kOverList buckets: their list's start
-    int fused_raw;    // kFusedList buckets: 0 = skipped (the fused P5a counted them), 1 = counted raw
 };
 
 constexpr u32 kRawList = 0xffffffffu;  // P5a: bucket not deduplicated
 constexpr u32 kOverList = 0x80000000u;  // P5a: dlen flag, the list is at dpos[b] (overflow list), not at the bucket's start
-constexpr u32 kFusedList = 0x40000000u;  // P5a: dlen flag, the bucket was counted by the fused P5a (P5 skips it)
 
 // key i of a record (see the record layout above)
 template <int W>
@@ -2177,8 +2175,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
     u32 pfb = ~0u;
     // bucket bb's record source: deduplicated list or its own records
     auto source = [&](u32 bb, const u64** rp, u64* st, const u32** cp, u64* l0, u64* h0) {
-        u32 dl = dlen_r ? dlen_r[bb] : kRawList;
-        if (dl != kRawList && (dl & kFusedList)) dl = kRawList;  // (fused_raw: counted again from its records)
+        const u32 dl = dlen_r ? dlen_r[bb] : kRawList;
         if (dl != kRawList) {
             *rp = a.recs;
             *st = a.stride;
@@ -2218,18 +2215,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
     // records past rec_cap are never written and the host reruns) is read
     // every 64 buckets, and the output range is reserved before the prefetch.
     u32 nb_done = 0;
-    // buckets the fused P5a counted are skipped (unless fused_raw: a rerun
-    // after a record overflow counts every bucket)
-    auto skip = [&](u32 bb) {
-        if (a.fused_raw || !dlen_r) return false;
-        const u32 dl = dlen_r[bb];
-        return dl != kRawList && (dl & kFusedList) != 0u;
-    };
-    auto next_b = [&](u32 bb) {
-        while (bb < a.nbuckets && skip(bb)) bb += gridDim.x;
-        return bb;
-    };
-    for (u32 b = next_b(a.b0 + blockIdx.x); b < a.nbuckets; b = next_b(b + gridDim.x), nb_done++) {
+    for (u32 b = a.b0 + blockIdx.x; b < a.nbuckets; b += gridDim.x, nb_done++) {
         if ((nb_done & 63u) == 0u) {
             if (tid == 0)
                 *lnext = (u32)(__hip_atomic_load((unsigned long long*)&a.stats[ST_ERR], __ATOMIC_RELAXED,
@@ -2483,8 +2469,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
             }
             // the next bucket's first batches go in flight during the emission
             // (unless another pass of this bucket follows)
-            const u32 bnext = next_b(b + gridDim.x);
-            const bool pf_next = sub + 1 >= m && bnext < a.nbuckets;
+            const bool pf_next = sub + 1 >= m && b + gridDim.x < a.nbuckets;
             if (qn && (last || !__hip_atomic_load(labort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
                 skm_drain<W>(a, tab, wq, wqw, qn, brecs, bstride, lo, last, limit);
             __syncthreads();
@@ -2533,7 +2518,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                 // the pass's records = its claimed slots: the output range is
                 // reserved now, its latency hidden by the waves' slot counts
                 if (a.skip & 16) {  // timing experiments: no emission
-                    if (pf_next) prefetch_pass(bnext);
+                    if (pf_next) prefetch_pass(b + gridDim.x);
                     __syncthreads();
                     ++sub;
                     continue;
@@ -2547,7 +2532,7 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
                         nclaimed ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)nclaimed) : 0ull;
                     misc[24] = 0u;
                 }
-                if (pf_next) prefetch_pass(bnext);
+                if (pf_next) prefetch_pass(b + gridDim.x);
                 __syncthreads();
                 const u64 rbase = *(const u64*)(misc + 16);
                 for (u32 c0 = s0; c0 < s1; c0 += 64) {
@@ -2598,7 +2583,6 @@ hipError_t launch_count_skm(int W, int k, const uint64_t* recs, uint64_t stride,
     a.dcnt = dd ? dd->cnt : nullptr;
     a.dlen = dd ? dd->len : nullptr;
     a.dpos = dd ? dd->pos : nullptr;
-    a.fused_raw = dd ? dd->fused_raw : 0;
     a.skip = experiment_knob("KC_P5_SKIP");
     const bool mask_last = ((k + 3) / 4) < 8 * W;
     a.last_mask = mask_last ? (~0ull << (64 - 2 * (k & 31))) : ~0ull;
@@ -2679,24 +2663,6 @@ struct RecDedupArgs {
     u64* over_cursor;
     u64 over_limit;
     u64* dpos;
-    // fused counting (round 6, `fuse`): a bucket whose distinct records the
-    // claim list holds is counted here as well, P5's job: the distinct records
-    // are compacted to the front of the LDS, the rest of the record table
-    // becomes a key table, their keys are walked from LDS with their
-    // multiplicities and the (key, count) records emitted; dlen[b] =
-    // kFusedList | distinct and P5 skips the bucket. A key table that fills
-    // writes the distinct records back as P5a does (dlen[b] = their number)
-    // and P5 counts them.
-    int fuse;
-    int count_keys;  // add the buckets' keys (weighted) to stats[ST_P5_KEYS]
-    u32 fslots;      // key table slots cap (0: all that fit; tests force the fallback)
-    u64 last_mask;
-    u64* rec_keys;
-    u32* rec_cnts;
-    unsigned char* rec_dig;
-    u64 rec_cap;
-    u64* rec_cursor;
-    u64* stats;
 };
 
 __device__ __forceinline__ u32 rec_hash(u64 k0, u64 k1) {
@@ -2706,7 +2672,6 @@ __device__ __forceinline__ u32 rec_hash(u64 k0, u64 k1) {
 }
 
 constexpr u32 kRecClaims = 4096;  // P5a: claimed entries listed for the write-back (u16 each)
-constexpr int kFuseProbe = 8;     // fused counting: key-table groups probed per key
 
 static size_t rec_dedup_lds(u32 ngrp) { return (size_t)ngrp * 40 + 64 * 4 + 16 + kRecClaims * 2; }
 
@@ -2858,241 +2823,6 @@ __global__ __launch_bounds__(kRecBlock) void count_rec_k(RecDedupArgs a, const u
         __syncthreads();
         return total;
     };
-    // Fused counting of bucket b (every record in the table, none lost):
-    // returns false, having changed nothing, when it does not apply (more
-    // distinct records than the claim list holds, or too little room left for
-    // a key table); else the bucket is done either way (counted, or its
-    // distinct records written back for P5) and the LDS is clear again.
-    auto fuse_bucket = [&](u32 b, u64 pos0, u32 claims) -> bool {
-        for (int o2 = 32; o2 >= 1; o2 >>= 1) claims += (u32)__shfl_xor((int)claims, o2);
-        if (lane == 0) misc[1 + wave] = claims;
-        __syncthreads();
-        u32 total = 0;
-        for (int w = 0; w < kRecWaves; w++) total += misc[1 + w];
-        // compact records: ck0 / ck1 (u64) and cw (u32) arrays of Dp entries,
-        // at least one spare past the last (read, never used, by a walk's
-        // next-record load); the key table after them
-        const u32 Dp = (total + 64u) & ~63u;
-        const u32 kt_off = (u32)(((size_t)Dp * 20 + 15) & ~(size_t)15);
-        const u32 region = a.ngrp * 40u;  // tab + cnt bytes
-        u32 ks = region > kt_off ? ((region - kt_off) / 12u) & ~63u : 0u;
-        if (a.fslots && ks > a.fslots) ks = a.fslots & ~63u;
-        if (total == 0 || total > kRecClaims || ks < 512u) {
-            __syncthreads();  // (misc[1..16] read by every thread before write_back rewrites them)
-            return false;
-        }
-        constexpr int PT = (int)(kRecClaims / kRecBlock);  // records per thread moved through registers
-        u64 r0[PT], r1[PT];
-        u32 rw[PT];
-#pragma unroll
-        for (int j = 0; j < PT; j++) {
-            const u32 i = (u32)tid + (u32)j * kRecBlock;
-            r0[j] = r1[j] = 0;
-            rw[j] = 0;
-            if (i < total) {
-                const u32 e = clist[i];
-                r0[j] = (tab[2 * (size_t)e] & kLow48) | ((u64)b << 48);
-                r1[j] = tab[2 * (size_t)e + 1];
-                rw[j] = cnt[e];
-            }
-        }
-        __syncthreads();  // (the whole table read before the compact records overwrite it)
-        u64* ck0 = (u64*)smem;
-        u64* ck1 = ck0 + Dp;
-        u32* cw = (u32*)(ck1 + Dp);
-        u64* lk = (u64*)((unsigned char*)smem + kt_off);
-        u32* lc = (u32*)(lk + ks);
-        u64 kn = 0;
-#pragma unroll
-        for (int j = 0; j < PT; j++) {
-            const u32 i = (u32)tid + (u32)j * kRecBlock;
-            if (i < total) {
-                ck0[i] = r0[j];
-                ck1[i] = r1[j];
-                cw[i] = rw[j];
-                kn += (r1[j] & 63u) * (u64)rw[j];
-            }
-        }
-        for (u32 i = tid; i < ks; i += kRecBlock) {
-            lk[i] = 0ull;
-            lc[i] = 0u;
-        }
-        if (a.count_keys) wave_add(&a.stats[ST_P5_KEYS], kn);
-        if (tid == 0) {
-            misc[0] = 0;   // abort: a key found no slot / the fill limit passed
-            misc[17] = 0;  // slots claimed
-            misc[18] = 0;  // emission cursor
-        }
-        __syncthreads();
-        const u32 ngk = ks / kSkmGroup;
-        const u32 flimit = (ks * 13u) >> 4;
-        // each wave an equal contiguous share of the distinct records, 64 at
-        // a time; the batch's keys as one flat sequence, lane l taking keys
-        // [l per, l per + per) (as P5)
-        const u32 per_w = (total + kRecWaves - 1) / kRecWaves;
-        const u32 wlo = min(total, (u32)wave * per_w), whi = min(total, (u32)(wave + 1) * per_w);
-        u32 fclaim = 0;
-        for (u32 base = wlo; base < whi; base += 64) {
-            if (__hip_atomic_load(&misc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            const u32 r = base + (u32)lane;
-            const u32 n = r < whi ? (u32)(ck1[r] & 63u) : 0u;
-            u32 inc = n;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const u32 y = __shfl_up(inc, o);
-                if (lane >= o) inc += y;
-            }
-            const u32 excl = inc - n;
-            const u32 T = (u32)__builtin_amdgcn_readlane((int)inc, 63);
-            if (T == 0) continue;
-            const u32 per = (T + 63) >> 6;
-            const u32 s0 = min(T, (u32)lane * per), s1 = min(T, s0 + per);
-            int o = 0;
-#pragma unroll
-            for (int st = 32; st >= 1; st >>= 1) {
-                const u32 e = (u32)__shfl((int)excl, o + st);
-                if (e <= s0) o += st;
-            }
-            u32 ki = s0 - (u32)__shfl((int)excl, o);
-            u32 ri = base + (u32)o;
-            u64 cur[2] = {ck0[ri], ck1[ri]};
-            u32 wcur = cw[ri];
-            u32 nn = (u32)(cur[1] & 63u);
-            u64 win[2];
-            skm_window<2>(cur, 16u + 2u * ki, win);
-            u64 nxt[2] = {ck0[ri + 1], ck1[ri + 1]};  // (ri + 1 <= total: the spare at most)
-            u32 wnxt = cw[ri + 1];
-            for (u32 t = 0; t < per; t++) {
-                const bool act = s0 + t < s1;
-                const u64 key = win[0] & a.last_mask;
-                // probe: home group, then the following ones (a group seen
-                // full stays full: slots are never emptied during the walk)
-                bool pend = act;
-                u32 g = __umulhi(skm_hash32<1>(*(const u64(*)[1])&key), ngk);
-                for (int pr = 0; pr < kFuseProbe && __ballot(pend); pr++) {
-                    if (pend) {
-                        const u32 sw = gswz(g);
-                        const v2u64 h0 = *(const lds_v2u64*)(lk + kSkmGroup * g + sw);
-                        const v2u64 h1 = *(const lds_v2u64*)(lk + kSkmGroup * g + (2u ^ sw));
-                        const bool e0 = h0.x == key, e1 = h0.y == key, e2 = h1.x == key, e3 = h1.y == key;
-                        if (e0 || e1 || e2 || e3) {
-                            const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : 3u));
-                            atomicAdd(&lc[kSkmGroup * g + (hit ^ sw)], wcur);
-                            pend = false;
-                        } else {
-                            const bool z0 = h0.x == 0ull, z1 = h0.y == 0ull, z2 = h1.x == 0ull, z3 = h1.y == 0ull;
-                            if (z0 || z1 || z2 || z3) {
-                                // the first empty slot (slots fill in order); a
-                                // lost race reads the group again
-                                const u32 sl = kSkmGroup * g + ((z0 ? 0u : (z1 ? 1u : (z2 ? 2u : 3u))) ^ sw);
-                                const u64 old =
-                                    atomicCAS((unsigned long long*)&lk[sl], 0ull, (unsigned long long)key);
-                                if (old == 0ull || old == key) {
-                                    atomicAdd(&lc[sl], wcur);
-                                    fclaim += old == 0ull ? 1u : 0u;
-                                    pend = false;
-                                }
-                            } else {
-                                g = g + 1 == ngk ? 0u : g + 1;
-                            }
-                        }
-                    }
-                }
-                if (__ballot(pend) && lane == 0) atomicOr(&misc[0], 1u);
-                // next key: one base rolled in; past the record's last key the
-                // next record (waiting in registers)
-                win[0] = (win[0] << 2) | (win[1] >> 62);
-                win[1] <<= 2;
-                ++ki;
-                if (ki == nn && s0 + t + 1 < s1) {
-                    ++ri;
-                    cur[0] = nxt[0];
-                    cur[1] = nxt[1];
-                    wcur = wnxt;
-                    nn = (u32)(cur[1] & 63u);
-                    skm_window<2>(cur, 16u, win);
-                    nxt[0] = ck0[ri + 1];
-                    nxt[1] = ck1[ri + 1];
-                    wnxt = cw[ri + 1];
-                    ki = 0;
-                }
-            }
-        }
-        {
-            u32 fc = fclaim;
-            for (int o2 = 32; o2 >= 1; o2 >>= 1) fc += (u32)__shfl_xor((int)fc, o2);
-            if (fc && lane == 0) {
-                const u32 f = atomicAdd(&misc[17], fc) + fc;
-                if (f > flimit) atomicOr(&misc[0], 1u);
-            }
-        }
-        __syncthreads();
-        const bool abort = misc[0] != 0u;
-        if (abort) {
-            // P5 counts the bucket: its distinct records go back to the front
-            // of its range, as P5a writes them (the compact records are
-            // intact: the key table lies after them)
-            for (u32 i = tid; i < total; i += kRecBlock) {
-                a.recs[pos0 + i] = ck0[i];
-                a.recs[a.stride + pos0 + i] = ck1[i];
-                a.cnt[pos0 + i] = cw[i];
-            }
-            if (tid == 0) a.dlen[b] = total;
-        } else {
-            // emission: the claimed slots' (key, count) records at a range of
-            // the record buffer reserved by one global atomic
-            const u32 nclaimed = misc[17];
-            if (tid == 0)
-                *(u64*)(misc + 20) =
-                    nclaimed ? atomicAdd((unsigned long long*)a.rec_cursor, (unsigned long long)nclaimed) : 0ull;
-            __syncthreads();
-            const u64 rbase = *(const u64*)(misc + 20);
-            const u32 spw = (ks + kRecWaves - 1) / kRecWaves;
-            const u32 c0s = min(ks, (u32)wave * spw), c1s = min(ks, c0s + spw);
-            for (u32 c0 = c0s; c0 < c1s; c0 += 64) {
-                const u32 i = c0 + (u32)lane;
-                const u64 kk = i < c1s ? lk[i] : 0ull;
-                const bool occ = kk != 0ull;
-                const u64 bm = __ballot(occ);
-                if (bm == 0ull) continue;
-                u32 at = 0;
-                if (lane == 0) at = atomicAdd(&misc[18], (u32)__popcll(bm));
-                at = (u32)__builtin_amdgcn_readfirstlane((int)at);
-                if (occ) {
-                    const u64 q = rbase + at + (u64)__popcll(bm & lt);
-                    if (q < a.rec_cap) {
-                        a.rec_keys[q] = kk;
-                        a.rec_cnts[q] = lc[i];
-                        if (a.rec_dig) a.rec_dig[q] = (unsigned char)(kk >> 48);
-                    }
-                }
-            }
-            __syncthreads();
-            if (tid == 0) {
-                const u32 emitted = misc[18];
-                if (rbase + emitted > a.rec_cap || emitted != nclaimed)
-                    atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_REC_OVERFLOW);
-                atomicAdd((unsigned long long*)&a.stats[ST_P5_PASSES], 1ull);
-                a.dlen[b] = kFusedList | total;
-            }
-        }
-        __syncthreads();
-        // the record table clear again for the next bucket (compact records
-        // and key table lie over all of it)
-        for (u32 i = tid; i < region / 16u; i += kRecBlock) {
-            v2u64 z;
-            z.x = 0ull;
-            z.y = 0ull;
-            *(v2u64*)((unsigned char*)smem + (size_t)i * 16) = z;
-        }
-        if (tid == 0) {
-            misc[0] = 0;
-            misc[17] = 0;
-            misc[18] = 0;
-        }
-        __syncthreads();
-        return true;
-    };
     // buckets with more records than the table has entries: how many this
     // workgroup has seen and how many of them held too many distinct records
     // (uniform values); when most overflowed, such a bucket goes straight to
@@ -3134,10 +2864,8 @@ __global__ __launch_bounds__(kRecBlock) void count_rec_k(RecDedupArgs a, const u
         const bool raw = skip_first || misc[0] != 0u;
         const u64 pos0 = starts_r[b];
         if (!raw) {
-            if (!(a.fuse && fuse_bucket(b, pos0, claims))) {
-                const u32 total = write_back(b, pos0, claims, true);
-                if (tid == 0) a.dlen[b] = total;
-            }
+            const u32 total = write_back(b, pos0, claims, true);
+            if (tid == 0) a.dlen[b] = total;
             big_seen += big ? 1u : 0u;
             continue;
         }
@@ -3206,7 +2934,7 @@ __global__ __launch_bounds__(kBlock) void dedup_total_k(const u32* __restrict__ 
                                                        u32 nb, u64* stats) {
     u64 v = 0;
     for (u32 b = blockIdx.x * kBlock + threadIdx.x; b < nb; b += gridDim.x * kBlock)
-        v += dlen[b] == kRawList ? starts[b + 1] - starts[b] : (u64)(dlen[b] & ~(kOverList | kFusedList));
+        v += dlen[b] == kRawList ? starts[b + 1] - starts[b] : (u64)(dlen[b] & ~kOverList);
     wave_add(&stats[ST_DEDUP], v);
 }
 
@@ -3218,21 +2946,9 @@ hipError_t launch_dedup_total(const uint32_t* dlen, const uint64_t* starts, uint
 
 hipError_t launch_count_rec(uint64_t* recs, uint64_t stride, const uint64_t* starts, uint32_t b0, uint32_t b1,
                             uint32_t* cnt, uint32_t* dlen, int grid, hipStream_t s, uint64_t* over_cursor,
-                            uint64_t over_limit, uint64_t* dpos, const SkmFuse* fuse) {
+                            uint64_t over_limit, uint64_t* dpos) {
     if (b1 <= b0) return hipSuccess;
     RecDedupArgs a;
-    a.fuse = fuse && !test_hook("KC_NO_FUSED") ? 1 : 0;
-    a.count_keys = fuse && fuse->count_keys ? 1 : 0;
-    a.fslots = 0;
-    if (const char* e = test_hook("KC_FUSED_SLOTS")) a.fslots = (u32)atol(e);  // tests: small key tables (fallback)
-    a.last_mask = ~0ull;
-    if (fuse && ((fuse->k + 3) / 4) < 8) a.last_mask = ~0ull << (64 - 2 * (fuse->k & 31));
-    a.rec_keys = fuse ? fuse->rec_keys : nullptr;
-    a.rec_cnts = fuse ? fuse->rec_cnts : nullptr;
-    a.rec_dig = fuse ? fuse->rec_dig : nullptr;
-    a.rec_cap = fuse ? fuse->rec_cap : 0;
-    a.rec_cursor = fuse ? fuse->rec_cursor : nullptr;
-    a.stats = fuse ? fuse->stats : nullptr;
     a.over_cursor = test_hook("KC_P5A_NO_SPLIT") ? nullptr : over_cursor;
     a.over_limit = over_limit;
     a.dpos = dpos;

@@ -338,33 +338,6 @@ def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
     assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
 
 
-@pytest.mark.parametrize("mode", ["fused", "nofuse", "slots512", "slots2048", "recbound", "groups64"])
-@pytest.mark.parametrize("k", [21, 31])
-def test_skm_fused_counting(kca, orc, monkeypatch, mode, k):
-    """The fused P5a (round 6): a bucket whose distinct records fit the claim
-    list is counted inside P5a (compact records in LDS, their keys walked
-    into a key table in the rest of the LDS, (key, count) records emitted);
-    the rest go to P5 as before. Every route gives the oracle's bytes: fused
-    (default), P5a + P5 only (KC_NO_FUSED), key tables too small for most or
-    some buckets so they fall back to P5 with their distinct records written
-    back (KC_FUSED_SLOTS), a record buffer too small for the first launch
-    (KC_P5_REC_BOUND: P5 reruns and counts the fused buckets again from their
-    records), and P5a tables that overflow (KC_P5A_GROUPS: split lists, P5)."""
-    env = {"nofuse": ("KC_NO_FUSED", "1"), "slots512": ("KC_FUSED_SLOTS", "512"),
-           "slots2048": ("KC_FUSED_SLOTS", "2048"), "recbound": ("KC_P5_REC_BOUND", "5000"),
-           "groups64": ("KC_P5A_GROUPS", "64")}.get(mode)
-    if env:
-        monkeypatch.setenv(*env)
-    fq = kca.synth_fastq(60000, 150, seed=36 + k, genome_length=300_000, n_rate=0.0005)
-    with kca.Context(kmer_length=k, line_length=150, engine="skm") as ctx:
-        ctx.count_fastq(fq)
-        got = ctx.records()
-        st = ctx.stats()
-    assert got == orc.count_fastq(fq, k)
-    assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
-    assert st["engines_used"] == 1
-
-
 @pytest.mark.parametrize("k", [21, 31])
 def test_skm_dedup_weighted_spill(kca, orc, tmp_path, k):
     """Deduplicated records with multiplicities > 1 through the last-resort
