@@ -73,10 +73,10 @@ struct kc_ctx {
     bool skm_used = false;         // a batch went through the skm engine since the last reset
     bool skm_force = false;        // KC_FLAG_ENGINE_SKM: no cardinality sample
     bool skm_checked = false;      // the skm cardinality sample has run since the last reset
-    // S's scratch layout in keys_b (0..2), chosen by timing on the context's
+    // S's scratch region in keys_b (0..2), chosen by timing on the context's
     // first large skm batch; kept for the context's life (page placement is)
     bool sprobe_done = false;
-    int slayout = 0;
+    int sregion = 0;
     double sprobe_ms[3] = {0, 0, 0};
     bool skm_big_off = false;      // a large skm batch overflowed the spill or record buffer: safe batches only
     uint32_t engines_used = 0;     // kc_stats.engines_used
@@ -1257,7 +1257,7 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
 // Reads of nw windows one skm batch may take beyond key_cap windows (see
 // count_reads_skm): the record pool at nw / 4 records per read, while the
 // global table is empty; 0 when only safe batches apply
-// S scratch-layout probe: batches of at least this many records (cfg2: 5.9e8)
+// S scratch-region probe: batches of at least this many records (cfg2: 5.9e8)
 static const uint64_t kSProbeMin = 100000000;
 
 static uint64_t skm_big_reads(const kc_ctx* c, uint64_t nw, uint64_t pool_cap) {
@@ -1369,61 +1369,41 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         if (np > 0) {
             double gm[2] = {0, 0};
             // S's scratch (the first pass's output, the second's input) in
-            // keys_b: at the default layout (offset 0, stride pool_cap) or
-            // another one. The two radix passes run at one of a few rates
-            // fixed for the life of a process by where the driver placed the
-            // pages (up to ~25% apart), and the rate depends on
-            // the layout of the buffers they read and write. The context's
-            // first large batch copies F's records aside (into keys_b's
-            // tail), groups them with the scratch at each candidate layout
-            // twice (records restored and F's first-pass digits rebuilt before
-            // every run) and keeps the fastest layout for its later batches.
+            // keys_b: region sregion of three, at its own stride. The two
+            // radix passes run at one of a few rates fixed for the life of a
+            // process by where the driver placed the pages (up to
+            // ~25% apart); the first large batch of a context times S with
+            // its scratch in each region (the data is regrouped each time,
+            // F's first-pass digit bytes rebuilt first) and keeps the fastest
             uint64_t sbs = pool_cap;
             uint64_t* sbase = c->keys_b;
             bool grouped = false;
             const char* pm_e = test_hook("KC_SPROBE_MIN");  // tests: probe small batches
             const uint64_t sprobe_min = pm_e ? strtoull(pm_e, nullptr, 10) : kSProbeMin;
-            const uint64_t cs = (np + 255) & ~255ull;            // compact stride
-            const uint64_t belems = (uint64_t)RW * pool_cap;     // keys_b's elements
-            const uint64_t copy_at = belems - (uint64_t)RW * cs;  // the records' copy, at the tail
-            // candidates (offset, stride): the default, compact at 0, compact
-            // half-way to the copy; every one ends before the copy
-            const uint64_t lay_off[3] = {0, 0, ((copy_at - (uint64_t)RW * cs) / 2) & ~255ull};
-            const uint64_t lay_str[3] = {pool_cap, cs, cs};
-            const bool fits = (uint64_t)(RW - 1) * pool_cap + cs <= copy_at && (uint64_t)RW * cs * 2 <= copy_at;
-            if (np >= sprobe_min && fits && dig1 && !test_hook("KC_NO_SPROBE")) {
+            if (np >= sprobe_min && !test_hook("KC_NO_SPROBE")) {
+                sbs = (np + 255) & ~255ull;
+                const uint64_t slack = (uint64_t)RW * (pool_cap - sbs);  // elements of keys_b beyond the scratch
+                auto region = [&](int r) { return c->keys_b + ((slack / 2) & ~255ull) * (uint64_t)r; };
                 if (!c->sprobe_done) {
-                    uint64_t* cp = c->keys_b + copy_at;
-                    for (int j = 0; j < RW; j++)
-                        HIPCHK(c, hipMemcpyAsync(cp + (size_t)j * cs, c->keys_a + (size_t)j * pool_cap, np * 8,
-                                                 hipMemcpyDeviceToDevice, c->stream));
                     double best = 0;
-                    for (int run = 0; run < 6; run++) {
-                        const int r = run >> 1;
-                        if (run > 0) {
-                            for (int j = 0; j < RW; j++)
-                                HIPCHK(c, hipMemcpyAsync(c->keys_a + (size_t)j * pool_cap, cp + (size_t)j * cs, np * 8,
-                                                         hipMemcpyDeviceToDevice, c->stream));
-                            HIPCHK(c, launch_key_digits(c->keys_a, 0, np, 48, dig1, c->stream));
-                        }
+                    for (int r = 0; r < 3; r++) {
+                        if (r > 0 && dig1) HIPCHK(c, launch_key_digits(c->keys_a, 0, np, 48, dig1, c->stream));
                         double pm[2] = {0, 0};
-                        if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, c->keys_b + lay_off[r], lay_str[r],
-                                         nullptr, c->digs, np, pm, dig1)))
+                        if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, region(r), sbs, nullptr, c->digs,
+                                         np, pm, dig1)))
                             return s;
-                        if (run == 0 || pm[1] < best) best = pm[1], c->slayout = r;
-                        if (run & 1) c->sprobe_ms[r] = std::min(c->sprobe_ms[r], pm[1]);
-                        else c->sprobe_ms[r] = pm[1];
+                        if (r == 0 || pm[1] < best) best = pm[1], c->sregion = r;
+                        c->sprobe_ms[r] = pm[1];
                         gm[0] = pm[0];
                         gm[1] = pm[1];
                     }
                     c->sprobe_done = true;
                     grouped = true;
                     if (getenv("KC_DEBUG"))
-                        fprintf(stderr, "kc: S scratch layouts %.3f / %.3f / %.3f ms: layout %d\n", c->sprobe_ms[0],
-                                c->sprobe_ms[1], c->sprobe_ms[2], c->slayout);
+                        fprintf(stderr, "kc: S scratch regions %.3f / %.3f / %.3f ms: region %d\n", c->sprobe_ms[0],
+                                c->sprobe_ms[1], c->sprobe_ms[2], c->sregion);
                 } else {
-                    sbase = c->keys_b + lay_off[c->slayout];
-                    sbs = lay_str[c->slayout];
+                    sbase = region(c->sregion);
                 }
             }
             if (!grouped &&

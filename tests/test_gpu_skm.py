@@ -340,12 +340,12 @@ def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
 
 @pytest.mark.parametrize("k,mem", [(31, 1 << 21), (55, 1 << 21), (31, 100_000_000)])
 def test_skm_s_region_probe(kca, orc, monkeypatch, capfd, k, mem):
-    """S's scratch-layout probe (round 6): the context's first large batch
-    copies F's records aside and groups them six times, twice with S's
-    scratch at each of three layouts of keys_b (records restored and F's
-    first-pass digit bytes rebuilt before every run); later batches use the
-    fastest layout. KC_SPROBE_MIN makes small batches large; several batches
-    (2 MiB working set) take the chosen layout. Same bytes as the oracle."""
+    """S's scratch-region probe (round 6): the context's first large batch
+    groups its records three times, with the scratch in each of three regions
+    of keys_b (F's first-pass digit bytes rebuilt before each rerun), and
+    later batches use the fastest region at their own stride. KC_SPROBE_MIN
+    makes small batches large; several batches (2 MiB working set) take the
+    chosen region. Same bytes as the oracle."""
     monkeypatch.setenv("KC_SPROBE_MIN", "1000")
     monkeypatch.setenv("KC_DEBUG", "1")
     fq = kca.synth_fastq(40000, 150, seed=51 + k, genome_length=300_000, n_rate=0.0005)
@@ -354,7 +354,7 @@ def test_skm_s_region_probe(kca, orc, monkeypatch, capfd, k, mem):
         got = ctx.records()
         st = ctx.stats()
     err = capfd.readouterr().err
-    assert err.count("kc: S scratch layouts") == 1, err[-2000:]
+    assert err.count("kc: S scratch regions") == 1, err[-2000:]
     assert got == orc.count_fastq(fq, k)
     if mem < 1 << 22:
         assert st["batches"] > 2
