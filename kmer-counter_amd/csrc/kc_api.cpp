@@ -73,11 +73,6 @@ struct kc_ctx {
     bool skm_used = false;         // a batch went through the skm engine since the last reset
     bool skm_force = false;        // KC_FLAG_ENGINE_SKM: no cardinality sample
     bool skm_checked = false;      // the skm cardinality sample has run since the last reset
-    // S's scratch region in keys_b (0..2), chosen by timing on the context's
-    // first large skm batch; kept for the context's life (page placement is)
-    bool sprobe_done = false;
-    int sregion = 0;
-    double sprobe_ms[3] = {0, 0, 0};
     bool skm_big_off = false;      // a large skm batch overflowed the spill or record buffer: safe batches only
     uint32_t engines_used = 0;     // kc_stats.engines_used
     bool skm_hc = false;           // high cardinality seen: the key-prefix engine counts
@@ -1257,9 +1252,6 @@ static kc_status group16(kc_ctx* c, int NW, bool pay, uint64_t* a, uint64_t sa, 
 // Reads of nw windows one skm batch may take beyond key_cap windows (see
 // count_reads_skm): the record pool at nw / 4 records per read, while the
 // global table is empty; 0 when only safe batches apply
-// S scratch-region probe: batches of at least this many records (cfg2: 5.9e8)
-static const uint64_t kSProbeMin = 100000000;
-
 static uint64_t skm_big_reads(const kc_ctx* c, uint64_t nw, uint64_t pool_cap) {
     if (c->skm_big_off || c->stats_h[ST_CLAIMED] || c->table_dirty || test_hook("KC_SKM_SAFE_BATCH")) return 0;
     return pool_cap / std::max<uint64_t>(1, nw / 4);
@@ -1368,46 +1360,8 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
         }
         if (np > 0) {
             double gm[2] = {0, 0};
-            // S's scratch (the first pass's output, the second's input) in
-            // keys_b: region sregion of three, at its own stride. The two
-            // radix passes run at one of a few rates fixed for the life of a
-            // process by where the driver placed the pages (up to
-            // ~25% apart); the first large batch of a context times S with
-            // its scratch in each region (the data is regrouped each time,
-            // F's first-pass digit bytes rebuilt first) and keeps the fastest
-            uint64_t sbs = pool_cap;
-            uint64_t* sbase = c->keys_b;
-            bool grouped = false;
-            const char* pm_e = test_hook("KC_SPROBE_MIN");  // tests: probe small batches
-            const uint64_t sprobe_min = pm_e ? strtoull(pm_e, nullptr, 10) : kSProbeMin;
-            if (np >= sprobe_min && !test_hook("KC_NO_SPROBE")) {
-                sbs = (np + 255) & ~255ull;
-                const uint64_t slack = (uint64_t)RW * (pool_cap - sbs);  // elements of keys_b beyond the scratch
-                auto region = [&](int r) { return c->keys_b + ((slack / 2) & ~255ull) * (uint64_t)r; };
-                if (!c->sprobe_done) {
-                    double best = 0;
-                    for (int r = 0; r < 3; r++) {
-                        if (r > 0 && dig1) HIPCHK(c, launch_key_digits(c->keys_a, 0, np, 48, dig1, c->stream));
-                        double pm[2] = {0, 0};
-                        if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, region(r), sbs, nullptr, c->digs,
-                                         np, pm, dig1)))
-                            return s;
-                        if (r == 0 || pm[1] < best) best = pm[1], c->sregion = r;
-                        c->sprobe_ms[r] = pm[1];
-                        gm[0] = pm[0];
-                        gm[1] = pm[1];
-                    }
-                    c->sprobe_done = true;
-                    grouped = true;
-                    if (getenv("KC_DEBUG"))
-                        fprintf(stderr, "kc: S scratch regions %.3f / %.3f / %.3f ms: region %d\n", c->sprobe_ms[0],
-                                c->sprobe_ms[1], c->sprobe_ms[2], c->sregion);
-                } else {
-                    sbase = region(c->sregion);
-                }
-            }
-            if (!grouped &&
-                (s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, sbase, sbs, nullptr, c->digs, np, gm, dig1)))
+            if ((s = group16(c, RW, false, c->keys_a, pool_cap, nullptr, c->keys_b, pool_cap, nullptr, c->digs, np,
+                             gm, dig1)))
                 return s;
             c->part_ms[3] += gm[0];
             c->part_ms[2] += gm[1];

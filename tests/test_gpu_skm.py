@@ -338,28 +338,6 @@ def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
     assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
 
 
-@pytest.mark.parametrize("k,mem", [(31, 1 << 21), (55, 1 << 21), (31, 100_000_000)])
-def test_skm_s_region_probe(kca, orc, monkeypatch, capfd, k, mem):
-    """S's scratch-region probe (round 6): the context's first large batch
-    groups its records three times, with the scratch in each of three regions
-    of keys_b (F's first-pass digit bytes rebuilt before each rerun), and
-    later batches use the fastest region at their own stride. KC_SPROBE_MIN
-    makes small batches large; several batches (2 MiB working set) take the
-    chosen region. Same bytes as the oracle."""
-    monkeypatch.setenv("KC_SPROBE_MIN", "1000")
-    monkeypatch.setenv("KC_DEBUG", "1")
-    fq = kca.synth_fastq(40000, 150, seed=51 + k, genome_length=300_000, n_rate=0.0005)
-    with kca.Context(kmer_length=k, line_length=150, gpu_memory_limit=mem, engine="skm") as ctx:
-        ctx.count_fastq(fq)
-        got = ctx.records()
-        st = ctx.stats()
-    err = capfd.readouterr().err
-    assert err.count("kc: S scratch regions") == 1, err[-2000:]
-    assert got == orc.count_fastq(fq, k)
-    if mem < 1 << 22:
-        assert st["batches"] > 2
-
-
 @pytest.mark.parametrize("k", [21, 31])
 def test_skm_dedup_weighted_spill(kca, orc, tmp_path, k):
     """Deduplicated records with multiplicities > 1 through the last-resort
