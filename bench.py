@@ -62,6 +62,7 @@ import importlib.util
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -236,6 +237,11 @@ def gather_runs_to_rank0(kca, ctx, D):
     return 0
 
 
+# --exchange files, shared merge: key-range parts per rank (rounds); the last
+# round's write is the only one not overlapped with merging
+FILES_MERGE_ROUNDS = 4
+
+
 def merge_threads(D):
     """Host threads one rank may use: the usable CPUs shared by the node's local ranks."""
     local = int(os.environ.get("LOCAL_WORLD_SIZE", str(D.world)))
@@ -249,12 +255,14 @@ def host_merge_runs(kca, ctx, D, run_dir, out_path, k, threads=0, where="ranks",
     SortedKMerFile into run_dir (kc_write_output), then the N run files are
     merged into out_path.
       where="ranks" (default): the merge is shared by the ranks, as the
-        reference runs its merge groups concurrently: rank r merges the r-th key
-        range of all N files (kc_merge_part_create; the ranges' boundary keys
+        reference runs its merge groups concurrently: the key space is cut into
+        N x FILES_MERGE_ROUNDS ranges (kc_merge_part_create; the boundary keys
         come from the files by one deterministic rule, so no rank sends another
-        any records), the ranks all-gather their merged sizes (one integer each
+        any records) and rank r merges ranges r, r + N, ... in key order; after
+        each round the ranks all-gather their merged sizes (one integer each
         over the process group: control, not data) and each writes its range at
-        its offset of the one output file (kc_merge_part_write).
+        its offset of the one output file (kc_merge_part_write) while it merges
+        its next one.
       where="rank0": rank 0 merges all N files alone (kc_merge_files).
     `threads` per rank (default: the usable CPUs shared by the node's ranks).
     The barriers only order the ranks. The files are overwritten in place each
@@ -279,15 +287,50 @@ def host_merge_runs(kca, ctx, D, run_dir, out_path, k, threads=0, where="ranks",
         D.barrier_sync()
         tm["merge"] = tm.get("merge", 0.0) + (time.perf_counter() - t1)
         return n, mine
-    with kca.MergePart(runs, k, D.rank, D.world, thr) as part:
+    # the key space in world x R parts, rank r merging parts r, r + N, ... in
+    # key order (rounds): after each round the ranks all-gather the round's
+    # sizes, which fixes the round's offsets, and a rank writes its part of
+    # round i (a background thread; the library releases the GIL) while it
+    # merges its part of round i + 1, so only the last round's write is not
+    # overlapped
+    R = FILES_MERGE_ROUNDS
+    parts = D.world * R
+    total, mine = 0, 0
+    writing = None  # (thread, part, errors) of the previous round
+    t_merge = 0.0
+
+    def finish_write(w):
+        w[0].join()
+        w[1].close()
+        if w[2]:
+            raise w[2][0]
+
+    for i in range(R):
+        t = time.perf_counter()
+        part = kca.MergePart(runs, k, i * D.world + D.rank, parts, thr)
         sizes = D.all_gather_int(part.nbytes)
-        t2 = time.perf_counter()
-        total = sum(sizes)
-        part.write(out_path, sum(sizes[:D.rank]), total)
-        mine = part.nbytes
+        t_merge += time.perf_counter() - t
+        off = total + sum(sizes[:D.rank])
+        total += sum(sizes)
+        if writing is not None:
+            finish_write(writing)
+        errs = []
+
+        def write(p=part, o=off, cut=total if i == R - 1 else 0, e=errs):
+            try:
+                p.write(out_path, o, cut)
+            except Exception as ex:  # raised again on the main thread
+                e.append(ex)
+
+        th = threading.Thread(target=write)
+        th.start()
+        writing = (th, part, errs)
+        mine += part.nbytes
+    t2 = time.perf_counter()
+    finish_write(writing)
     D.barrier_sync()
     t3 = time.perf_counter()
-    tm["merge"] = tm.get("merge", 0.0) + (t2 - t1)
+    tm["merge"] = tm.get("merge", 0.0) + t_merge
     tm["write"] = tm.get("write", 0.0) + (t3 - t2)
     return total // ctx.rs, mine
 

@@ -620,12 +620,10 @@ bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& 
 // One part of a merge shared by several processes (the ranks of a read-shard
 // job, cfg3). Part boundaries are keys chosen from the runs themselves by a
 // deterministic rule, so every process computes the same cuts from the same
-// files without exchanging anything: boundary j (of parts - 1) aims at
-// j / parts of all input records; its candidates are the record at that
-// fraction of each run, and the candidate whose rank (records below it, summed
-// over the runs by binary search) is closest to the target wins; boundaries
-// are made non-decreasing. A key's copies in every run fall on one side of
-// each boundary, so the parts' merges concatenate to the whole merge.
+// files without exchanging anything: boundary j (of parts - 1) is the median
+// of the runs' keys at fraction j / parts of each run. A key's copies in every
+// run fall on one side of each boundary, so the parts' merges concatenate to
+// the whole merge.
 // ---------------------------------------------------------------------------
 
 bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, uint32_t parts, uint32_t threads,
@@ -642,51 +640,42 @@ bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, u
     const int m = (int)acc.size();
     uint64_t total = 0;
     for (int i = 0; i < m; i++) total += acc[i].n;
-    // cut[j][i]: run i's first record of part j (cut[0] = 0, cut[parts] = n)
-    std::vector<std::vector<uint64_t>> cut(parts + 1, std::vector<uint64_t>(m, 0));
-    for (int i = 0; i < m; i++) cut[parts][i] = acc[i].n;
-    std::vector<uint8_t> prev_key;
-    uint8_t key[8 * 4 + 4];
-    for (uint32_t j = 1; j < parts; j++) {
-        const long double target = (long double)total * j / parts;
-        bool have = false;
-        long double best_d = 0;
-        std::vector<uint8_t> best_key(rs);
-        std::vector<uint64_t> best_pos(m);
+    // run i's first record of part j: 0 for j = 0, n_i for j = parts, else
+    // the lower bound of boundary key K_j, the median of the runs' keys at
+    // fraction j / parts of each run. Each run's candidate is non-decreasing
+    // in j, so their median is, and the parts are disjoint key ranges in
+    // order; only boundaries part and part + 1 are needed (O(m log n) reads).
+    auto cut_at = [&](uint32_t j, std::vector<uint64_t>* cut) -> bool {
+        cut->assign(m, 0);
+        if (j == 0) return true;
+        if (j >= parts) {
+            for (int i = 0; i < m; i++) (*cut)[i] = acc[i].n;
+            return true;
+        }
+        std::vector<std::vector<uint8_t>> cand;
+        uint8_t key[8 * 4 + 4];
         for (int c = 0; c < m; c++) {
             if (acc[c].n == 0) continue;
             const uint64_t at = std::min<uint64_t>(acc[c].n - 1, (uint64_t)((long double)acc[c].n * j / parts));
-            if (!acc[c].read(at, 1, key)) {
-                if (err_no) *err_no = errno ? errno : EIO;
-                return false;
-            }
-            std::vector<uint64_t> pos(m);
-            uint64_t below = 0;
-            for (int i = 0; i < m; i++) {
-                if (!acc[i].lower_bound(key, W, 0, acc[i].n, &pos[i])) {
-                    if (err_no) *err_no = errno ? errno : EIO;
-                    return false;
-                }
-                below += pos[i];
-            }
-            const long double d = below > target ? below - target : target - below;
-            if (!have || d < best_d || (d == best_d && key_compare(key, best_key.data(), W) < 0)) {
-                have = true;
-                best_d = d;
-                memcpy(best_key.data(), key, rs);
-                best_pos = pos;
-            }
+            if (!acc[c].read(at, 1, key)) return false;
+            cand.emplace_back(key, key + rs);
         }
-        if (!have) continue;  // every run empty: all cuts stay 0
-        if (!prev_key.empty() && key_compare(best_key.data(), prev_key.data(), W) < 0) {
-            best_key = prev_key;  // non-decreasing boundaries
-            best_pos = cut[j - 1];
-        }
-        cut[j] = best_pos;
-        prev_key = best_key;
+        if (cand.empty()) return true;  // every run empty
+        std::sort(cand.begin(), cand.end(), [&](const std::vector<uint8_t>& x, const std::vector<uint8_t>& y) {
+            return key_compare(x.data(), y.data(), W) < 0;
+        });
+        const uint8_t* kj = cand[(cand.size() - 1) / 2].data();
+        for (int i = 0; i < m; i++)
+            if (!acc[i].lower_bound(kj, W, 0, acc[i].n, &(*cut)[i])) return false;
+        return true;
+    };
+    std::vector<uint64_t> lo, hi;
+    if (!cut_at(part, &lo) || !cut_at(part + 1, &hi)) {
+        if (err_no) *err_no = errno ? errno : EIO;
+        return false;
     }
     std::vector<std::vector<uint64_t>> bounds;
-    if (!plan_ranges(acc, W, cut[part], cut[part + 1], &bounds, err_no)) return false;
+    if (!plan_ranges(acc, W, lo, hi, &bounds, err_no)) return false;
     out->ranges.assign(bounds.size() - 1, std::vector<uint8_t>());
     uint64_t merged = 0;
     bool ok = merge_ranges(acc, W, bounds, threads, &merged, err_no,
@@ -696,7 +685,7 @@ bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, u
                            });
     out->bytes = merged;
     out->threads = threads;
-    for (int i = 0; i < m; i++) out->in_records += cut[part + 1][i] - cut[part][i];
+    for (int i = 0; i < m; i++) out->in_records += hi[i] - lo[i];
     return ok;
 }
 
