@@ -423,9 +423,10 @@ static uint64_t merge_slices(const std::vector<const uint8_t*>& beg, const std::
 // the cut moves past the repeat (upper bound), so no worker is handed the
 // whole remainder. A range of one repeated key stays whole.
 static bool plan_ranges(const std::vector<RunAccess>& acc, int W, const std::vector<uint64_t>& lo0,
-                        const std::vector<uint64_t>& hi0, std::vector<std::vector<uint64_t>>* bounds, int* err_no) {
+                        const std::vector<uint64_t>& hi0, std::vector<std::vector<uint64_t>>* bounds, int* err_no,
+                        uint64_t rr = 0) {
     const int m = (int)acc.size();
-    const uint64_t rr = range_recs();
+    if (rr == 0) rr = range_recs();
     using Rg = std::pair<std::vector<uint64_t>, std::vector<uint64_t>>;
     std::vector<Rg> todo{{lo0, hi0}}, done;
     uint8_t key[8 * 4 + 4], rec[8 * 4 + 4];
@@ -514,7 +515,7 @@ static bool merge_ranges(const std::vector<RunAccess>& acc, int W, const std::ve
     std::atomic<size_t> cursor(0);
     std::atomic<int> bad(0);
     auto work = [&]() {
-        std::vector<uint8_t> in, res;
+        ByteBuf in, res;
         for (;;) {
             const size_t r = cursor.fetch_add(1);
             if (r >= nr) break;
@@ -545,7 +546,7 @@ static bool merge_ranges(const std::vector<RunAccess>& acc, int W, const std::ve
                 committed = r + 1;
             }
             cv.notify_all();
-            if (ok && !sink(r, res.data(), nbytes, off)) bad = errno ? errno : EIO;
+            if (ok && !sink(r, res, nbytes, off)) bad = errno ? errno : EIO;
         }
     };
     std::vector<std::thread> pool;
@@ -603,7 +604,9 @@ bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& 
     }
     uint64_t total = 0;
     bool ok = merge_ranges(acc, W, bounds, threads, &total, err_no,
-                           [&](size_t, const uint8_t* p, uint64_t n, uint64_t off) { return pwrite_all(fd, p, n, off); });
+                           [&](size_t, ByteBuf& res, uint64_t n, uint64_t off) {
+                               return pwrite_all(fd, res.data(), n, off);
+                           });
     // written in place, cut to size (no truncation of an old file first)
     if (ok && ftruncate(fd, (off_t)total) != 0) {
         if (err_no) *err_no = errno;
@@ -674,13 +677,23 @@ bool merge_runs_part(const std::vector<RunSource>& runs, int W, uint32_t part, u
         if (err_no) *err_no = errno ? errno : EIO;
         return false;
     }
+    // sub-ranges small enough that every worker gets several (a part is a
+    // fraction of the merge: with kRangeRecs ranges the last few would leave
+    // most workers idle)
+    uint64_t part_recs = 0;
+    for (int i = 0; i < m; i++) part_recs += hi[i] - lo[i];
+    const uint64_t rr = std::max<uint64_t>(1u << 16, std::min<uint64_t>(range_recs(),
+                                                                       part_recs / (8ull * std::max(1u, threads))));
     std::vector<std::vector<uint64_t>> bounds;
-    if (!plan_ranges(acc, W, lo, hi, &bounds, err_no)) return false;
-    out->ranges.assign(bounds.size() - 1, std::vector<uint8_t>());
+    if (!plan_ranges(acc, W, lo, hi, &bounds, err_no, rr)) return false;
+    out->ranges.assign(bounds.size() - 1, ByteBuf());
     uint64_t merged = 0;
+    // a range's merged bytes stay in the worker's buffer, which the part
+    // keeps (no copy; its unused tail is never touched)
     bool ok = merge_ranges(acc, W, bounds, threads, &merged, err_no,
-                           [&](size_t r, const uint8_t* p, uint64_t n, uint64_t) {
-                               out->ranges[r].assign(p, p + n);
+                           [&](size_t r, ByteBuf& res, uint64_t n, uint64_t) {
+                               res.resize((size_t)n);
+                               out->ranges[r].swap(res);
                                return true;
                            });
     out->bytes = merged;

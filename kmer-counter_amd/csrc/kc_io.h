@@ -8,10 +8,34 @@
 #include <stdint.h>
 
 #include <fstream>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace kc {
+
+// Byte buffers whose growth does not zero-fill (merge input and output
+// buffers are written before they are read).
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() noexcept = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+using ByteBuf = std::vector<uint8_t, DefaultInitAlloc<uint8_t>>;
 
 // A sorted run: either a file or a host memory range.
 struct RunSource {
@@ -86,7 +110,7 @@ bool merge_runs_parallel(const std::vector<RunSource>& runs, const std::string& 
 // merge_runs' bytes; part p's offset in the output is the sum of the sizes of
 // parts 0..p-1 (the caller gathers them).
 struct MergedPart {
-    std::vector<std::vector<uint8_t>> ranges;  // merged bytes, range by range in key order
+    std::vector<ByteBuf> ranges;               // merged bytes, range by range in key order
     uint64_t bytes = 0;                        // sum of the ranges' sizes
     uint64_t in_records = 0;                   // input records of the part (all runs)
     uint32_t threads = 1;                      // writers of write_part_at
