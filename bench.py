@@ -237,8 +237,8 @@ def gather_runs_to_rank0(kca, ctx, D):
     return 0
 
 
-# --exchange files, shared merge: key-range parts per rank (rounds); the last
-# round's write is the only one not overlapped with merging
+# --exchange files, shared merge: key-range parts per rank (rounds, at least
+# this many); the last round's write is the only one not overlapped with merging
 FILES_MERGE_ROUNDS = 4
 
 
@@ -293,7 +293,7 @@ def host_merge_runs(kca, ctx, D, run_dir, out_path, k, threads=0, where="ranks",
     # round i (a background thread; the library releases the GIL) while it
     # merges its part of round i + 1, so only the last round's write is not
     # overlapped
-    R = FILES_MERGE_ROUNDS
+    R = max(FILES_MERGE_ROUNDS, 16 // D.world)  # (the last round's part: ~1/16 of the output at any N)
     parts = D.world * R
     total, mine = 0, 0
     writing = None  # (thread, part, errors) of the previous round
