@@ -205,15 +205,25 @@ def test_auto_engine_switches_on_high_cardinality(kca, orc):
     assert got == orc.count_fastq(fq, k)
 
 
-def test_auto_engine_keeps_skm_on_genome_reads(kca, orc):
+@pytest.mark.parametrize("sample", [False, True])
+def test_auto_engine_keeps_skm_on_genome_reads(kca, orc, monkeypatch, capfd, sample):
+    """Genome reads at coverage keep the skm engine: the coverage sketch sees
+    clear coverage and skips the skm bucket sample (round 6), or
+    (KC_SKM_SAMPLE) the sample runs and agrees."""
+    monkeypatch.setenv("KC_DEBUG", "1")
+    if sample:
+        monkeypatch.setenv("KC_SKM_SAMPLE", "1")
     n, L, k = 160_000, 150, 31
     fq = kca.synth_fastq(n, L, seed=78, genome_length=400_000)
     with kca.Context(kmer_length=k, line_length=L, engine="auto", gpu_memory_limit=4 << 30) as ctx:
         ctx.count_fastq(fq)
         got = ctx.records()
         st = ctx.stats()
+    err = capfd.readouterr().err
     assert st["engines_used"] == 1
     assert got == orc.count_fastq(fq, k)
+    # the sample's launch over the first 256 buckets (P5[0,256)) runs only when forced
+    assert ("P5[0,256)" in err) == sample, err[-2000:]
 
 
 def test_auto_engine_switch_after_skm_batches(kca, orc):
