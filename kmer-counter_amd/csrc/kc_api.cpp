@@ -1551,7 +1551,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
 // stays as the second check. Saves the skm engine's F and S passes over a
 // batch it would give up.
 static const double kSketchDistinctMax = 0.7;
-static const double kSketchCoveredMax = 0.2;  // below: the skm bucket sample is not needed
+static const double kSketchCoveredMax = 0.6;  // below: the skm bucket sample is not needed
 
 static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t pre0) {
     kc_status s;
@@ -1592,8 +1592,11 @@ static kc_status sketch_engine(kc_ctx* c, uint64_t n_reads, int64_t L, int64_t p
         c->skm_checked = true;
     } else if ((double)distinct < kSketchCoveredMax * (double)m && !test_hook("KC_SKM_SAMPLE")) {
         // clear coverage: the skm engine's bucket sample (its own check, at
-        // 35% distinct) would keep the skm engine too; skipped, which saves
-        // its two small launches and their synchronisation (~0.3 ms per reset)
+        // 35% distinct keys) would keep the skm engine too; skipped, which
+        // saves its two small launches and their synchronisation. (The sketch
+        // samples only 16-base-aligned positions, so a k-mer covered c times
+        // is sampled ~c/16 times: 60% distinct samples is a window coverage of
+        // ~16, where about 6% of the keys are distinct)
         c->skm_checked = true;
     }
     return KC_OK;
