@@ -1278,9 +1278,15 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
     // batches, so fewer runs for the finish to merge (SURVEY cfg4: 125M reads
     // per GPU in one batch). A spill overflow in such a batch undoes it (table
     // cleared, records and statistics restored) and retries it at the safe size.
-    const uint64_t safe_reads = c->key_cap / nw;
+    uint64_t safe_reads = c->key_cap / nw;
     if (safe_reads == 0) return fail(c, KC_ERR_ARG, "gpu_memory_limit too small for one read's windows");
     uint64_t max_reads = std::max(safe_reads, skm_big_reads(c, nw, pool_cap));
+    // even batch sizes when a read's code row is an odd number of words: every
+    // batch's masks then start 4-byte aligned, which F3's dword DMA needs
+    const bool even = (groups_per_read((int)L) & 1) != 0;
+    auto even_down = [&](uint64_t v) { return even && v > 1 ? v & ~1ull : v; };
+    safe_reads = even_down(safe_reads);
+    max_reads = even_down(max_reads);
     kc_status s;
     uint64_t done = 0;
     float t = 0.f;
@@ -1350,7 +1356,7 @@ static kc_status count_reads_skm(kc_ctx* c, const uint8_t* base, const uint64_t*
             memcpy(c->stats_h, saved.data(), ST_N * 8);
             restore_host_counters(c, hsaved);
             if (nr <= 1) return fail(c, KC_ERR_INTERNAL, "skm pool overflow on one read");
-            max_reads = nr / 2;
+            max_reads = nr / 2 > 1 ? even_down(nr / 2) : 1;
             continue;
         }
         if (experiment_knob("KC_F_SKIP")) {  // records are invalid, stop after F
@@ -1720,6 +1726,9 @@ static kc_status pend_count_fixed(kc_ctx* c, uint64_t n) {
                 const uint64_t nw = (uint64_t)(L - c->k + 1);
                 bs = std::max(b, skm_big_reads(c, nw, (uint64_t)c->W * c->key_cap / (c->W + 1)));
             }
+            // (an even read count per slice when a code row has an odd number
+            // of words: each slice's masks start 4-byte aligned for F3)
+            if ((groups_per_read((int)L) & 1) && bs > 1) bs &= ~1ull;
             for (uint64_t r0 = 0; r0 < n; r0 += bs) {
                 if ((s = count_reads(c, nullptr, nullptr, n - r0 < bs ? n - r0 : bs, L, (int64_t)r0))) return s;
                 if ((s = cut_run_if_full(c))) return s;
@@ -1878,7 +1887,10 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
     // skips an empty row for free): the key-prefix front end walks them
     // (cfg5, k = 55: P1 + P2 +1.5 ms against 0.7 ms saved in the index,
     // same-box A/B), as do F2 and the W >= 2 front ends
-    const bool f3_rows = c->skm && c->W == 1 && c->k >= 19 && c->k <= 32;
+    // (the same conditions as F3's own choice: skm engine not
+    // handed over to the key-prefix engine, F3's geometry and LDS budget)
+    const bool f3_rows = c->skm && !c->skm_hc && c->W == 1 && c->k >= 19 && c->k <= 32 &&
+                         skm_f3_applies((int)L, (int)c->k);
     const bool spec = count && !var && !two_pass && !no_spec && f3_rows && engine_reads_codes(c, L) &&
                       fq_spec_ok((int)L) && !test_hook("KC_NO_FQ_ENCODE") && !test_hook("KC_NO_FQ_SPEC");
     const uint64_t spec_rows = spec ? nch * fq_spec_rows_per_chunk((int)L) : 0;

@@ -325,6 +325,7 @@ struct SkmGeom {
     size_t lds;     // F dynamic LDS bytes
 };
 SkmGeom skm_geometry(int L, int k);
+bool skm_f3_applies(int L, int k);  // the F3 front end counts (L, k) batches
 // F: records (RW = W + 1 words, SoA at pool_cap) of the launch's reads; *pool_cursor
 // (zeroed by the caller) ends as the number of records handed out (padding
 // included); > pool_cap means the pool overflowed and nothing may be used.

@@ -1347,6 +1347,23 @@ static bool f3_args(const CountLaunch& l, const SkmGeom& g, F3Args* a, size_t* l
     return true;
 }
 
+// Whether F3 counts (L, k) batches (its geometry and LDS budget; the codes'
+// alignment is the batch split's, kept even by count_reads_skm): the one-pass
+// FASTQ index is used only then, since only F3 skips its empty rows for free
+bool skm_f3_applies(int L, int k) {
+    const SkmGeom g = skm_geometry(L, k);
+    if (!g.ok) return false;
+    static const uint32_t aligned[4] = {0, 0, 0, 0};
+    CountLaunch l{};
+    l.L = L;
+    l.k = k;
+    l.codes = aligned;
+    l.inval = (const uint16_t*)aligned;
+    F3Args a;
+    size_t lds = 0;
+    return f3_args(l, g, &a, &lds);
+}
+
 // F2 geometry for (L, k) (W = 1, m = 11): false when F2 does not apply
 static bool f2_args(const CountLaunch& l, const SkmGeom& g, F2Args* a, size_t* lds) {
     const int W = (l.k + 31) / 32;
