@@ -1923,7 +1923,13 @@ static kc_status ingest_fastq(kc_ctx* c, const uint8_t* base, uint64_t n, int64_
             lr[1] <= fq_spec_rows_per_chunk((int)L)) {
             const uint64_t n_rec = lines / 4;
             if (n_rec_out) *n_rec_out = n_rec;
-            c->pend_reads += nch * lr[1];  // rows the kernel used (<= the reserved spec_rows)
+            // rows the kernel used (<= the reserved spec_rows). The pending
+            // batch counts rows, empty ones included (~4% at cfg2's headers, up
+            // to ~15% for short headers): batch sizing, the record pool's
+            // reservation and the sketch's sampling rate treat every row as a
+            // read, so they err on the safe side (more room reserved, a few
+            // more samples); st.reads and st.windows count the real records
+            c->pend_reads += nch * lr[1];
             c->pend_sparse = true;
             c->st.reads += n_rec;
             c->st.windows += n_rec * (uint64_t)(L - c->k + 1);

@@ -348,6 +348,21 @@ def test_skm_dedup_genome_reads(kca, orc, monkeypatch, groups):
     assert st["valid_kmers"] == sum(int.from_bytes(got[i + 8:i + 12], "little") for i in range(0, len(got), 12))
 
 
+@pytest.mark.parametrize("L,mem", [(140, 1 << 21), (140, 3 << 20), (150, 1 << 21), (129, 5 << 20)])
+def test_skm_odd_code_rows_batches(kca, orc, L, mem):
+    """Reads whose code row is an odd number of words (L = 140: 9 words;
+    129: 9) counted in many skm batches from one-pass index rows: batch slices
+    hold an even number of reads so every slice's masks are 4-byte aligned for
+    F3's DMA; L = 150 (10 words) alongside. Oracle bytes."""
+    fq = kca.synth_fastq(30000, L, seed=60 + L, genome_length=200_000, n_rate=0.0005)
+    with kca.Context(kmer_length=31, line_length=L, gpu_memory_limit=mem, engine="skm") as ctx:
+        ctx.count_fastq(fq)
+        got = ctx.records()
+        st = ctx.stats()
+    assert st["batches"] > 2
+    assert got == orc.count_fastq(fq, 31)
+
+
 @pytest.mark.parametrize("k", [21, 31])
 def test_skm_dedup_weighted_spill(kca, orc, tmp_path, k):
     """Deduplicated records with multiplicities > 1 through the last-resort
