@@ -7,10 +7,18 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <vector>
 
 #include "kc_device.h"
+
+// RP_PAD experiment: digit d's output run starts d x pad records later (gaps
+// between the 256 digit regions; the output check is skipped then)
+__global__ void pad_pos_k(uint64_t* pos, uint64_t n, uint64_t pad) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        pos[i] += (i & 255) * pad;
+}
 
 __global__ void fill_k(uint64_t* a, uint64_t n, int NW, uint64_t seed) {
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
@@ -50,21 +58,30 @@ int main(int argc, char** argv) {
     // of three regions each, six (input, output) region pairs timed in one
     // process; >= 0: one, b at a + its size + layout bytes
     const long long layout = argc > 6 ? atoll(argv[6]) : -1;
-    const int nreg = layout == -3 ? 3 : 1;  // -3: three regions per buffer, pairs timed in one process
+    // -3: RP_NREG (default 3) regions per buffer, (input, output) pairs timed in one process
+    const int nreg = layout == -3 ? (getenv("RP_NREG") ? atoi(getenv("RP_NREG")) : 3) : 1;
+    uint64_t padn = 0;
+    for (const char* q = getenv("RP_PADS") ? getenv("RP_PADS") : getenv("RP_PAD"); q && *q;) {
+        const uint64_t v = 256 * strtoull(q, nullptr, 10);
+        if (v > padn) padn = v;
+        const char* c = strchr(q, ',');
+        q = c ? c + 1 : nullptr;
+    }
+    const uint64_t ob = n + padn;  // output stride (records)
     if (layout == -3) {
-        CK(hipMalloc(&a, 3 * n * 8 * NW));
-        CK(hipMalloc(&b, 3 * n * 8 * NW));
+        CK(hipMalloc(&a, nreg * n * 8 * NW));
+        CK(hipMalloc(&b, nreg * ob * 8 * NW));
     } else if (layout == -2) {  // physically contiguous allocations
         CK(hipExtMallocWithFlags((void**)&a, n * 8 * NW, hipDeviceMallocContiguous));
         CK(hipExtMallocWithFlags((void**)&b, n * 8 * NW, hipDeviceMallocContiguous));
     } else if (layout < 0) {
         CK(hipMalloc(&a, n * 8 * NW));
-        CK(hipMalloc(&b, n * 8 * NW));
+        CK(hipMalloc(&b, ob * 8 * NW));
     } else {
         CK(hipMalloc(&a, 2 * n * 8 * NW + (uint64_t)layout + 256));
         b = (uint64_t*)((char*)a + ((n * 8 * NW + (uint64_t)layout + 255) & ~255ull));
     }
-    CK(hipMalloc(&digs, n + 64));
+    CK(hipMalloc(&digs, ob + 64));
     CK(hipMalloc(&rt, 64));
     CK(hipMalloc(&pos, nt * 256 * 8));
     CK(hipMalloc(&tmp, nt * 256 * 8 + (64 << 20)));
@@ -78,17 +95,33 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    // RP_PADS=p0,p1,...: the pairs are timed once per pad (the largest sizes
+    // the output buffer; RP_PAD: one pad)
+    std::vector<uint64_t> pads;
+    {
+        const char* e = getenv("RP_PADS") ? getenv("RP_PADS") : getenv("RP_PAD");
+        for (const char* q = e; q && *q;) {
+            pads.push_back(strtoull(q, nullptr, 10));
+            const char* c = strchr(q, ',');
+            q = c ? c + 1 : nullptr;
+        }
+        if (pads.empty()) pads.push_back(0);
+    }
+    for (uint64_t pad : pads) {
     CK(kc::launch_rp_hist(nullptr, a, dshift, rt, rt + 2, 1, nt, (uint32_t)tile, pos, tmp, 2 * ncu, s));
-    const int pairs[6][2] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {2, 2}, {2, 0}};
+    if (pad) hipLaunchKernelGGL(pad_pos_k, dim3(1024), dim3(256), 0, s, pos, nt * 256, pad);
+    const int R1 = nreg - 1, RH = nreg / 2;
+    const int pairs[6][2] = {{0, 0}, {0, nreg > 3 ? R1 : 1}, {nreg > 3 ? RH : 1, 0}, {nreg > 3 ? RH : 1, nreg > 3 ? RH : 1},
+                             {R1, R1}, {R1, 0}};
     const int sweeps = getenv("RP_SWEEPS") ? atoi(getenv("RP_SWEEPS")) : 1;  // repeat the pairs: stable?
     for (int pk = 0; pk < (nreg > 1 ? 6 * sweeps : 1); pk++) {
     const int pi = pk % 6;
     uint64_t* ai = a + (uint64_t)pairs[pi][0] * n * NW;
-    uint64_t* bi = b + (uint64_t)pairs[pi][1] * n * NW;
+    uint64_t* bi = b + (uint64_t)pairs[pi][1] * ob * NW;
     float best = 1e30f, tot = 0.f;
     for (int r = 0; r < reps + 1; r++) {
         CK(hipEventRecord(e0, s));
-        CK(kc::launch_rp_scatter(NW, false, ai, n, bi, n, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift,
+        CK(kc::launch_rp_scatter(NW, false, ai, n, bi, ob, nullptr, nullptr, rt, rt + 2, 1, nt, pos, dshift,
                                  with_emit ? digs : nullptr, 56, 2 * ncu, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
@@ -100,7 +133,7 @@ int main(int argc, char** argv) {
         }
     }
     // check: output digits ascending, every item once (hash sums), emitted digit bytes
-    {
+    if (!pad && !getenv("RP_NOCHECK")) {
         std::vector<uint64_t> hi((size_t)n * NW), ho((size_t)n * NW);
         std::vector<uint8_t> hd(with_emit ? n : 1);
         CK(hipMemcpy(hi.data(), ai, n * 8 * NW, hipMemcpyDeviceToHost));
@@ -126,9 +159,10 @@ int main(int argc, char** argv) {
         }
     }
     const double bytes = (double)n * (16.0 * NW + (with_emit ? 1.0 : 0.0));
-    printf("{\"pair\": [%d, %d], \"dshift\": %d, \"n\": %llu, \"NW\": %d, \"emit\": %d, \"tile\": %llu, \"avg_ms\": %.3f, \"best_ms\": %.3f, \"GBps_avg\": %.1f}\n",
-           pairs[pi][0], pairs[pi][1], dshift, (unsigned long long)n, NW, with_emit ? 1 : 0, (unsigned long long)tile, tot / reps, best,
+    printf("{\"pad\": %llu, \"pair\": [%d, %d], \"dshift\": %d, \"n\": %llu, \"NW\": %d, \"emit\": %d, \"tile\": %llu, \"avg_ms\": %.3f, \"best_ms\": %.3f, \"GBps_avg\": %.1f}\n",
+           (unsigned long long)pad, pairs[pi][0], pairs[pi][1], dshift, (unsigned long long)n, NW, with_emit ? 1 : 0, (unsigned long long)tile, tot / reps, best,
            bytes / (tot / reps / 1e3) / 1e9);
+    }
     }
     return 0;
 }
