@@ -111,11 +111,23 @@ int main(int argc, char** argv) {
     CK(kc::launch_rp_hist(nullptr, a, dshift, rt, rt + 2, 1, nt, (uint32_t)tile, pos, tmp, 2 * ncu, s));
     if (pad) hipLaunchKernelGGL(pad_pos_k, dim3(1024), dim3(256), 0, s, pos, nt * 256, pad);
     const int R1 = nreg - 1, RH = nreg / 2;
-    const int pairs[6][2] = {{0, 0}, {0, nreg > 3 ? R1 : 1}, {nreg > 3 ? RH : 1, 0}, {nreg > 3 ? RH : 1, nreg > 3 ? RH : 1},
-                             {R1, R1}, {R1, 0}};
+    int pairs[64][2] = {{0, 0}, {0, nreg > 3 ? R1 : 1}, {nreg > 3 ? RH : 1, 0}, {nreg > 3 ? RH : 1, nreg > 3 ? RH : 1},
+                        {R1, R1}, {R1, 0}};
+    int npairs = 6;
+    if (const char* e = getenv("RP_PAIRS")) {  // "i:o,i:o,..."
+        npairs = 0;
+        for (const char* q = e; q && *q && npairs < 64;) {
+            pairs[npairs][0] = atoi(q);
+            const char* c = strchr(q, ':');
+            pairs[npairs][1] = c ? atoi(c + 1) : 0;
+            npairs++;
+            c = strchr(q, ',');
+            q = c ? c + 1 : nullptr;
+        }
+    }
     const int sweeps = getenv("RP_SWEEPS") ? atoi(getenv("RP_SWEEPS")) : 1;  // repeat the pairs: stable?
-    for (int pk = 0; pk < (nreg > 1 ? 6 * sweeps : 1); pk++) {
-    const int pi = pk % 6;
+    for (int pk = 0; pk < (nreg > 1 ? npairs * sweeps : 1); pk++) {
+    const int pi = pk % npairs;
     uint64_t* ai = a + (uint64_t)pairs[pi][0] * n * NW;
     uint64_t* bi = b + (uint64_t)pairs[pi][1] * ob * NW;
     float best = 1e30f, tot = 0.f;
