@@ -952,7 +952,11 @@ struct F3Cfg {
 #ifndef KC_F3_WPE
 #define KC_F3_WPE 4  // F3: waves per SIMD the register budget is sized for
 #endif
-constexpr int kF3Ring = 384;  // per wave (u64): < 64 + 4 x 64 descriptors between drain checks, then a spare slot per lane
+// per wave (u64): < 64 + 2 x 64 descriptors between drain checks, then a
+// spare slot per lane (with a check every 4 windows and 384 slots, a
+// wave's LDS at L = 150 kept F3 to 3 waves per SIMD instead of 4)
+constexpr int kF3Ring = 256;
+constexpr int kF3Check = 2;  // windows between drain checks
 
 struct F3Args {
     const u32* codes;             // kernel E output, G u32 per read
@@ -1000,6 +1004,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     unsigned char* wb = smem + (size_t)wave * a.wbytes;
     u64* ring = (u64*)wb;
+    u64* const spare = ring + (kF3Ring - 64 + lane_id());  // the lane's slot when it pushes nothing
     u32* rflag = (u32*)(wb + kF3Ring * 8);
     u32* codes = rflag + 64;                 // 64 rows x NG words
     u32* stage = codes + 64 * a.NG;          // next tile: 64 G code words, then 32 G mask dwords (u16 pairs)
@@ -1053,10 +1058,8 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
             ccur += ptot;
         }
         const u32* crw = codes + (hi >> 16) * NG;
-        for (u32 p = 0; p < pieces; p++) {
-            const u32 off = p * NMAX;
-            const u32 nn = min(NMAX, n - off);
-            const int ps = (int)(s0 + off);
+        // record of the piece of nn windows from window ps
+        auto piece = [&](int ps, u32 nn, u64 (&rec)[RW]) {
             const int g = ps >> 4, o = ps & 15;
             u32 cw[2 * RW + 1];
 #pragma unroll
@@ -1064,7 +1067,6 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
             u32 sw[2 * RW];
 #pragma unroll
             for (int x = 0; x < 2 * RW; x++) sw[x] = o ? __builtin_amdgcn_alignbit(cw[x], cw[x + 1], 32 - 2 * o) : cw[x];
-            u64 rec[RW];
             rec[0] = (bkt << 48) | ((((u64)sw[0] << 32) | sw[1]) >> 16);
 #pragma unroll
             for (int j = 1; j < RW; j++) rec[j] = ((((u64)sw[2 * j - 1] << 32) | sw[2 * j]) << 16) | (sw[2 * j + 1] >> 16);
@@ -1076,6 +1078,25 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                 if (bits < 64) rec[j] &= bits <= 0 ? 0ull : (~0ull << (64 - bits));
             }
             rec[RW - 1] |= (u64)nn;
+        };
+        // the usual drain (wave-uniform test): one piece per lane, all in the
+        // current chunk and the pool, slot b0 + lane (uniform bases, 32-bit
+        // lane offsets, no 64-bit slot arithmetic per lane)
+        if (!multi && (u64)ptot <= room && b0 + (u64)ptot <= a.pool_cap && !(a.skip & 1)) {
+            if (has) {
+                u64 rec[RW];
+                piece((int)s0, min(NMAX, n), rec);  // n <= NMAX here (!multi)
+                u64* const w0 = a.pool + readlane64(b0, 0);
+#pragma unroll
+                for (int j = 0; j < RW; j++) (w0 + (u64)j * a.pool_cap)[(u32)lane] = rec[j];
+                if (a.dig1) (a.dig1 + readlane64(b0, 0))[(u32)lane] = (unsigned char)bkt;
+            }
+            return;
+        }
+        for (u32 p = 0; p < pieces; p++) {
+            const u32 off = p * NMAX;
+            u64 rec[RW];
+            piece((int)(s0 + off), min(NMAX, n - off), rec);
             const u32 gq = pb + p;
             const u64 dst = ((u64)gq < room ? b0 : b1) + gq;
             if (dst < a.pool_cap && !(a.skip & 1)) {
@@ -1191,7 +1212,10 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
 #pragma unroll
                 for (int i = 0; i < B; i++) h[i] = mul_u24(f3_mmer(c0, c1, OFF + i) ^ 0xd1e995u, 0x9e3779u);
                 u32 P = h[0];
-                const u32 wv0 = (u32)(p0 - E) + (u32)lane * 0u;  // window of j = 0, in a VGPR
+                const u32 wv0 = (u32)(p0 - E);  // window of j = 0
+                // the open run as one register, first window << 16 | bucket:
+                // a boundary replaces it, its low half is prev (16-bit compare)
+                u32 sl = (s << 16) | prev;
                 f3_static_for<0, B>([&](auto jt) {
                     constexpr int j = decltype(jt)::value;
                     if constexpr (j > 0) P = min(P, h[j]);
@@ -1203,17 +1227,28 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                     u32 u = min(v & 0xffffu, kNoKey - 1u);
                     const u32 w = wv0 + (u32)j;
                     if constexpr (VT) u = (int)w < nwr ? u : kNoKey;
-                    const bool bnd = u != prev;
+                    const bool bnd = (unsigned short)u != (unsigned short)sl;
                     const u64 pm = __builtin_amdgcn_ballot_w64(bnd) & livem;
-                    const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0u)) + qn;
-                    const u32 slot = (bnd && live) ? rank : (u32)(kF3Ring - 64 + lane);
-                    ring[slot] = ((u64)(ltag | (w - 1u)) << 32) | ((s << 16) | prev);
+                    u32 mb = __builtin_amdgcn_mbcnt_hi((u32)(pm >> 32), __builtin_amdgcn_mbcnt_lo((u32)pm, 0u));
+                    // the rank in every lane, then a select: without this the
+                    // compiler sinks the rank into a branch on bnd and the
+                    // select into a second one (~8 more SALU per window)
+                    asm volatile("" : "+v"(mb));
+                    // every lane stores (a lane that pushes nothing to its spare
+                    // slot): faster than a store by the pushing lanes only,
+                    // whose exec mask costs more than the bank conflicts it
+                    // avoids (7.91-7.97 vs 7.85-7.88 ms at cfg2)
+                    u64* const slot = (bnd && live) ? ring + qn + mb : spare;
+                    *slot = ((u64)(ltag | (w - 1u)) << 32) | sl;
                     qn += (u32)__popcll(pm);
-                    if (bnd) s = w;
-                    prev = u;
-                    if constexpr ((j & 3) == 3)
+                    u32 wsh = w << 16;
+                    asm volatile("" : "+s"(wsh));  // one SGPR, not (first << 16) | u | (j << 16)
+                    sl = bnd ? (wsh | u) : sl;
+                    if constexpr (j % kF3Check == kF3Check - 1)
                         while (qn >= 64u) drain(64u);
                 });
+                s = sl >> 16;
+                prev = sl & 0xffffu;
 #pragma unroll
                 for (int x = 0; x < D; x++) St[x] = Sp[B - D + x];
                 Sp[B - 1] = h[B - 1];
@@ -1275,7 +1310,7 @@ __global__ __launch_bounds__(kSkmBlock) __attribute__((amdgpu_waves_per_eu(KC_F3
                         }
                         prev = u;
                     }
-                    if constexpr ((j & 3) == 3)
+                    if constexpr (j % kF3Check == kF3Check - 1)
                         while (qn >= 64u) drain(64u);
                 });
 #pragma unroll
@@ -2157,7 +2192,6 @@ __global__ __launch_bounds__(kBucketBlock) void count_skm_k(SkmBucketArgs a, con
     u32* labort = misc + 21;
     u32* lnext = misc + 22;
     u32* lkscan = misc + 23;  // keys of an aborted pass scanned (abort estimate)
-    u32* wtot_l = misc + 24;
     const int tid = threadIdx.x;
     const int lane = (int)lane_id();
     const u64 lane_lt = lanemask_lt();
