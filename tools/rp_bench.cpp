@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "kc_device.h"
@@ -68,7 +69,48 @@ int main(int argc, char** argv) {
         q = c ? c + 1 : nullptr;
     }
     const uint64_t ob = n + padn;  // output stride (records)
-    if (layout == -3) {
+    // -4: the output in three places, timed as pairs (0, r): r = 0 a plain
+    // allocation, 1 mapped from RP_CHUNK_MB physical chunks in creation order
+    // (virtual memory API), 2 the same chunks mapped in a shuffled order
+    std::vector<uint64_t*> outs;
+    if (layout == -4) {
+        CK(hipMalloc(&a, n * 8 * NW));
+        uint64_t* p0;
+        CK(hipMalloc(&p0, ob * 8 * NW));
+        outs.push_back(p0);
+        hipMemAllocationProp prop = {};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = 0;
+        size_t gran = 0;
+        CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+        const size_t chunk = std::max<size_t>(gran, (size_t)(getenv("RP_CHUNK_MB") ? atoi(getenv("RP_CHUNK_MB")) : 64) << 20);
+        const size_t bytes = ((ob * 8 * NW + chunk - 1) / chunk) * chunk;
+        const size_t nch = bytes / chunk;
+        fprintf(stderr, "rp_bench: granularity %zu, chunk %zu, %zu chunks per mapped buffer\n", gran, chunk, nch);
+        for (int v = 0; v < 2; v++) {
+            void* va = nullptr;
+            CK(hipMemAddressReserve(&va, bytes, 0, nullptr, 0));
+            std::vector<hipMemGenericAllocationHandle_t> hs(nch);
+            for (size_t i = 0; i < nch; i++) CK(hipMemCreate(&hs[i], chunk, &prop, 0));
+            std::vector<size_t> perm(nch);
+            for (size_t i = 0; i < nch; i++) perm[i] = i;
+            if (v == 1) {
+                uint64_t x = 88172645463325252ull;
+                for (size_t i = nch - 1; i > 0; i--) {
+                    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                    std::swap(perm[i], perm[x % (i + 1)]);
+                }
+            }
+            for (size_t i = 0; i < nch; i++) CK(hipMemMap((char*)va + i * chunk, chunk, 0, hs[perm[i]], 0));
+            hipMemAccessDesc acc = {};
+            acc.location = prop.location;
+            acc.flags = hipMemAccessFlagsProtReadWrite;
+            CK(hipMemSetAccess(va, bytes, &acc, 1));
+            outs.push_back((uint64_t*)va);
+        }
+        b = outs[0];
+    } else if (layout == -3) {
         CK(hipMalloc(&a, nreg * n * 8 * NW));
         CK(hipMalloc(&b, nreg * ob * 8 * NW));
     } else if (layout == -2) {  // physically contiguous allocations
@@ -126,10 +168,14 @@ int main(int argc, char** argv) {
         }
     }
     const int sweeps = getenv("RP_SWEEPS") ? atoi(getenv("RP_SWEEPS")) : 1;  // repeat the pairs: stable?
-    for (int pk = 0; pk < (nreg > 1 ? npairs * sweeps : 1); pk++) {
+    if (layout == -4 && !getenv("RP_PAIRS")) {
+        npairs = 3;
+        for (int r = 0; r < 3; r++) pairs[r][0] = 0, pairs[r][1] = r;
+    }
+    for (int pk = 0; pk < ((nreg > 1 || layout == -4) ? npairs * sweeps : 1); pk++) {
     const int pi = pk % npairs;
-    uint64_t* ai = a + (uint64_t)pairs[pi][0] * n * NW;
-    uint64_t* bi = b + (uint64_t)pairs[pi][1] * ob * NW;
+    uint64_t* ai = a + (layout == -4 ? 0 : (uint64_t)pairs[pi][0] * n * NW);
+    uint64_t* bi = layout == -4 ? outs[pairs[pi][1]] : b + (uint64_t)pairs[pi][1] * ob * NW;
     float best = 1e30f, tot = 0.f;
     for (int r = 0; r < reps + 1; r++) {
         CK(hipEventRecord(e0, s));
