@@ -9,7 +9,8 @@ N=${N:-592344064}
 for ch in ${CHUNKS:-64 2}; do
   for p in 1 2 3; do
     chk=1; [ $p -eq 1 ] && [ $ch = "${CHUNKS%% *}" ] && chk=
-    RP_CHUNK_MB=$ch RP_SWEEPS=2 ${chk:+RP_NOCHECK=1} timeout -k 10 300 ./tools/rp_bench $N 2 3 1 48 -4 > $O/c$ch.p$p.txt 2> $O/c$ch.p$p.err
+    ( [ -n "$chk" ] && export RP_NOCHECK=1
+      RP_CHUNK_MB=$ch RP_SWEEPS=2 timeout -k 10 300 ./tools/rp_bench $N 2 3 1 48 -4 > $O/c$ch.p$p.txt 2> $O/c$ch.p$p.err )
     rc=$?; echo "chunk $ch MB process $p rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/c$ch.p$p.err; exit $rc; }
     python3 -c "
 import json
