@@ -4517,6 +4517,7 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
     bool vhole = false;
     u64 vwin = 0;
     const FastDivU divg((u32)G);
+    const FastDivU divg1((u32)(G > 1 ? G - 1 : 1));  // fixed L: the full groups of a read
     u64 err = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (n == 0 || base[0] != '@') err |= ERR_FQ_NOT_AT;
@@ -4790,15 +4791,12 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
             // r G + g = item past that row's first word (no per-item 64-bit math)
             u32* const hcodes = codes + (rowoff + rec0) * (u64)G;
             unsigned short* const hinval = inval + (rowoff + rec0) * (u64)G;
-#pragma unroll 1
-            for (u32 item = (u32)lane; item < nrec * (u32)G; item += 64) {
-                const u32 r = divg.div(item);
-                const int g = (int)(item - r * (u32)G);
+            // group g of listed record r (item r G + g)
+            auto encode = [&](u32 r, int g, int nb0, bool lastg) {
+                const u32 item = r * (u32)G + (u32)g;
                 const int s0 = (int)lst[r] + 16 * g;  // staged offset of the group's first base
-                const int nb0 = min(16, L - 16 * g);  // slot bases in the group
                 const int lr = VAR ? (int)lenl[r] : L;
                 const int nb = VAR ? max(0, min(nb0, lr - 16 * g)) : nb0;  // of them, bases of the read
-                const bool lastg = g == G - 1;
                 const int need = nb + ((lastg && !VAR) ? 1 : 0);  // the group (+ the byte after the read)
                 const int sh = s0 & 3;
                 u32 d[5];
@@ -4841,6 +4839,25 @@ __global__ __launch_bounds__(kFqEncBlock) __attribute__((amdgpu_waves_per_eu(KC_
                 hcodes[item] = cw;
                 hinval[item] = (unsigned short)bad;
                 if (SP && g == 0) rlen[rowoff + rec0 + r] = (unsigned short)L;
+            };
+            if constexpr (!VAR) {
+                // fixed L: the groups before a read's last hold 16 bases each
+                // (their loop has no byte masks and no end-of-read test), the
+                // last group L - 16 (G - 1) and the byte after the read
+#pragma unroll 1
+                for (u32 item = (u32)lane; item < nrec * (u32)(G - 1); item += 64) {
+                    const u32 r = divg1.div(item);
+                    encode(r, (int)(item - r * (u32)(G - 1)), 16, false);
+                }
+#pragma unroll 1
+                for (u32 r = (u32)lane; r < nrec; r += 64) encode(r, G - 1, L - 16 * (G - 1), true);
+            } else {
+#pragma unroll 1
+                for (u32 item = (u32)lane; item < nrec * (u32)G; item += 64) {
+                    const u32 r = divg.div(item);
+                    const int g = (int)(item - r * (u32)G);
+                    encode(r, g, min(16, L - 16 * g), g == G - 1);
+                }
             }
             if constexpr (SP) {
                 if (hn == 0) {
