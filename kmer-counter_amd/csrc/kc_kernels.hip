@@ -4416,22 +4416,17 @@ __device__ __forceinline__ u32 nl_nib(u32 w) {
 }
 
 // '\n' bytes of 16 bytes (4 dwords, first byte lowest) as a 16-bit mask, bit
-// i = byte i: the per-byte flags (0x80 per byte) of the 4 dwords are merged as
-// y = z0 >> 7 | z1 >> 6 | z2 >> 5 | z3 >> 4 (byte b, bit q = byte 4q + b),
-// packed to 16 bits and the 4 x 4 bit block transposed
+// i = byte i: the per-byte flags (0x80 per byte) of each dword are weighted
+// by v_dot4_u32_u8 (bytes 1 2 4 8 for dwords 0 and 2, 16 32 64 128 for 1 and
+// 3, two dwords accumulated per half), so each half is its 8-bit mask times 128
 __device__ __forceinline__ u32 nl_mask16w(u32 w0, u32 w1, u32 w2, u32 w3) {
     auto z = [](u32 w) {
         const u32 t = w ^ 0x0a0a0a0au;
         return ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
     };
-    const u32 y = (z(w0) >> 7) | (z(w1) >> 6) | (z(w2) >> 5) | (z(w3) >> 4);
-    const u32 v1 = (y | (y >> 4)) & 0x00ff00ffu;
-    u32 p = (v1 & 0xffu) | ((v1 >> 8) & 0xff00u);
-    u32 t = (p ^ (p >> 3)) & 0x0a0au;
-    p ^= t ^ (t << 3);
-    t = (p ^ (p >> 6)) & 0x00ccu;
-    p ^= t ^ (t << 6);
-    return p & 0xffffu;
+    const u32 lo = __builtin_amdgcn_udot4(z(w1), 0x80402010u, __builtin_amdgcn_udot4(z(w0), 0x08040201u, 0u, false), false);
+    const u32 hi = __builtin_amdgcn_udot4(z(w3), 0x80402010u, __builtin_amdgcn_udot4(z(w2), 0x08040201u, 0u, false), false);
+    return (lo >> 7) | (hi << 1);
 }
 
 // newline bytes among the first nv bytes of a dword (any)
